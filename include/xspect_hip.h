@@ -1,0 +1,159 @@
+/*
+ * xspect_hip.h — C ABI of libxspect_hip.so, the MI355X (gfx950) k-mer x filter
+ * probe engine behind the XspecT model classes.
+ *
+ * The reference crosses a Python<->native FFI once per READ (pybind11 into
+ * cobs_index, PyO3 into rbloom with a Python callback per k-mer).  This ABI
+ * replaces those crossings with one call per BATCH of reads.  Each entry point
+ * names the reference interface it replaces (paths relative to the reference
+ * repository):
+ *
+ *   xs_bank_open            cobs_index.Search(path, True/False)
+ *                             src/xspect/models/probabilistic_filter_model.py:389
+ *                             src/xspect/models/probabilistic_filter_svm_model.py:313
+ *                             src/xspect/models/probabilistic_filter_mlst_model.py:188
+ *                           rbloom.Bloom.load(path, hash_func=xxh3_64_intdigest)
+ *                             src/xspect/models/probabilistic_single_filter_model.py:155-158
+ *   xs_query                Search.search(str(seq), step=step), batched over reads
+ *                             probabilistic_filter_model.py:227 (+ _count_kmers :462)
+ *                             probabilistic_filter_mlst_model.py:242,274-276
+ *                           sum(1 for kmer in _generate_kmers(seq, step) if kmer in bf)
+ *                             probabilistic_single_filter_model.py:122-124
+ *   xs_query_totals         ModelResult.get_total_hits() + sum(num_kmers)
+ *                             src/xspect/models/result.py:57-72,76-90 (device-side)
+ *   xs_query_device         same as xs_query on device-resident buffers/stream
+ *   xs_bank_create_cobs,    cobs_index.ClassicIndexParameters/classic_construct_list
+ *   xs_bank_build,            probabilistic_filter_model.py:186-192
+ *   xs_bank_save            CompactIndexParameters/compact_construct_list
+ *                             probabilistic_filter_mlst_model.py:132-141
+ *   xs_bank_create_bloom    rbloom.Bloom(n, fpr, hash_func), .add(kmer), .save(path)
+ *                             probabilistic_single_filter_model.py:88-96
+ *
+ * Conventions: every int-returning call returns XS_OK (0) or a negative
+ * XS_ERR_* code; xs_last_error() returns a thread-local message for the last
+ * failure on the calling thread.  Host buffers are borrowed for the duration of
+ * the call only.  A bank handle owns its device memory and one HIP stream;
+ * calls on one handle are serialised by an internal mutex, distinct handles are
+ * independent.  No callbacks into the caller.
+ */
+#ifndef XSPECT_HIP_H
+#define XSPECT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define XS_OK 0
+#define XS_ERR_ARG (-1)
+#define XS_ERR_IO (-2)
+#define XS_ERR_FORMAT (-3)
+#define XS_ERR_HIP (-4)
+#define XS_ERR_UNSUPPORTED (-5)
+
+#define XS_BANK_COBS_CLASSIC 0
+#define XS_BANK_COBS_COMPACT 1
+#define XS_BANK_RBLOOM 2
+
+typedef struct xs_bank xs_bank;
+
+typedef struct xs_bank_info_t {
+    int32_t kind;             /* XS_BANK_* */
+    int32_t device;           /* HIP device ordinal the bank is resident on */
+    uint32_t term_size;       /* k */
+    uint32_t num_hashes;      /* COBS h, or rbloom K */
+    uint32_t canonicalize;    /* 1: canonical k-mers (always 1 for XspecT banks) */
+    uint32_t reserved;
+    uint64_t num_docs;        /* D (1 for rbloom) */
+    uint64_t num_groups;      /* COBS doc groups (1 for classic) */
+    uint64_t page_size;       /* bytes per row per group in the file layout */
+    uint64_t signature_rows;  /* sum of signature sizes over groups */
+    uint64_t bloom_bits;      /* rbloom bit count (0 for COBS) */
+    uint64_t device_bytes;    /* device bytes held by the bank image */
+    uint64_t device_row_pitch;/* padded device bytes per row per group */
+} xs_bank_info_t;
+
+int xs_version(void);
+const char* xs_last_error(void);
+int xs_device_count(int* count);
+
+/* Open a bank file and make it resident on `device`.  kind = XS_BANK_*. */
+int xs_bank_open(const char* path, int kind, int device, xs_bank** out);
+
+/* Create an empty COBS bank (classic: num_groups = 1 and page_size =
+ * ceil(num_docs/8); compact: num_groups groups of 8*page_size docs each, the
+ * last one partial).  sig[g] = signature size of group g.  doc_names may be
+ * NULL (names "0", "1", ...). */
+int xs_bank_create_cobs(int device, int kind, uint32_t term_size, uint32_t num_hashes,
+                        uint64_t num_docs, uint64_t page_size, uint64_t num_groups,
+                        const uint64_t* sig, const char* const* doc_names, xs_bank** out);
+
+/* Create an empty rbloom bank of nbytes bytes and nhash index functions. */
+int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32_t nhash,
+                         xs_bank** out);
+
+/* Insert every k-mer (step 1) of n_rec host records; record r belongs to doc
+ * rec_doc[r] (ignored for rbloom; may be NULL there). */
+int xs_bank_build(xs_bank* bank, const char* seqs, const uint64_t* offsets,
+                  const uint32_t* rec_doc, uint64_t n_rec);
+/* Same with device-resident buffers, enqueued on `stream` (NULL = bank stream). */
+int xs_bank_build_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes,
+                         const uint64_t* d_offsets, const uint32_t* d_rec_doc, uint64_t n_rec,
+                         void* stream);
+
+int xs_bank_save(xs_bank* bank, const char* path);
+/* Copy the bank back in FILE layout (rows of page_size bytes, groups in order;
+ * rbloom: the raw bit bytes). nbytes must equal the file payload size. */
+int xs_bank_download(xs_bank* bank, void* host, uint64_t nbytes);
+/* Replace the bank image from a FILE-layout payload (the inverse of download). */
+int xs_bank_upload(xs_bank* bank, const void* host, uint64_t nbytes);
+
+/* rbloom files carry no k-mer length (XspecT keeps it in the model JSON,
+ * probabilistic_single_filter_model.py:143-151); set it after xs_bank_open. */
+int xs_bank_set_term_size(xs_bank* bank, uint32_t term_size);
+
+int xs_bank_info(const xs_bank* bank, xs_bank_info_t* out);
+const char* xs_bank_doc_name(const xs_bank* bank, uint64_t i);
+
+/* Probe n reads (host buffers): read r = seqs[offsets[r] .. offsets[r+1]).
+ * hits_out: n x D uint32 (row-major, may be NULL), num_kmers_out: n (may be
+ * NULL).  k-mers are taken at positions i*step, i < ceil((len-k+1)/step);
+ * reads shorter than k contribute no k-mers. */
+int xs_query(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+             uint32_t* hits_out, uint64_t* num_kmers_out);
+
+/* totals_out[d] = sum over reads of hits[r][d] (D entries, uint64),
+ * *total_kmers_out = sum of num_kmers.  No per-read matrix is materialised. */
+int xs_query_totals(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n,
+                    uint32_t step, uint64_t* totals_out, uint64_t* total_kmers_out);
+
+/* Device-resident variant, asynchronous on `stream` (NULL = bank stream).
+ * d_seqs holds seq_bytes bytes; d_offsets n+1 uint64.  Any of d_hits (n x D
+ * uint32), d_num_kmers (n uint64) and d_totals (D+1 uint64: per-doc totals then
+ * the k-mer total) may be NULL.  The bank must live on the current device. */
+int xs_query_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes,
+                    const uint64_t* d_offsets, uint64_t n, uint32_t step, uint32_t* d_hits,
+                    uint64_t* d_num_kmers, uint64_t* d_totals, void* stream);
+
+/* MLST chunk scoring (probabilistic_filter_mlst_model.py:237-256): for chunk
+ * hit rows hits[c][d] whose owner is seq_of_chunk[c] (non-decreasing), sum
+ * hits[c][d] into scores[seq][d] only where hits[c][d] > threshold
+ * (get_cobs_result :378).  Host buffers; computed on the device. */
+int xs_mlst_sum(xs_bank* bank, const uint32_t* hits, const uint32_t* seq_of_chunk,
+                uint64_t n_chunks, uint64_t n_seqs, uint32_t threshold, uint64_t* scores);
+
+/* Record HIP events around the probe kernel of every query on this handle. */
+int xs_bank_set_profiling(xs_bank* bank, int on);
+/* Duration of the probe kernel of the last profiled query, milliseconds. */
+int xs_bank_last_probe_ms(xs_bank* bank, float* ms);
+/* Count, summed and maximum duration of every probe kernel launched since
+ * profiling was enabled or the last call of this function (then resets). */
+int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float* max_ms);
+
+void xs_bank_close(xs_bank* bank);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* XSPECT_HIP_H */

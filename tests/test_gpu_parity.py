@@ -1,0 +1,210 @@
+"""Parity of the HIP probe path with the CPU oracle, through the C ABI (GPU).
+
+Bit-exact for every integer output: hit matrices, k-mer counts, totals and
+the bank images built on the device.  Inputs are seeded; edge cases follow
+what the reference's path meets: reads of length <= k (no k-mers), exactly
+k+1, non-ACGT bytes (N, IUPAC, lower case), long records split into several
+work units, sparse sampling steps, empty reads, D spanning 1..1000 docs.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def xs():
+    from xspect_amd import bank as bank_mod
+    from xspect_amd import _lib
+    assert _lib.device_count() >= 1, "no HIP device visible"
+    return bank_mod
+
+
+def _reads(rng, n, k, alphabet="ACGT", min_len=None, max_len=300):
+    lo = min_len if min_len is not None else max(0, k - 2)
+    alph = np.frombuffer(alphabet.encode(), dtype=np.uint8)
+    return [alph[rng.integers(0, alph.size, int(L))].tobytes() for L in rng.integers(lo, max_len, n)]
+
+
+def _docs(rng, D, k, per_doc=2, max_len=2000):
+    seqs, ids = [], []
+    for d in range(D):
+        for _ in range(per_doc):
+            L = int(rng.integers(k, max_len))
+            seqs.append(np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, L)].tobytes())
+            ids.append(d)
+    return seqs, ids
+
+
+def _pair(xs, oracle_mod, D, k, h, sig, page=None, seed=0, per_doc=2):
+    """Oracle bank and device bank holding the same image."""
+    rng = np.random.default_rng(seed)
+    seqs, ids = _docs(rng, D, k, per_doc)
+    compact = page is not None
+    P = page if compact else (D + 7) // 8
+    ob = oracle_mod.CobsBank.empty(sig, P, D, h, k)
+    ob.build(seqs, ids)
+    gb = xs.Bank.create_cobs(k, h, sig, D, [f"doc{i}" for i in range(D)],
+                             page_size=P if compact else None, compact=compact)
+    gb.upload(ob.rows)
+    return ob, gb, seqs, ids
+
+
+CLASSIC_CASES = [
+    # D, k, h, sig
+    (1, 21, 7, [997]),
+    (3, 21, 7, [5000]),
+    (8, 5, 2, [301]),
+    (100, 21, 7, [40_000]),
+    (129, 31, 1, [20_011]),
+    (300, 16, 3, [7_919]),
+    (1000, 21, 7, [3_001]),
+    (13, 32, 4, [2_048]),
+    (40, 17, 9, [1_231]),
+]
+
+
+@pytest.mark.parametrize("D,k,h,sig", CLASSIC_CASES)
+def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D * 31 + k)
+    rng = np.random.default_rng(D + k + h)
+    reads = _reads(rng, 300, k)
+    reads += [s[: int(rng.integers(k, len(s) + 1))] for s in seqs[:40]]      # true positives
+    reads += _reads(rng, 40, k, alphabet="ACGTNacgtnRYKM")                   # non-ACGT
+    reads += [b"", b"A" * (k - 1) if k > 1 else b"", b"C" * k, b"G" * (k + 1)]
+    reads += [seqs[0] * 3]                                                   # multi-unit read
+    for step in (1, 2, 7):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n), f"num_kmers differ (step {step})"
+        assert np.array_equal(got_h, want_h), f"hits differ (step {step})"
+        tot, nk = gb.query_totals(reads, step=step)
+        assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64))
+        assert nk == int(want_n.sum())
+    gb.close()
+
+
+@pytest.mark.parametrize("D,k,h,page,G", [(600, 31, 1, 64, 2), (20, 21, 7, 1, 3), (1500, 21, 2, 64, 3),
+                                          (70, 25, 3, 3, 3)])
+def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
+    assert (G - 1) * 8 * page < D <= G * 8 * page
+    rng = np.random.default_rng(D)
+    sig = [int(x) for x in rng.integers(500, 6000, G)]
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, page=page, seed=D, per_doc=1)
+    reads = _reads(rng, 200, k) + [s[:300] for s in seqs[:50]] + _reads(rng, 20, k, "ACGTN")
+    for step in (1, 3):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h, want_h)
+    gb.close()
+
+
+@pytest.mark.parametrize("D,k,h,page", [(5, 21, 7, None), (100, 21, 7, None), (37, 31, 1, 2), (12, 32, 3, None)])
+def test_device_build_matches_oracle_build(xs, oracle_mod, D, k, h, page):
+    rng = np.random.default_rng(7 * D + k)
+    seqs, ids = _docs(rng, D, k, per_doc=3)
+    seqs += _reads(rng, 5, k, "ACGTNacgtRY")
+    ids += [int(rng.integers(0, D)) for _ in range(5)]
+    compact = page is not None
+    P = page if compact else (D + 7) // 8
+    G = 1 if not compact else (D + 8 * P - 1) // (8 * P)
+    sig = [int(x) for x in rng.integers(300, 5000, G)]
+    ob = oracle_mod.CobsBank.empty(sig, P, D, h, k)
+    ob.build(seqs, ids)
+    gb = xs.Bank.create_cobs(k, h, sig, D, page_size=P if compact else None, compact=compact)
+    gb.build(seqs, ids)
+    assert np.array_equal(gb.download(), ob.rows)
+    gb.close()
+
+
+def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 10, 21, 7, [4099], seed=3)
+    path = tmp_path / "m" / "index.cobs_classic"
+    gb.save(path)
+    gb2 = xs.Bank.open(path, xs.XS_BANK_COBS_CLASSIC)
+    assert gb2.doc_names == [f"doc{i}" for i in range(10)]
+    assert np.array_equal(gb2.download(), ob.rows)
+    reads = [s[:150] for s in seqs]
+    assert np.array_equal(gb2.query(reads)[0], ob.query(reads)[0])
+    gb.close()
+    gb2.close()
+
+
+@pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
+def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, k):
+    rng = np.random.default_rng(k)
+    genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
+    n_items = sum(len(s) for s in genome) - k + 1
+    nbytes, K = oracle_mod.BloomFilter.params(n_items, 0.01)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.build(genome)
+    assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
+    reads = _reads(rng, 300, k, alphabet="ACGTacgtNRY") + [g[:500] for g in genome] + [genome[0]]
+    for step in (1, 4):
+        want_h, want_n = bf.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h[:, 0], want_h)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+    gb.close()
+
+
+def test_bloom_file_roundtrip(xs, oracle_mod, tmp_path):
+    bits = np.random.default_rng(1).integers(0, 256, 4097, dtype=np.uint8)
+    gb = xs.Bank.create_bloom(21, bits.size, 7)
+    gb.upload(bits)
+    gb.save(tmp_path / "filter.bloom")
+    raw = (tmp_path / "filter.bloom").read_bytes()
+    assert int.from_bytes(raw[:8], "little") == 7 and raw[8:] == bits.tobytes()
+    gb2 = xs.Bank.open(tmp_path / "filter.bloom", xs.XS_BANK_RBLOOM, term_size=21)
+    assert np.array_equal(gb2.download(), bits)
+    bf = oracle_mod.BloomFilter(bits, 7, 21)
+    reads = _reads(np.random.default_rng(2), 100, 21)
+    assert np.array_equal(gb2.query(reads)[0][:, 0], bf.query(reads)[0])
+    gb.close()
+    gb2.close()
+
+
+def test_device_api_with_torch_stream(xs, oracle_mod):
+    torch = pytest.importorskip("torch")
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=9)
+    rng = np.random.default_rng(4)
+    reads = _reads(rng, 2000, 21, min_len=150, max_len=151)
+    buf = np.frombuffer(b"".join(reads), dtype=np.uint8)
+    offs = np.arange(len(reads) + 1, dtype=np.uint64) * 150
+    dev = torch.device("cuda", 0)
+    d_seqs = torch.from_numpy(buf.copy()).to(dev)
+    d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_hits = torch.empty((len(reads), 100), dtype=torch.int32, device=dev)
+    d_nk = torch.empty(len(reads), dtype=torch.int64, device=dev)
+    d_tot = torch.empty(101, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream()
+    gb.query_device(d_seqs, buf.size, d_offs, len(reads), 1, d_hits, d_nk, d_tot, stream=s.cuda_stream)
+    torch.cuda.synchronize()
+    want_h, want_n = ob.query(reads)
+    assert np.array_equal(d_hits.cpu().numpy().view(np.uint32), want_h)
+    assert np.array_equal(d_nk.cpu().numpy().view(np.uint64), want_n)
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert np.array_equal(tot[:100], want_h.sum(axis=0, dtype=np.uint64))
+    assert int(tot[100]) == int(want_n.sum())
+    gb.close()
+
+
+def test_mlst_sum_matches_numpy(xs):
+    rng = np.random.default_rng(0)
+    gb = xs.Bank.create_cobs(21, 1, [101], 50)
+    hits = rng.integers(0, 120, (37, 50)).astype(np.uint32)
+    owner = np.sort(rng.integers(0, 4, 37)).astype(np.uint32)
+    got = gb.mlst_sum(hits, owner, 4, 50)
+    want = np.zeros((4, 50), dtype=np.uint64)
+    for c in range(37):
+        m = hits[c] > 50
+        want[owner[c], m] += hits[c, m]
+    assert np.array_equal(got, want)
+    gb.close()

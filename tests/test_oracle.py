@@ -1,0 +1,140 @@
+"""Pin the CPU oracle before trusting it (CPU only).
+
+* hash layer vs python-xxhash golden vectors (tests/golden/xxh_vectors.json)
+* the C restatement vs the independent pure-Python restatement
+* the reference tests' own known answers (tests/golden/reference_known_answers.json)
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+
+
+def test_xxh_golden_vectors(oracle_mod, golden):
+    g = golden("xxh_vectors.json")
+    assert g["cases"], "empty golden file"
+    for case in g["cases"]:
+        data = bytes.fromhex(case["hex"])
+        for seed, want in enumerate(case["xxh64"]):
+            assert oracle_mod.xxh64(data, seed) == int(want), (case["hex"], seed)
+        if len(data) <= 240:
+            assert oracle_mod.xxh3_64(data) == int(case["xxh3_64"]), case["hex"]
+
+
+def test_xxh_matches_python_xxhash_random(oracle_mod):
+    xxhash = pytest.importorskip("xxhash")
+    rng = np.random.default_rng(3)
+    for n in list(range(0, 70)) + [100, 128, 129, 240]:
+        b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        s = int(rng.integers(0, 2**63))
+        assert oracle_mod.xxh64(b, s) == xxhash.xxh64_intdigest(b, seed=s)
+        assert oracle_mod.xxh3_64(b) == xxhash.xxh3_64_intdigest(b)
+
+
+@pytest.mark.parametrize("k", [1, 2, 5, 20, 21, 31, 32, 33])
+def test_canonical_c_vs_python(oracle_mod, k):
+    rng = np.random.default_rng(k)
+    for t in range(300):
+        alph = "ACGT" if t % 3 else "ACGTNacgtnRYKMSWBDHVXU-"
+        s = "".join(rng.choice(list(alph), k))
+        assert oracle_mod.canonical_cobs(s.encode()).decode() == oracle_mod.canonical_cobs_py(s)
+        assert oracle_mod.canonical_bio(s.encode()).decode() == oracle_mod.canonical_bio_py(s)
+
+
+def test_canonical_semantics(oracle_mod):
+    # reverse complement of AAAC is GTTT; min is AAAC
+    assert oracle_mod.canonical_cobs_py("GTTT") == "AAAC"
+    assert oracle_mod.canonical_bio_py("GTTT") == "AAAC"
+    # case preserved on the genus path, normalised on the COBS path
+    assert oracle_mod.canonical_bio_py("gttt") == "aaac"
+    assert oracle_mod.canonical_cobs_py("gttt") == "AAAC"
+    assert oracle_mod.canonical_cobs_py("ANNT") == "ANNT"
+
+
+def test_signature_size_formula(oracle_mod):
+    for n, h, f in [(4_000_000, 7, 0.01), (500, 1, 0.001), (1, 7, 0.01), (123457, 3, 0.05)]:
+        assert oracle_mod.signature_size(n, h, f) == oracle_mod.signature_size_py(n, h, f)
+    # ~9.59 rows per term at (h=7, fpr=0.01), ~1000 at (h=1, fpr=0.001)
+    assert abs(oracle_mod.signature_size(10**6, 7, 0.01) / 1e6 - 9.594) < 0.01
+    assert abs(oracle_mod.signature_size(10**6, 1, 0.001) / 1e6 - 999.5) < 0.5
+
+
+def test_known_answer_kmer_counts(oracle_mod, golden):
+    ka = golden("reference_known_answers.json")["salmonella_80bp"]
+    assert oracle_mod.num_kmers(len(ka["seq"]), ka["k"], 1) == ka["num_kmers"]
+    for step, want in ka["hits_self_by_step"].items():
+        assert oracle_mod.num_kmers(len(ka["seq"]), ka["k"], int(step)) == want
+        assert math.ceil((len(ka["seq"]) - ka["k"] + 1) / int(step)) == want
+
+
+def test_known_answer_splitter(oracle_mod, golden):
+    ka = golden("reference_known_answers.json")["splitter"]
+    parts = oracle_mod.sequence_splitter(ka["seq"], ka["allele_len"], ka["k"])
+    assert len(parts) == ka["num_parts"]
+    # every k-mer of the input is in exactly one chunk
+    k = ka["k"]
+    got = [p[i:i + k] for p in parts for i in range(len(p) - k + 1)]
+    want = [ka["seq"][i:i + k] for i in range(len(ka["seq"]) - k + 1)]
+    assert got == want
+
+
+def _small_bank(oracle_mod, D, k, h, seqs_per_doc=2, seed=0, compact_page=None):
+    rng = np.random.default_rng(seed)
+    docs = []
+    for d in range(D):
+        for _ in range(seqs_per_doc):
+            L = int(rng.integers(k, 400))
+            docs.append(("".join(rng.choice(list("ACGT"), L)), d))
+    if compact_page is None:
+        page, G = (D + 7) // 8, 1
+    else:
+        page, G = compact_page, (D + 8 * compact_page - 1) // (8 * compact_page)
+    sig = [int(rng.integers(50, 3000)) for _ in range(G)]
+    bank = oracle_mod.CobsBank.empty(sig, page, D, h, k)
+    bank.build([s for s, _ in docs], [d for _, d in docs])
+    return bank, docs
+
+
+@pytest.mark.parametrize("D,k,h,page", [(3, 21, 7, None), (9, 5, 2, None), (20, 31, 1, 1), (17, 16, 3, 1)])
+def test_cobs_query_c_vs_python(oracle_mod, D, k, h, page):
+    bank, docs = _small_bank(oracle_mod, D, k, h, compact_page=page)
+    rng = np.random.default_rng(11)
+    queries = [s[: int(rng.integers(k, len(s) + 1))] for s, _ in docs[:6]]
+    queries += ["".join(rng.choice(list("ACGTN"), int(rng.integers(k, 200)))) for _ in range(4)]
+    queries += ["ACG", ""]  # shorter than k: zero k-mers
+    for step in (1, 2, 5):
+        hits_c, nk = bank.query(queries, step=step)
+        hits_py = bank.query_py(queries, step=step)
+        assert np.array_equal(hits_c, hits_py)
+        assert [int(x) for x in nk] == [oracle_mod.num_kmers(len(q), k, step) for q in queries]
+
+
+def test_cobs_self_hits_are_full(oracle_mod):
+    """A document's own sequence hits its doc at every position (no false negatives)."""
+    bank, docs = _small_bank(oracle_mod, 5, 21, 7, seqs_per_doc=1)
+    hits, nk = bank.query([s for s, _ in docs])
+    for i, (_, d) in enumerate(docs):
+        assert hits[i, d] == nk[i]
+
+
+def test_bloom_c_vs_python(oracle_mod):
+    rng = np.random.default_rng(5)
+    seqs = ["".join(rng.choice(list("ACGTacgtN"), int(rng.integers(21, 300)))) for _ in range(8)]
+    nbytes, K = oracle_mod.BloomFilter.params(sum(len(s) for s in seqs), 0.01)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, 21)
+    bf.build(seqs)
+    queries = seqs[:4] + ["".join(rng.choice(list("ACGT"), 120)) for _ in range(4)]
+    hits, nk = bf.query(queries)
+    for q, hv in zip(queries, hits):
+        want = sum(bf.contains_py(q[i:i + 21]) for i in range(len(q) - 20))
+        assert int(hv) == want
+    # inserted k-mers are members
+    assert all(int(hits[i]) == int(nk[i]) for i in range(4))
+
+
+def test_bloom_params_restated(oracle_mod):
+    nbytes, K = oracle_mod.BloomFilter.params(1000, 0.01)
+    assert K == 7
+    assert nbytes == (int(-1000 * math.log(0.01) / math.log(2) ** 2) + 7) // 8

@@ -1,0 +1,124 @@
+"""ctypes binding of libxspect_hip.so (include/xspect_hip.h).
+
+The library is built in-tree (``xspect_amd/libxspect_hip.so``) by
+``xspect_amd.build.build_library()``.  There is no CPU fallback: if the shared
+object is missing or cannot be loaded, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+PKG = Path(__file__).resolve().parent
+SO_PATH = PKG / "libxspect_hip.so"
+
+XS_OK = 0
+XS_ERR_ARG = -1
+XS_ERR_IO = -2
+XS_ERR_FORMAT = -3
+XS_ERR_HIP = -4
+XS_ERR_UNSUPPORTED = -5
+
+XS_BANK_COBS_CLASSIC = 0
+XS_BANK_COBS_COMPACT = 1
+XS_BANK_RBLOOM = 2
+
+
+class XsError(RuntimeError):
+    """A failed libxspect_hip call (message from xs_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[xs {code}] {msg}")
+        self.code = code
+
+
+class BankInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", ctypes.c_int32),
+        ("device", ctypes.c_int32),
+        ("term_size", ctypes.c_uint32),
+        ("num_hashes", ctypes.c_uint32),
+        ("canonicalize", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("num_docs", ctypes.c_uint64),
+        ("num_groups", ctypes.c_uint64),
+        ("page_size", ctypes.c_uint64),
+        ("signature_rows", ctypes.c_uint64),
+        ("bloom_bits", ctypes.c_uint64),
+        ("device_bytes", ctypes.c_uint64),
+        ("device_row_pitch", ctypes.c_uint64),
+    ]
+
+
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+# name -> (restype, argtypes); every symbol of include/xspect_hip.h
+SIGNATURES = {
+    "xs_version": (_int, []),
+    "xs_last_error": (ctypes.c_char_p, []),
+    "xs_device_count": (_int, [ctypes.POINTER(_int)]),
+    "xs_bank_open": (_int, [ctypes.c_char_p, _int, _int, _pp]),
+    "xs_bank_create_cobs": (_int, [_int, _int, _u32, _u32, _u64, _u64, _u64, _vp, _vp, _pp]),
+    "xs_bank_create_bloom": (_int, [_int, _u32, _u64, _u32, _pp]),
+    "xs_bank_build": (_int, [_vp, _vp, _vp, _vp, _u64]),
+    "xs_bank_build_device": (_int, [_vp, _vp, _u64, _vp, _vp, _u64, _vp]),
+    "xs_bank_save": (_int, [_vp, ctypes.c_char_p]),
+    "xs_bank_download": (_int, [_vp, _vp, _u64]),
+    "xs_bank_upload": (_int, [_vp, _vp, _u64]),
+    "xs_bank_set_term_size": (_int, [_vp, _u32]),
+    "xs_bank_info": (_int, [_vp, ctypes.POINTER(BankInfo)]),
+    "xs_bank_doc_name": (ctypes.c_char_p, [_vp, _u64]),
+    "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
+    "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
+    "xs_query_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "xs_mlst_sum": (_int, [_vp, _vp, _vp, _u64, _u64, _u32, _vp]),
+    "xs_bank_set_profiling": (_int, [_vp, _int]),
+    "xs_bank_last_probe_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
+    "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_float)]),
+    "xs_bank_close": (None, [_vp]),
+}
+
+_LIB = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree shared library (raises if it is missing)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not SO_PATH.exists():
+        raise ImportError(
+            f"{SO_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the probe path has no CPU fallback)")
+    # torch (if present) must own the HIP runtime first: libamdhip64.so.7 is
+    # then shared by soname instead of loading a second copy from /opt/rocm.
+    if os.environ.get("XSPECT_AMD_NO_TORCH_PRELOAD") is None:
+        try:
+            import torch  # noqa: F401
+        except Exception:  # pragma: no cover - torch is optional for the ABI
+            pass
+    lib = ctypes.CDLL(str(SO_PATH))
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != XS_OK:
+        msg = load().xs_last_error()
+        raise XsError(rc, msg.decode() if msg else "unknown error")
+
+
+def device_count() -> int:
+    n = _int(0)
+    rc = load().xs_device_count(ctypes.byref(n))
+    return n.value if rc == XS_OK else 0

@@ -1,0 +1,253 @@
+"""Device-resident filter banks (COBS classic / compact, rbloom) behind the C ABI.
+
+A :class:`Bank` owns one ``xs_bank`` handle: the bank image lives in HBM for
+the lifetime of the object (reference: ``cobs.Search(path, True)`` at
+``src/xspect/models/probabilistic_filter_model.py:389`` keeps it in host RAM
+and is re-entered once per read).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from pathlib import Path
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (XS_BANK_COBS_CLASSIC, XS_BANK_COBS_COMPACT, XS_BANK_RBLOOM, BankInfo,
+                   check, load)
+from .packing import PackedReads, pack_sequences
+
+KIND_NAMES = {XS_BANK_COBS_CLASSIC: "cobs_classic", XS_BANK_COBS_COMPACT: "cobs_compact",
+              XS_BANK_RBLOOM: "rbloom"}
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None and a.size else 0
+
+
+def cobs_signature_size(num_terms: int, num_hashes: int, fpr: float) -> int:
+    """COBS calc_signature_size (restated): ceil(-h*n / ln(1 - fpr^(1/h)))."""
+    return int(math.ceil(-num_hashes * num_terms / math.log(1.0 - math.pow(fpr, 1.0 / num_hashes))))
+
+
+def bloom_parameters(expected_items: int, fpr: float) -> tuple[int, int]:
+    """(nbytes, K) of rbloom.Bloom(expected_items, fpr) (restated, unverified)."""
+    if expected_items <= 0 or not 0.0 < fpr < 1.0:
+        raise ValueError("expected_items must be > 0 and 0 < fpr < 1")
+    size_bits = int(-expected_items * math.log(fpr) / (math.log(2) ** 2))
+    nhash = max(1, math.ceil(size_bits / expected_items * math.log(2)))
+    return (max(size_bits, 1) + 7) // 8, nhash
+
+
+class Bank:
+    """One filter bank resident on one GPU."""
+
+    def __init__(self, handle: ctypes.c_void_p):
+        self._h = handle
+        self._names: list[str] | None = None
+
+    # ------------------------------------------------------------ creation
+    @classmethod
+    def open(cls, path: str | Path, kind: int, device: int = 0, term_size: int | None = None) -> "Bank":
+        path = Path(path)
+        if not path.exists():
+            raise FileNotFoundError(f"Index file not found at {path}")
+        h = ctypes.c_void_p()
+        check(load().xs_bank_open(str(path).encode(), kind, device, ctypes.byref(h)))
+        bank = cls(h)
+        if kind == XS_BANK_RBLOOM and term_size is not None:
+            check(load().xs_bank_set_term_size(h, term_size))
+        return bank
+
+    @classmethod
+    def create_cobs(cls, term_size: int, num_hashes: int, signature_sizes: Sequence[int],
+                    num_docs: int, doc_names: Sequence[str] | None = None,
+                    page_size: int | None = None, compact: bool = False,
+                    device: int = 0) -> "Bank":
+        if compact:
+            if page_size is None:
+                raise ValueError("compact banks need a page size")
+            kind = XS_BANK_COBS_COMPACT
+        else:
+            kind = XS_BANK_COBS_CLASSIC
+            page_size = (num_docs + 7) // 8
+        sig = np.ascontiguousarray(signature_sizes, dtype=np.uint64)
+        names_arr = None
+        keep = []
+        if doc_names is not None:
+            if len(doc_names) != num_docs:
+                raise ValueError("doc_names must have num_docs entries")
+            keep = [n.encode() for n in doc_names]
+            names_arr = (ctypes.c_char_p * num_docs)(*keep)
+        h = ctypes.c_void_p()
+        check(load().xs_bank_create_cobs(device, kind, term_size, num_hashes, num_docs, page_size,
+                                         len(sig), _ptr(sig),
+                                         ctypes.cast(names_arr, ctypes.c_void_p) if names_arr else None,
+                                         ctypes.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def create_bloom(cls, term_size: int, nbytes: int, num_hashes: int, device: int = 0) -> "Bank":
+        h = ctypes.c_void_p()
+        check(load().xs_bank_create_bloom(device, term_size, nbytes, num_hashes, ctypes.byref(h)))
+        return cls(h)
+
+    # ------------------------------------------------------------ properties
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise ValueError("bank is closed")
+        return self._h
+
+    @property
+    def info(self) -> BankInfo:
+        inf = BankInfo()
+        check(load().xs_bank_info(self.handle, ctypes.byref(inf)))
+        return inf
+
+    @property
+    def kind(self) -> int:
+        return self.info.kind
+
+    @property
+    def num_docs(self) -> int:
+        return int(self.info.num_docs)
+
+    @property
+    def term_size(self) -> int:
+        return int(self.info.term_size)
+
+    @property
+    def doc_names(self) -> list[str]:
+        if self._names is None:
+            lib = load()
+            self._names = [lib.xs_bank_doc_name(self.handle, i).decode() for i in range(self.num_docs)]
+        return self._names
+
+    def payload_bytes(self) -> int:
+        inf = self.info
+        if inf.kind == XS_BANK_RBLOOM:
+            return int(inf.bloom_bits // 8)
+        return int(inf.signature_rows * inf.page_size)
+
+    # ------------------------------------------------------------ building
+    def build(self, reads: PackedReads | Iterable, docs: Sequence[int] | np.ndarray | None = None) -> None:
+        pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
+        d = None
+        if self.kind != XS_BANK_RBLOOM:
+            if docs is None:
+                raise ValueError("COBS banks need the doc index of every record")
+            d = np.ascontiguousarray(docs, dtype=np.uint32)
+            if d.size != pr.n:
+                raise ValueError("one doc index per record")
+        check(load().xs_bank_build(self.handle, _ptr(pr.buf), _ptr(pr.offsets), _ptr(d) if d is not None else None, pr.n))
+
+    def build_device(self, seqs, seq_bytes: int, offsets, n: int, docs=None, stream: int | None = None) -> None:
+        """Device-pointer variant (torch tensors or raw ints)."""
+        check(load().xs_bank_build_device(self.handle, _dptr(seqs), seq_bytes, _dptr(offsets),
+                                          _dptr(docs) if docs is not None else None, n, stream))
+
+    def save(self, path: str | Path) -> None:
+        Path(path).parent.mkdir(parents=True, exist_ok=True)
+        check(load().xs_bank_save(self.handle, str(path).encode()))
+
+    def download(self) -> np.ndarray:
+        out = np.empty(self.payload_bytes(), dtype=np.uint8)
+        check(load().xs_bank_download(self.handle, _ptr(out), out.size))
+        return out
+
+    def upload(self, payload: np.ndarray) -> None:
+        p = np.ascontiguousarray(payload, dtype=np.uint8)
+        check(load().xs_bank_upload(self.handle, _ptr(p), p.size))
+
+    # ------------------------------------------------------------ queries
+    def query(self, reads: PackedReads | Iterable, step: int = 1, want_hits: bool = True):
+        """(hits [n, D] uint32, num_kmers [n] uint64) for host reads."""
+        pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
+        if step < 1:
+            raise ValueError("step must be >= 1")
+        cols = self.num_docs
+        hits = np.empty((pr.n, cols), dtype=np.uint32) if want_hits else None
+        nk = np.empty(pr.n, dtype=np.uint64)
+        check(load().xs_query(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
+                              _ptr(hits) if hits is not None else None, _ptr(nk)))
+        return hits, nk
+
+    def query_totals(self, reads: PackedReads | Iterable, step: int = 1):
+        """(totals [D] uint64, total k-mers) without materialising the hit matrix."""
+        pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
+        tot = np.zeros(self.num_docs, dtype=np.uint64)
+        nk = ctypes.c_uint64(0)
+        check(load().xs_query_totals(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
+                                     _ptr(tot), ctypes.byref(nk)))
+        return tot, int(nk.value)
+
+    def query_device(self, seqs, seq_bytes: int, offsets, n: int, step: int = 1, hits=None,
+                     num_kmers=None, totals=None, stream: int | None = None) -> None:
+        """Enqueue a query on device buffers (torch tensors or raw device pointers)."""
+        check(load().xs_query_device(self.handle, _dptr(seqs), seq_bytes, _dptr(offsets), n, step,
+                                     _dptr(hits), _dptr(num_kmers), _dptr(totals), stream))
+
+    def mlst_sum(self, chunk_hits: np.ndarray, seq_of_chunk: np.ndarray, n_seqs: int,
+                 threshold: int) -> np.ndarray:
+        h = np.ascontiguousarray(chunk_hits, dtype=np.uint32)
+        s = np.ascontiguousarray(seq_of_chunk, dtype=np.uint32)
+        out = np.zeros((n_seqs, self.num_docs), dtype=np.uint64)
+        check(load().xs_mlst_sum(self.handle, _ptr(h), _ptr(s), s.size, n_seqs, threshold, _ptr(out)))
+        return out
+
+    def set_profiling(self, on: bool = True) -> None:
+        check(load().xs_bank_set_profiling(self.handle, 1 if on else 0))
+
+    def last_probe_ms(self) -> float:
+        ms = ctypes.c_float(0.0)
+        check(load().xs_bank_last_probe_ms(self.handle, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def probe_stats(self) -> tuple[int, float, float]:
+        """(launches, total ms, max ms) of the probe kernel since the last call."""
+        n = ctypes.c_uint64(0)
+        tot = ctypes.c_double(0.0)
+        mx = ctypes.c_float(0.0)
+        check(load().xs_bank_probe_stats(self.handle, ctypes.byref(n), ctypes.byref(tot), ctypes.byref(mx)))
+        return int(n.value), float(tot.value), float(mx.value)
+
+    # ------------------------------------------------------------ lifetime
+    def close(self) -> None:
+        if self._h is not None:
+            load().xs_bank_close(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - interpreter shutdown order
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def _dptr(x) -> int | None:
+    """Device pointer of a torch tensor, or an int pointer, or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    ptr = getattr(x, "data_ptr", None)
+    if ptr is None:
+        raise TypeError(f"expected a device tensor or pointer, got {type(x)!r}")
+    if not getattr(x, "is_cuda", False):
+        raise ValueError("device queries need tensors on the GPU")
+    if not x.is_contiguous():
+        raise ValueError("device tensors must be contiguous")
+    return ptr()
+
+
+__all__ = ["Bank", "bloom_parameters", "cobs_signature_size", "KIND_NAMES",
+           "XS_BANK_COBS_CLASSIC", "XS_BANK_COBS_COMPACT", "XS_BANK_RBLOOM", "_lib"]

@@ -1,0 +1,845 @@
+// xs_api.cpp — host side of libxspect_hip.so: bank files, device residency,
+// per-handle workspace and the C ABI declared in include/xspect_hip.h.
+//
+// Bank file layouts (restated; COBS and rbloom are not available offline, see
+// DESIGN.md "Oracle" — parity with their real files is unpinned):
+//   COBS classic  "COBS:CLASSIC_INDEX" u32 version=1, u32 num_docs, u32 term_size,
+//                 u8 canonicalize, u64 signature_size, u64 num_hashes,
+//                 num_docs x (name '\n'), "CLASSIC_INDEX",
+//                 then signature_size rows of ceil(num_docs/8) bytes
+//                 (doc d = byte d>>3, bit d&7).
+//   COBS compact  "COBS:COMPACT_INDEX" u32 version=1, u32 term_size, u8 canonicalize,
+//                 u64 num_groups, num_groups x (u64 signature_size, u64 num_hashes),
+//                 u64 page_size, u32 num_docs, names, "COMPACT_INDEX", zero pad to a
+//                 multiple of page_size; then per group signature_size rows of
+//                 page_size bytes (group g = docs [8*page_size*g, 8*page_size*(g+1))).
+//   rbloom        u64 little-endian K, then the filter bytes (bit i = byte i>>3,
+//                 bit i&7).
+// On the device every row is padded to a 16-byte pitch so that one row of a
+// group is one aligned dwordx4 per 128 docs and never straddles a 64-byte line.
+#include "../../include/xspect_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "xs_internal.h"
+
+using namespace xs;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                       \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return fail(XS_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+const char kClassicMagic[] = "CLASSIC_INDEX";
+const char kCompactMagic[] = "COMPACT_INDEX";
+constexpr uint64_t kPad = 64;  // device over-read guard for strand windows
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return XS_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes < 256 ? 256 : bytes;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess)
+            return fail(XS_ERR_HIP, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        cap = want;
+        return XS_OK;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+}  // namespace
+
+struct xs_bank {
+    int kind = 0;
+    int device = 0;
+    uint32_t k = 0, h = 0, canonicalize = 1;
+    uint64_t D = 0, G = 0, page = 0;
+    std::vector<uint64_t> sig;
+    std::vector<std::string> names;
+    // device image
+    uint64_t pitch = 0;  // COBS: padded bytes per row
+    uint64_t dev_bytes = 0;
+    uint64_t nbytes = 0;  // rbloom filter bytes
+    DevBuf image;
+    DevBuf groups;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    // workspace
+    DevBuf seqs, offs, fwd, rc, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials,
+        totals, tmp;
+    bool profiling = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
+    size_t events_used = 0;
+
+    uint64_t sig_total() const {
+        uint64_t s = 0;
+        for (auto v : sig) s += v;
+        return s;
+    }
+    uint64_t payload_bytes() const {
+        return kind == XS_BANK_RBLOOM ? nbytes : sig_total() * page;
+    }
+    CobsView cobs_view() const {
+        CobsView v;
+        v.rows = image.as<uint8_t>();
+        v.groups = groups.as<GroupDesc>();
+        v.G = (uint32_t)G;
+        v.pitch = (uint32_t)pitch;
+        v.nchunks = (uint32_t)(pitch / 16);
+        v.h = h;
+        v.page = page;
+        v.D = D;
+        return v;
+    }
+    BloomView bloom_view() const {
+        BloomView v;
+        v.bits = image.as<uint32_t>();
+        v.mbits = nbytes * 8;
+        v.magic = barrett_magic(v.mbits);
+        v.K = h;
+        return v;
+    }
+};
+
+namespace {
+
+int validate_geometry(xs_bank* b) {
+    if (b->k < 1 || b->k > kMaxK)
+        return fail(XS_ERR_UNSUPPORTED, "term_size %u unsupported on the device (1..%u)", b->k, kMaxK);
+    if (b->h < 1 || b->h > kMaxHashes)
+        return fail(XS_ERR_UNSUPPORTED, "num_hashes %u unsupported on the device (1..%u)", b->h,
+                    kMaxHashes);
+    if (b->kind == XS_BANK_RBLOOM) {
+        if (b->nbytes == 0) return fail(XS_ERR_FORMAT, "empty rbloom filter");
+        return XS_OK;
+    }
+    if (b->D == 0) return fail(XS_ERR_FORMAT, "bank has no documents");
+    if (b->page == 0 || b->G == 0 || b->sig.size() != b->G)
+        return fail(XS_ERR_FORMAT, "bad group geometry");
+    if (b->G * 8 * b->page < b->D || (b->G - 1) * 8 * b->page >= b->D)
+        return fail(XS_ERR_FORMAT, "groups (%llu x %llu bytes) do not match %llu docs",
+                    (unsigned long long)b->G, (unsigned long long)b->page,
+                    (unsigned long long)b->D);
+    for (auto s : b->sig)
+        if (s == 0) return fail(XS_ERR_FORMAT, "zero signature size");
+    b->pitch = (b->page + 15) / 16 * 16;
+    if (b->pitch / 16 > kMaxChunks)
+        return fail(XS_ERR_UNSUPPORTED, "page of %llu bytes exceeds %u docs per group",
+                    (unsigned long long)b->page, kMaxChunks * 128);
+    int wpb;
+    size_t lds;
+    if (probe_blocks(b->D, &wpb, &lds) != 0)
+        return fail(XS_ERR_UNSUPPORTED, "%llu documents exceed the LDS counter budget",
+                    (unsigned long long)b->D);
+    return XS_OK;
+}
+
+// Allocate the (zeroed) device image and group table.
+int alloc_image(xs_bank* b) {
+    HIPCHK(hipSetDevice(b->device));
+    if (!b->stream) HIPCHK(hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking));
+    if (b->kind == XS_BANK_RBLOOM) {
+        b->dev_bytes = (b->nbytes + 15) / 16 * 16 + 16;
+        if (int rc = b->image.ensure(b->dev_bytes)) return rc;
+        HIPCHK(hipMemsetAsync(b->image.p, 0, b->dev_bytes, b->stream));
+    } else {
+        b->dev_bytes = b->sig_total() * b->pitch;
+        if (int rc = b->image.ensure(b->dev_bytes)) return rc;
+        HIPCHK(hipMemsetAsync(b->image.p, 0, b->dev_bytes, b->stream));
+        std::vector<GroupDesc> gd(b->G);
+        uint64_t base = 0;
+        for (uint64_t g = 0; g < b->G; ++g) {
+            gd[g].sig = b->sig[g];
+            gd[g].magic = barrett_magic(b->sig[g]);
+            gd[g].base = base;
+            base += b->sig[g] * b->pitch;
+        }
+        if (int rc = b->groups.ensure(sizeof(GroupDesc) * b->G)) return rc;
+        HIPCHK(hipMemcpyAsync(b->groups.p, gd.data(), sizeof(GroupDesc) * b->G,
+                              hipMemcpyHostToDevice, b->stream));
+    }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+// FILE layout payload (host) -> device image.
+int upload_payload(xs_bank* b, const void* host, uint64_t nbytes) {
+    if (nbytes != b->payload_bytes())
+        return fail(XS_ERR_ARG, "payload of %llu bytes, bank expects %llu",
+                    (unsigned long long)nbytes, (unsigned long long)b->payload_bytes());
+    HIPCHK(hipSetDevice(b->device));
+    if (b->kind == XS_BANK_RBLOOM) {
+        HIPCHK(hipMemcpyAsync(b->image.p, host, nbytes, hipMemcpyHostToDevice, b->stream));
+    } else if (b->pitch == b->page) {
+        HIPCHK(hipMemcpyAsync(b->image.p, host, nbytes, hipMemcpyHostToDevice, b->stream));
+    } else {
+        if (int rc = b->tmp.ensure(nbytes)) return rc;
+        HIPCHK(hipMemcpyAsync(b->tmp.p, host, nbytes, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(launch_repack(b->tmp.as<uint8_t>(), b->page, b->image.as<uint8_t>(), b->pitch,
+                             b->sig_total(), b->page, b->stream));
+    }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int download_payload(xs_bank* b, void* host, uint64_t nbytes) {
+    if (nbytes != b->payload_bytes())
+        return fail(XS_ERR_ARG, "buffer of %llu bytes, payload is %llu",
+                    (unsigned long long)nbytes, (unsigned long long)b->payload_bytes());
+    HIPCHK(hipSetDevice(b->device));
+    if (b->kind == XS_BANK_RBLOOM || b->pitch == b->page) {
+        HIPCHK(hipMemcpyAsync(host, b->image.p, nbytes, hipMemcpyDeviceToHost, b->stream));
+    } else {
+        if (int rc = b->tmp.ensure(nbytes)) return rc;
+        HIPCHK(launch_repack(b->image.as<uint8_t>(), b->pitch, b->tmp.as<uint8_t>(), b->page,
+                             b->sig_total(), b->page, b->stream));
+        HIPCHK(hipMemcpyAsync(host, b->tmp.p, nbytes, hipMemcpyDeviceToHost, b->stream));
+    }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+// ---- little binary reader -------------------------------------------------
+struct Reader {
+    std::ifstream f;
+    bool ok = true;
+    template <class T>
+    T get() {
+        T v{};
+        f.read(reinterpret_cast<char*>(&v), sizeof(T));
+        if (!f) ok = false;
+        return v;
+    }
+    bool expect(const char* s) {
+        std::string got(strlen(s), '\0');
+        f.read(&got[0], (std::streamsize)got.size());
+        if (!f || got != s) ok = false;
+        return ok;
+    }
+    std::string line() {
+        std::string s;
+        if (!std::getline(f, s)) ok = false;
+        return s;
+    }
+};
+
+template <class T>
+void put(std::ofstream& o, T v) {
+    o.write(reinterpret_cast<const char*>(&v), sizeof(T));
+}
+
+int read_cobs_header(xs_bank* b, Reader& rd, const char* path) {
+    if (!rd.expect("COBS:")) return fail(XS_ERR_FORMAT, "%s: not a COBS index", path);
+    if (b->kind == XS_BANK_COBS_CLASSIC) {
+        if (!rd.expect(kClassicMagic)) return fail(XS_ERR_FORMAT, "%s: not a classic index", path);
+        const uint32_t ver = rd.get<uint32_t>();
+        const uint32_t nd = rd.get<uint32_t>();
+        b->k = rd.get<uint32_t>();
+        b->canonicalize = rd.get<uint8_t>();
+        const uint64_t s = rd.get<uint64_t>();
+        b->h = (uint32_t)rd.get<uint64_t>();
+        if (!rd.ok || ver != 1) return fail(XS_ERR_FORMAT, "%s: bad classic header", path);
+        b->D = nd;
+        b->G = 1;
+        b->page = (nd + 7) / 8;
+        b->sig.assign(1, s);
+        for (uint32_t i = 0; i < nd; ++i) b->names.push_back(rd.line());
+        if (!rd.expect(kClassicMagic)) return fail(XS_ERR_FORMAT, "%s: bad classic trailer", path);
+    } else {
+        if (!rd.expect(kCompactMagic)) return fail(XS_ERR_FORMAT, "%s: not a compact index", path);
+        const uint32_t ver = rd.get<uint32_t>();
+        b->k = rd.get<uint32_t>();
+        b->canonicalize = rd.get<uint8_t>();
+        const uint64_t G = rd.get<uint64_t>();
+        if (!rd.ok || ver != 1 || G == 0 || G > (1u << 20))
+            return fail(XS_ERR_FORMAT, "%s: bad compact header", path);
+        b->G = G;
+        for (uint64_t g = 0; g < G; ++g) {
+            b->sig.push_back(rd.get<uint64_t>());
+            const uint32_t hg = (uint32_t)rd.get<uint64_t>();
+            if (g == 0) b->h = hg;
+            else if (hg != b->h) return fail(XS_ERR_FORMAT, "%s: mixed num_hashes", path);
+        }
+        b->page = rd.get<uint64_t>();
+        const uint32_t nd = rd.get<uint32_t>();
+        b->D = nd;
+        for (uint32_t i = 0; i < nd; ++i) b->names.push_back(rd.line());
+        if (!rd.expect(kCompactMagic)) return fail(XS_ERR_FORMAT, "%s: bad compact trailer", path);
+        if (b->page == 0) return fail(XS_ERR_FORMAT, "%s: zero page size", path);
+        const uint64_t pos = (uint64_t)rd.f.tellg();
+        const uint64_t pad = (b->page - pos % b->page) % b->page;
+        rd.f.seekg((std::streamoff)(pos + pad));
+    }
+    if (!rd.ok) return fail(XS_ERR_FORMAT, "%s: truncated header", path);
+    if (b->canonicalize != 1)
+        return fail(XS_ERR_UNSUPPORTED, "%s: non-canonical COBS indices are not supported", path);
+    return XS_OK;
+}
+
+int write_cobs_file(xs_bank* b, const char* path) {
+    std::vector<uint8_t> payload(b->payload_bytes());
+    if (int rc = download_payload(b, payload.data(), payload.size())) return rc;
+    std::ofstream o(path, std::ios::binary | std::ios::trunc);
+    if (!o) return fail(XS_ERR_IO, "cannot open %s for writing", path);
+    o.write("COBS:", 5);
+    if (b->kind == XS_BANK_COBS_CLASSIC) {
+        o.write(kClassicMagic, (std::streamsize)strlen(kClassicMagic));
+        put<uint32_t>(o, 1);
+        put<uint32_t>(o, (uint32_t)b->D);
+        put<uint32_t>(o, b->k);
+        put<uint8_t>(o, (uint8_t)b->canonicalize);
+        put<uint64_t>(o, b->sig[0]);
+        put<uint64_t>(o, b->h);
+        for (auto& n : b->names) o << n << '\n';
+        o.write(kClassicMagic, (std::streamsize)strlen(kClassicMagic));
+    } else {
+        o.write(kCompactMagic, (std::streamsize)strlen(kCompactMagic));
+        put<uint32_t>(o, 1);
+        put<uint32_t>(o, b->k);
+        put<uint8_t>(o, (uint8_t)b->canonicalize);
+        put<uint64_t>(o, b->G);
+        for (uint64_t g = 0; g < b->G; ++g) {
+            put<uint64_t>(o, b->sig[g]);
+            put<uint64_t>(o, b->h);
+        }
+        put<uint64_t>(o, b->page);
+        put<uint32_t>(o, (uint32_t)b->D);
+        for (auto& n : b->names) o << n << '\n';
+        o.write(kCompactMagic, (std::streamsize)strlen(kCompactMagic));
+        const uint64_t pos = (uint64_t)o.tellp();
+        const uint64_t pad = (b->page - pos % b->page) % b->page;
+        std::vector<char> z(pad, 0);
+        o.write(z.data(), (std::streamsize)pad);
+    }
+    o.write(reinterpret_cast<const char*>(payload.data()), (std::streamsize)payload.size());
+    if (!o) return fail(XS_ERR_IO, "write to %s failed", path);
+    return XS_OK;
+}
+
+int write_bloom_file(xs_bank* b, const char* path) {
+    std::vector<uint8_t> payload(b->nbytes);
+    if (int rc = download_payload(b, payload.data(), payload.size())) return rc;
+    std::ofstream o(path, std::ios::binary | std::ios::trunc);
+    if (!o) return fail(XS_ERR_IO, "cannot open %s for writing", path);
+    put<uint64_t>(o, b->h);
+    o.write(reinterpret_cast<const char*>(payload.data()), (std::streamsize)payload.size());
+    if (!o) return fail(XS_ERR_IO, "write to %s failed", path);
+    return XS_OK;
+}
+
+// ---- query / build pipeline --------------------------------------------------
+struct Inputs {
+    const uint8_t* seqs;
+    uint64_t seq_bytes;
+    const uint64_t* offs;
+    uint64_t n;
+};
+
+// Strands + unit decomposition for n device-resident reads.
+int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, uint32_t* hits_zero,
+                  uint64_t zero_cols, hipStream_t s, ReadView* rv) {
+    const int mode = b->kind == XS_BANK_RBLOOM ? kStrandBio : kStrandCobs;
+    const uint64_t nb = in.seq_bytes + kPad;
+    if (int rc = b->fwd.ensure(nb)) return rc;
+    if (int rc = b->rc.ensure(nb)) return rc;
+    if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;
+    if (int rc = b->unit_ofs.ensure((in.n + 1) * 8)) return rc;
+    if (int rc = b->n_units.ensure(16)) return rc;
+    const uint64_t unit_bound = in.n + in.seq_bytes / kSegKmers + 1;
+    if (int rc = b->unit_read.ensure(unit_bound * 4)) return rc;
+    const size_t tb = scan_temp_bytes(in.n ? in.n : 1);
+    if (int rc = b->scan_tmp.ensure(tb)) return rc;
+    HIPCHK(launch_strands(in.seqs, in.offs, in.n, in.seq_bytes, mode, b->fwd.as<uint8_t>(),
+                          b->rc.as<uint8_t>(), s));
+    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(), s));
+    HIPCHK(launch_scan(b->scan_tmp.p, b->scan_tmp.cap, b->nseg.as<uint64_t>(),
+                       b->unit_ofs.as<uint64_t>(), in.n, s));
+    HIPCHK(launch_scatter_units(b->nseg.as<uint64_t>(), b->unit_ofs.as<uint64_t>(), in.n,
+                                b->unit_read.as<uint32_t>(), b->n_units.as<uint64_t>(), hits_zero,
+                                zero_cols, s));
+    rv->fwd = b->fwd.as<uint8_t>();
+    rv->rc = b->rc.as<uint8_t>();
+    rv->offs = in.offs;
+    rv->unit_read = b->unit_read.as<uint32_t>();
+    rv->unit_ofs = b->unit_ofs.as<uint64_t>();
+    rv->n_units = b->n_units.as<uint64_t>();
+    rv->n = in.n;
+    rv->k = b->k;
+    rv->step = step;
+    return XS_OK;
+}
+
+int probe_grid(xs_bank* b, const Inputs& in) {
+    int wpb = 4;
+    size_t lds;
+    if (b->kind != XS_BANK_RBLOOM) probe_blocks(b->D, &wpb, &lds);
+    const uint64_t unit_bound = in.n + in.seq_bytes / kSegKmers + 1;
+    uint64_t g = (unit_bound + wpb - 1) / wpb;
+    const uint64_t cap = 256ull * 8 * 4 / (uint64_t)wpb;
+    if (g > cap) g = cap;
+    return (int)(g ? g : 1);
+}
+
+// Enqueue one query on device buffers.  d_totals: D+1 entries (or 2 for rbloom).
+int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uint64_t* d_nk,
+              uint64_t* d_totals, hipStream_t s) {
+    if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
+    if (in.n >= (1ull << 31)) return fail(XS_ERR_ARG, "at most 2^31-1 reads per call");
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    ReadView rv;
+    if (int rc = prepare_units(b, in, step, d_nk, d_hits, cols, s, &rv)) return rc;
+    const int blocks = probe_grid(b, in);
+    uint64_t* partials = nullptr;
+    const uint64_t pcols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
+    if (d_totals) {
+        if (int rc = b->partials.ensure((size_t)blocks * pcols * 8)) return rc;
+        partials = b->partials.as<uint64_t>();
+    }
+    if (b->profiling) {
+        if (b->events_used == b->events.size()) {
+            hipEvent_t a, c;
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&c));
+            b->events.emplace_back(a, c);
+        }
+        HIPCHK(hipEventRecord(b->events[b->events_used].first, s));
+    }
+    if (b->kind == XS_BANK_RBLOOM) HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, partials, blocks, s));
+    else HIPCHK(launch_probe_cobs(rv, b->cobs_view(), d_hits, partials, blocks, s));
+    if (b->profiling) {
+        HIPCHK(hipEventRecord(b->events[b->events_used].second, s));
+        ++b->events_used;
+    }
+    if (d_totals) HIPCHK(launch_reduce_partials(partials, blocks, pcols, d_totals, s));
+    return XS_OK;
+}
+
+// Copy host reads to the handle's device buffers (offsets rebased to 0).
+int stage_host_reads(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n,
+                     Inputs* in) {
+    const uint64_t base = offsets[0];
+    const uint64_t bytes = offsets[n] - base;
+    for (uint64_t r = 0; r < n; ++r)
+        if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    std::vector<uint64_t> rebased(n + 1);
+    for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
+    if (int rc = b->seqs.ensure(bytes + kPad)) return rc;
+    if (int rc = b->offs.ensure((n + 1) * 8)) return rc;
+    if (bytes) HIPCHK(hipMemcpyAsync(b->seqs.p, seqs + base, bytes, hipMemcpyHostToDevice, b->stream));
+    HIPCHK(hipMemcpyAsync(b->offs.p, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));  // `rebased` leaves scope
+    in->seqs = b->seqs.as<uint8_t>();
+    in->seq_bytes = bytes;
+    in->offs = b->offs.as<uint64_t>();
+    in->n = n;
+    return XS_OK;
+}
+
+xs_bank* new_bank(int device, int kind) {
+    xs_bank* b = new xs_bank();
+    b->device = device;
+    b->kind = kind;
+    return b;
+}
+
+}  // namespace
+
+extern "C" {
+
+int xs_version(void) { return 100; }
+
+const char* xs_last_error(void) { return g_err.c_str(); }
+
+int xs_device_count(int* count) {
+    if (!count) return fail(XS_ERR_ARG, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(XS_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    }
+    *count = n;
+    return XS_OK;
+}
+
+int xs_bank_open(const char* path, int kind, int device, xs_bank** out) {
+    if (!path || !out) return fail(XS_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT && kind != XS_BANK_RBLOOM)
+        return fail(XS_ERR_ARG, "unknown bank kind %d", kind);
+    Reader rd;
+    rd.f.open(path, std::ios::binary);
+    if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
+    rd.f.seekg(0, std::ios::end);
+    const uint64_t fsize = (uint64_t)rd.f.tellg();
+    rd.f.seekg(0);
+    xs_bank* b = new_bank(device, kind);
+    int rc = XS_OK;
+    if (kind == XS_BANK_RBLOOM) {
+        b->h = (uint32_t)rd.get<uint64_t>();
+        if (!rd.ok || fsize <= 8) rc = fail(XS_ERR_FORMAT, "%s: truncated rbloom file", path);
+        b->nbytes = fsize - 8;
+        b->D = 1;
+        b->names.push_back("0");
+        b->k = 0;  // set by the caller's model metadata through xs_bank_create_bloom
+    } else {
+        rc = read_cobs_header(b, rd, path);
+    }
+    if (rc == XS_OK && kind == XS_BANK_RBLOOM) {
+        // An rbloom file carries no k (the model JSON does); default to XspecT's
+        // k = 21 (train.py:167-174) until xs_bank_set_term_size overrides it.
+        b->k = 21;
+    }
+    if (rc == XS_OK) rc = validate_geometry(b);
+    if (rc == XS_OK) {
+        const uint64_t pos = (uint64_t)rd.f.tellg();
+        if (fsize - pos != b->payload_bytes())
+            rc = fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
+                      (unsigned long long)(fsize - pos), (unsigned long long)b->payload_bytes());
+    }
+    if (rc == XS_OK) rc = alloc_image(b);
+    if (rc == XS_OK) {
+        std::vector<uint8_t> payload(b->payload_bytes());
+        rd.f.read(reinterpret_cast<char*>(payload.data()), (std::streamsize)payload.size());
+        if (!rd.f) rc = fail(XS_ERR_IO, "%s: short read", path);
+        else rc = upload_payload(b, payload.data(), payload.size());
+    }
+    if (rc != XS_OK) {
+        delete b;
+        return rc;
+    }
+    *out = b;
+    return XS_OK;
+}
+
+int xs_bank_create_cobs(int device, int kind, uint32_t term_size, uint32_t num_hashes,
+                        uint64_t num_docs, uint64_t page_size, uint64_t num_groups,
+                        const uint64_t* sig, const char* const* doc_names, xs_bank** out) {
+    if (!out || !sig) return fail(XS_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT)
+        return fail(XS_ERR_ARG, "kind must be a COBS kind");
+    if (kind == XS_BANK_COBS_CLASSIC && (num_groups != 1 || page_size != (num_docs + 7) / 8))
+        return fail(XS_ERR_ARG, "classic banks have one group of ceil(D/8) bytes");
+    xs_bank* b = new_bank(device, kind);
+    b->k = term_size;
+    b->h = num_hashes;
+    b->D = num_docs;
+    b->G = num_groups;
+    b->page = page_size;
+    b->sig.assign(sig, sig + num_groups);
+    for (uint64_t i = 0; i < num_docs; ++i)
+        b->names.push_back(doc_names ? std::string(doc_names[i]) : std::to_string(i));
+    int rc = validate_geometry(b);
+    if (rc == XS_OK) rc = alloc_image(b);
+    if (rc != XS_OK) {
+        delete b;
+        return rc;
+    }
+    *out = b;
+    return XS_OK;
+}
+
+int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32_t nhash,
+                         xs_bank** out) {
+    if (!out) return fail(XS_ERR_ARG, "null argument");
+    *out = nullptr;
+    xs_bank* b = new_bank(device, XS_BANK_RBLOOM);
+    b->k = term_size;
+    b->h = nhash;
+    b->nbytes = nbytes;
+    b->D = 1;
+    b->names.push_back("0");
+    int rc = validate_geometry(b);
+    if (rc == XS_OK) rc = alloc_image(b);
+    if (rc != XS_OK) {
+        delete b;
+        return rc;
+    }
+    *out = b;
+    return XS_OK;
+}
+
+static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipStream_t s) {
+    ReadView rv;
+    if (int rc = prepare_units(b, in, 1, nullptr, nullptr, 0, s, &rv)) return rc;
+    const int blocks = probe_grid(b, in);
+    if (b->kind == XS_BANK_RBLOOM)
+        HIPCHK(launch_build_bloom(rv, b->bloom_view(), b->image.as<uint32_t>(), blocks, s));
+    else
+        HIPCHK(launch_build_cobs(rv, d_doc, b->cobs_view(), b->image.as<uint32_t>(), blocks, s));
+    return XS_OK;
+}
+
+int xs_bank_build(xs_bank* b, const char* seqs, const uint64_t* offsets, const uint32_t* rec_doc,
+                  uint64_t n_rec) {
+    if (!b || (!seqs && n_rec) || !offsets) return fail(XS_ERR_ARG, "null argument");
+    if (b->kind != XS_BANK_RBLOOM && n_rec && !rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    if (n_rec == 0) return XS_OK;
+    if (b->kind != XS_BANK_RBLOOM)
+        for (uint64_t r = 0; r < n_rec; ++r)
+            if (rec_doc[r] >= b->D) return fail(XS_ERR_ARG, "rec_doc[%llu] out of range", (unsigned long long)r);
+    Inputs in;
+    if (int rc = stage_host_reads(b, seqs, offsets, n_rec, &in)) return rc;
+    uint32_t* d_doc = nullptr;
+    if (b->kind != XS_BANK_RBLOOM) {
+        if (int rc = b->tmp.ensure(n_rec * 4)) return rc;
+        d_doc = b->tmp.as<uint32_t>();
+        HIPCHK(hipMemcpyAsync(d_doc, rec_doc, n_rec * 4, hipMemcpyHostToDevice, b->stream));
+    }
+    if (int rc = build_impl(b, in, d_doc, b->stream)) return rc;
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_bank_build_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes,
+                         const uint64_t* d_offsets, const uint32_t* d_rec_doc, uint64_t n_rec,
+                         void* stream) {
+    if (!b || !d_offsets) return fail(XS_ERR_ARG, "null argument");
+    if (b->kind != XS_BANK_RBLOOM && n_rec && !d_rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    if (n_rec == 0) return XS_OK;
+    Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n_rec};
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : b->stream;
+    return build_impl(b, in, d_rec_doc, s);
+}
+
+int xs_bank_save(xs_bank* b, const char* path) {
+    if (!b || !path) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipDeviceSynchronize());
+    return b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, path) : write_cobs_file(b, path);
+}
+
+int xs_bank_download(xs_bank* b, void* host, uint64_t nbytes) {
+    if (!b || !host) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipDeviceSynchronize());
+    return download_payload(b, host, nbytes);
+}
+
+int xs_bank_upload(xs_bank* b, const void* host, uint64_t nbytes) {
+    if (!b || !host) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    return upload_payload(b, host, nbytes);
+}
+
+int xs_bank_set_term_size(xs_bank* b, uint32_t term_size) {
+    if (!b) return fail(XS_ERR_ARG, "null argument");
+    if (b->kind != XS_BANK_RBLOOM)
+        return fail(XS_ERR_ARG, "COBS banks carry their term size in the file header");
+    if (term_size < 1 || term_size > kMaxK)
+        return fail(XS_ERR_UNSUPPORTED, "term_size %u unsupported on the device (1..%u)", term_size, kMaxK);
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->k = term_size;
+    return XS_OK;
+}
+
+int xs_bank_info(const xs_bank* b, xs_bank_info_t* o) {
+    if (!b || !o) return fail(XS_ERR_ARG, "null argument");
+    memset(o, 0, sizeof(*o));
+    o->kind = b->kind;
+    o->device = b->device;
+    o->term_size = b->k;
+    o->num_hashes = b->h;
+    o->canonicalize = b->canonicalize;
+    o->num_docs = b->D;
+    o->num_groups = b->kind == XS_BANK_RBLOOM ? 0 : b->G;
+    o->page_size = b->page;
+    o->signature_rows = b->sig_total();
+    o->bloom_bits = b->kind == XS_BANK_RBLOOM ? b->nbytes * 8 : 0;
+    o->device_bytes = b->dev_bytes;
+    o->device_row_pitch = b->pitch;
+    return XS_OK;
+}
+
+const char* xs_bank_doc_name(const xs_bank* b, uint64_t i) {
+    if (!b || i >= b->names.size()) {
+        fail(XS_ERR_ARG, "doc index out of range");
+        return nullptr;
+    }
+    return b->names[i].c_str();
+}
+
+int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+             uint32_t* hits_out, uint64_t* num_kmers_out) {
+    if (!b || !offsets || (!seqs && n)) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    if (n == 0) return XS_OK;
+    Inputs in;
+    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    uint32_t* d_hits = nullptr;
+    uint64_t* d_nk = nullptr;
+    if (hits_out) {
+        if (int rc = b->hits.ensure(n * cols * 4)) return rc;
+        d_hits = b->hits.as<uint32_t>();
+    }
+    if (num_kmers_out) {
+        if (int rc = b->nk.ensure(n * 8)) return rc;
+        d_nk = b->nk.as<uint64_t>();
+    }
+    if (int rc = run_query(b, in, step, d_hits, d_nk, nullptr, b->stream)) return rc;
+    if (hits_out) HIPCHK(hipMemcpyAsync(hits_out, d_hits, n * cols * 4, hipMemcpyDeviceToHost, b->stream));
+    if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_query_totals(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n,
+                    uint32_t step, uint64_t* totals_out, uint64_t* total_kmers_out) {
+    if (!b || !offsets || (!seqs && n) || !totals_out) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    if (n == 0) {
+        memset(totals_out, 0, cols * 8);
+        if (total_kmers_out) *total_kmers_out = 0;
+        return XS_OK;
+    }
+    Inputs in;
+    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
+    if (int rc = b->totals.ensure((cols + 1) * 8)) return rc;
+    if (int rc = run_query(b, in, step, nullptr, nullptr, b->totals.as<uint64_t>(), b->stream)) return rc;
+    std::vector<uint64_t> t(cols + 1);
+    HIPCHK(hipMemcpyAsync(t.data(), b->totals.p, (cols + 1) * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    memcpy(totals_out, t.data(), cols * 8);
+    if (total_kmers_out) *total_kmers_out = t[cols];
+    return XS_OK;
+}
+
+int xs_query_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, const uint64_t* d_offsets,
+                    uint64_t n, uint32_t step, uint32_t* d_hits, uint64_t* d_num_kmers,
+                    uint64_t* d_totals, void* stream) {
+    if (!b || !d_offsets || (!d_seqs && n)) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : b->stream;
+    if (n == 0) {
+        if (d_totals) {
+            const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
+            HIPCHK(hipMemsetAsync(d_totals, 0, cols * 8, s));
+        }
+        return XS_OK;
+    }
+    Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n};
+    return run_query(b, in, step, d_hits, d_num_kmers, d_totals, s);
+}
+
+int xs_mlst_sum(xs_bank* b, const uint32_t* hits, const uint32_t* seq_of_chunk, uint64_t n_chunks,
+                uint64_t n_seqs, uint32_t threshold, uint64_t* scores) {
+    if (!b || (!hits && n_chunks) || (!seq_of_chunk && n_chunks) || !scores)
+        return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t D = b->D;
+    for (uint64_t c = 0; c < n_chunks; ++c)
+        if (seq_of_chunk[c] >= n_seqs) return fail(XS_ERR_ARG, "seq_of_chunk[%llu] out of range", (unsigned long long)c);
+    if (n_seqs == 0) return XS_OK;
+    if (int rc = b->hits.ensure(n_chunks * D * 4 + 4)) return rc;
+    if (int rc = b->tmp.ensure(n_chunks * 4 + 4)) return rc;
+    if (int rc = b->totals.ensure(n_seqs * D * 8)) return rc;
+    if (n_chunks) {
+        HIPCHK(hipMemcpyAsync(b->hits.p, hits, n_chunks * D * 4, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(hipMemcpyAsync(b->tmp.p, seq_of_chunk, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
+    }
+    HIPCHK(hipMemsetAsync(b->totals.p, 0, n_seqs * D * 8, b->stream));
+    HIPCHK(launch_mlst_sum(b->hits.as<uint32_t>(), b->tmp.as<uint32_t>(), n_chunks, D, threshold,
+                           b->totals.as<unsigned long long>(), b->stream));
+    HIPCHK(hipMemcpyAsync(scores, b->totals.p, n_seqs * D * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_bank_set_profiling(xs_bank* b, int on) {
+    if (!b) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    b->profiling = on != 0;
+    return XS_OK;
+}
+
+int xs_bank_last_probe_ms(xs_bank* b, float* ms) {
+    if (!b || !ms) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    if (b->events_used == 0) return fail(XS_ERR_ARG, "no profiled query on this handle");
+    HIPCHK(hipSetDevice(b->device));
+    auto& ev = b->events[b->events_used - 1];
+    HIPCHK(hipEventSynchronize(ev.second));
+    HIPCHK(hipEventElapsedTime(ms, ev.first, ev.second));
+    return XS_OK;
+}
+
+int xs_bank_probe_stats(xs_bank* b, uint64_t* count, double* total_ms, float* max_ms) {
+    if (!b || !count || !total_ms) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    double tot = 0.0;
+    float mx = 0.0f;
+    for (size_t i = 0; i < b->events_used; ++i) {
+        float ms = 0.0f;
+        HIPCHK(hipEventSynchronize(b->events[i].second));
+        HIPCHK(hipEventElapsedTime(&ms, b->events[i].first, b->events[i].second));
+        tot += ms;
+        mx = ms > mx ? ms : mx;
+    }
+    *count = b->events_used;
+    *total_ms = tot;
+    if (max_ms) *max_ms = mx;
+    b->events_used = 0;
+    return XS_OK;
+}
+
+void xs_bank_close(xs_bank* b) {
+    if (!b) return;
+    (void)hipSetDevice(b->device);
+    if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (auto& ev : b->events) {
+        (void)hipEventDestroy(ev.first);
+        (void)hipEventDestroy(ev.second);
+    }
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    delete b;  // DevBuf destructors free device memory
+}
+
+}  // extern "C"

@@ -1,0 +1,95 @@
+// xs_internal.h — shared between the host library (xs_api.cpp) and the
+// gfx950 kernels (xs_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace xs {
+
+// k-mers per work unit.  A read with more sampled k-mers is split into
+// ceil(nk / kSegKmers) units whose partial counts are added atomically.
+constexpr uint32_t kSegKmers = 256;
+// Block geometry of the probe kernels (4 waves).
+constexpr int kProbeThreads = 256;
+constexpr int kWave = 64;
+// Maximum k supported on the device (canonical k-mer held in 8 dwords).
+constexpr uint32_t kMaxK = 32;
+// Maximum hash functions per bank on the device.
+constexpr uint32_t kMaxHashes = 16;
+// Maximum 16-byte chunks per padded row of one group (1024 docs per group).
+constexpr uint32_t kMaxChunks = 8;
+// LDS budget per probe block for per-wave doc counters.
+constexpr uint32_t kLdsBudget = 64 * 1024;
+
+enum StrandMode : int { kStrandCobs = 0, kStrandBio = 1 };
+
+// One COBS doc group on the device.
+struct GroupDesc {
+    uint64_t sig;    // signature size (rows)
+    uint64_t magic;  // floor((2^64-1)/sig) for Barrett reduction
+    uint64_t base;   // byte offset of row 0 in the device image
+};
+
+struct CobsView {
+    const uint8_t* rows;      // device image, rows of `pitch` bytes per group
+    const GroupDesc* groups;  // device array [G]
+    uint32_t G;
+    uint32_t pitch;           // device bytes per row (multiple of 16)
+    uint32_t nchunks;         // pitch / 16
+    uint32_t h;
+    uint64_t page;            // file bytes per row (docs per group = 8*page)
+    uint64_t D;
+};
+
+struct BloomView {
+    const uint32_t* bits;  // device image, padded to 16 bytes
+    uint64_t mbits;        // number of bits (nbytes*8)
+    uint64_t magic;        // floor((2^64-1)/mbits)
+    uint32_t K;
+};
+
+// Reads / records laid out for one probe or build call.
+struct ReadView {
+    const uint8_t* fwd;        // forward strand (normalised for COBS)
+    const uint8_t* rc;         // reverse-complement strand, same offsets
+    const uint64_t* offs;      // n+1
+    const uint32_t* unit_read; // units -> read
+    const uint64_t* unit_ofs;  // first unit of each read (n)
+    const uint64_t* n_units;   // device scalar
+    uint64_t n;
+    uint32_t k;
+    uint32_t step;
+};
+
+// ---- launchers (xs_kernels.hip) -------------------------------------------
+hipError_t launch_strands(const uint8_t* seqs, const uint64_t* offs, uint64_t n, uint64_t nbytes,
+                          int mode, uint8_t* fwd_out, uint8_t* rc_out, hipStream_t s);
+hipError_t launch_units(const uint64_t* offs, uint64_t n, uint32_t k, uint32_t step,
+                        uint64_t* nk_out, uint64_t* nseg, hipStream_t s);
+size_t scan_temp_bytes(uint64_t n);
+hipError_t launch_scan(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out,
+                       uint64_t n, hipStream_t s);
+hipError_t launch_scatter_units(const uint64_t* nseg, const uint64_t* unit_ofs, uint64_t n,
+                                uint32_t* unit_read, uint64_t* n_units, uint32_t* hits_zero,
+                                uint64_t D, hipStream_t s);
+int probe_blocks(uint64_t D, int* waves_per_block, size_t* lds_bytes);
+hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* hits,
+                             uint64_t* partials, int blocks, hipStream_t s);
+hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
+                              uint64_t* partials, int blocks, hipStream_t s);
+hipError_t launch_reduce_partials(const uint64_t* partials, int blocks, uint64_t cols,
+                                  uint64_t* totals, hipStream_t s);
+hipError_t launch_build_cobs(const ReadView& rv, const uint32_t* rec_doc, const CobsView& bv,
+                             uint32_t* rows_mut, int blocks, hipStream_t s);
+hipError_t launch_build_bloom(const ReadView& rv, const BloomView& bv, uint32_t* bits_mut,
+                              int blocks, hipStream_t s);
+hipError_t launch_repack(const uint8_t* src, uint64_t src_pitch, uint8_t* dst, uint64_t dst_pitch,
+                         uint64_t rows, uint64_t copy_bytes, hipStream_t s);
+hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, uint64_t n_chunks,
+                           uint64_t D, uint32_t threshold, unsigned long long* scores,
+                           hipStream_t s);
+
+// Host-side constants shared with the kernels.
+inline uint64_t barrett_magic(uint64_t d) { return d ? (~0ull) / d : 0; }
+
+}  // namespace xs

@@ -1,0 +1,295 @@
+"""Species model over a COBS classic bank resident in HBM.
+
+Drop-in for ``xspect.models.probabilistic_filter_model.ProbabilisticFilterModel``
+(reference ``src/xspect/models/probabilistic_filter_model.py:28-601``): same
+constructor, ``fit``/``save``/``load``/``predict``/``calculate_hits``/
+``to_dict``/``slug`` and the same ``ModelResult``.  What changes is below the
+surface: the reference re-enters ``cobs_index.Search.search`` once per read
+(``:291-310``, ``:227``); here a whole batch of reads is one call into
+libxspect_hip.so, which probes the bank on the GPU.
+"""
+from __future__ import annotations
+
+import json
+import math
+from pathlib import Path
+from typing import Iterable
+
+import numpy as np
+
+from .bank import Bank, cobs_signature_size
+from ._lib import XS_BANK_COBS_CLASSIC
+from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, get_record_iterator, is_record, seq_text)
+from .packing import PackedReads, pack_sequences
+from .result import ModelResult
+from .util import default_device, slugify
+
+# One C-ABI call handles at most this many sequence bytes / reads.
+MAX_BATCH_BYTES = 1 << 30
+MAX_BATCH_READS = 1 << 24
+
+
+def _records(sequence_input) -> list | None:
+    """Materialise a record list / iterator; None if the input is neither."""
+    if isinstance(sequence_input, (list, tuple)):
+        return list(sequence_input) if all(is_record(r) for r in sequence_input) else None
+    if isinstance(sequence_input, (str, bytes, Path)) or is_record(sequence_input):
+        return None
+    if hasattr(sequence_input, "__iter__") and hasattr(sequence_input, "__next__"):
+        return list(sequence_input)
+    return None
+
+
+def _check_seq_type(sequence) -> str:
+    """The reference accepts only Bio.Seq here (:219-222); str/bytes are the
+    offline stand-ins.  Records and other objects are rejected."""
+    if is_record(sequence) or not isinstance(sequence, (str, bytes, bytearray)) and \
+            type(sequence).__name__ not in ("Seq", "MutableSeq"):
+        raise ValueError("Invalid sequence, must be a Bio.Seq or a Bio.SeqRecord object")
+    return seq_text(sequence)
+
+
+def cobs_result_order(row: np.ndarray) -> np.ndarray:
+    """Doc order of one COBS result: score descending, ties by doc index
+    (the tie order of the real library is implementation-defined)."""
+    return np.argsort(-row.astype(np.int64), kind="stable")
+
+
+class ProbabilisticFilterModel:
+    """Probabilistic filter (COBS classic) species model on the GPU."""
+
+    def __init__(
+        self,
+        k: int,
+        model_display_name: str,
+        author: str | None,
+        author_email: str | None,
+        model_type: str,
+        base_path: Path,
+        fpr: float = 0.01,
+        num_hashes: int = 7,
+        training_accessions: dict[str, list[str]] | None = None,
+    ) -> None:
+        if k < 1:
+            raise ValueError("Invalid k value, must be greater than 0")
+        if not model_display_name:
+            raise ValueError("Invalid filter display name, must be a non-empty string")
+        if not model_type:
+            raise ValueError("Invalid filter type, must be a non-empty string")
+        if not isinstance(base_path, Path):
+            raise ValueError("Invalid base path, must be a pathlib.Path object")
+        self.k = k
+        self.model_display_name = model_display_name
+        self.author = author
+        self.author_email = author_email
+        self.model_type = model_type
+        self.base_path = base_path
+        self.display_names: dict[str, str] = {}
+        self.fpr = fpr
+        self.num_hashes = num_hashes
+        self.index: Bank | None = None
+        self.training_accessions = training_accessions
+        self.device = default_device()
+
+    # ------------------------------------------------------------ identity
+    def get_cobs_index_path(self) -> str:
+        return str(self.base_path / self.slug() / "index.cobs_classic")
+
+    def to_dict(self) -> dict:
+        return {
+            "model_slug": self.slug(),
+            "k": self.k,
+            "model_display_name": self.model_display_name,
+            "author": self.author,
+            "author_email": self.author_email,
+            "model_type": self.model_type,
+            "model_class": self.__class__.__name__,
+            "display_names": self.display_names,
+            "fpr": self.fpr,
+            "num_hashes": self.num_hashes,
+            "training_accessions": self.training_accessions,
+        }
+
+    def slug(self) -> str:
+        return slugify(self.model_display_name + "-" + str(self.model_type))
+
+    # ------------------------------------------------------------ training
+    def fit(self, dir_path: Path, display_names: dict | None = None,
+            training_accessions: dict[str, list[str]] | None = None) -> None:
+        """Build the COBS classic bank from one FASTA/FASTQ file per species
+        (reference :131-194).  Files are taken in name order; the doc name is the
+        file name up to its first '.' (as COBS does)."""
+        display_names = display_names or {}
+        if not isinstance(dir_path, Path):
+            raise ValueError("Invalid directory path, must be a pathlib.Path object")
+        if not dir_path.exists():
+            raise ValueError("Directory path does not exist")
+        if not dir_path.is_dir():
+            raise ValueError("Directory path must be a directory")
+        self.training_accessions = training_accessions
+        files = sorted(f for f in dir_path.iterdir()
+                       if f.is_file() and f.suffix[1:] in FASTA_ENDINGS + FASTQ_ENDINGS)
+        if not files:
+            raise ValueError("No valid files found in directory. Must be fasta or fastq")
+        names = []
+        for f in files:
+            doc = f.stem.split(".")[0]
+            self.display_names[doc] = display_names.get(f.stem, f.stem)
+            names.append(doc)
+        # signature size from the largest document's term count
+        terms = [sum(max(0, len(r.seq) - self.k + 1) for r in get_record_iterator(f)) for f in files]
+        sig = cobs_signature_size(max(max(terms), 1), self.num_hashes, self.fpr)
+        bank = Bank.create_cobs(self.k, self.num_hashes, [sig], len(files), names, device=self.device)
+        for d, f in enumerate(files):
+            recs = [seq_text(r.seq) for r in get_record_iterator(f)]
+            if recs:
+                bank.build(pack_sequences(recs), np.full(len(recs), d, dtype=np.uint32))
+        path = Path(self.get_cobs_index_path())
+        bank.save(path)
+        if self.index is not None:
+            self.index.close()
+        self.index = bank
+
+    # ------------------------------------------------------------ queries
+    def _query(self, packed: PackedReads, step: int):
+        if self.index is None:
+            raise ValueError("The model has not been trained yet")
+        return self.index.query(packed, step=step)
+
+    def _hit_dict(self, row: np.ndarray, exclude_ids) -> dict:
+        names = self.index.doc_names
+        order = cobs_result_order(row)
+        vals = row[order].tolist()
+        out = {names[i]: v for i, v in zip(order.tolist(), vals)}
+        if exclude_ids:
+            return {doc: s for doc, s in out.items() if doc not in exclude_ids}
+        return out
+
+    def calculate_hits(self, sequence, exclude_ids: list[str] | None = None, step: int = 1) -> dict:
+        """{doc_name: score} of one sequence (reference :196-235)."""
+        text = _check_seq_type(sequence)
+        if not len(text) > self.k:
+            raise ValueError("Invalid sequence, must be longer than k")
+        hits, _ = self._query(pack_sequences([text]), step)
+        return self._hit_dict(hits[0], exclude_ids)
+
+    def predict_matrix(self, sequence_input, step: int = 1):
+        """Columnar result of a batch: (ids, hits [n, D] uint32, num_kmers [n] uint64).
+
+        Same hits as ``predict`` without per-read dictionaries (the form that
+        scales to 10^8 reads)."""
+        ids, _, hits, nk = self._matrix(sequence_input, step)
+        return ids, hits, nk
+
+    def _matrix(self, sequence_input, step: int):
+        if step < 1:
+            raise ValueError("step must be >= 1")
+        records = self._collect(sequence_input)
+        ids = [r.id for r in records]
+        texts = [seq_text(r.seq) for r in records]
+        lens = [len(t) for t in texts]
+        for n in lens:
+            if not n > self.k:
+                raise ValueError("Invalid sequence, must be longer than k")
+        if self.index is None:
+            raise ValueError("The model has not been trained yet")
+        hits = np.zeros((len(texts), self.index.num_docs), dtype=np.uint32)
+        nk = np.zeros(len(texts), dtype=np.uint64)
+        for lo, hi in _batches(lens):
+            h, n = self._query(pack_sequences(texts[lo:hi]), step)
+            hits[lo:hi] = h
+            nk[lo:hi] = n
+        return ids, lens, hits, nk
+
+    def _collect(self, sequence_input) -> list:
+        if is_record(sequence_input):
+            return [sequence_input]
+        if isinstance(sequence_input, Path):
+            return list(get_record_iterator(sequence_input))
+        recs = _records(sequence_input)
+        if recs is None:
+            raise ValueError(
+                "Invalid sequence input, must be a Seq object, a list of Seq objects, a"
+                " SeqIO FastaIterator, a SeqIO FastqPhredIterator, or a Path object to a"
+                " fasta/fastq file")
+        return recs
+
+    def predict(self, sequence_input, exclude_ids: list[str] = None, step: int = 1,
+                display_name: bool = False, validation: bool = False) -> ModelResult:
+        """ModelResult of a record / list / iterator / FASTA-FASTQ path (reference :237-331)."""
+        if validation:
+            # misclassification detection maps reads with minimap2 against NCBI
+            # downloads (:508-601): outside the probe path, see DESIGN.md.
+            raise NotImplementedError("validation (alignment-based misclassification detection) "
+                                      "is outside the GPU probe path")
+        ids, lens, hits_m, _ = self._matrix(sequence_input, step)
+        hits: dict[str, dict] = {}
+        num_kmers: dict[str, int] = {}
+        for i, rid in enumerate(ids):
+            per = self._hit_dict(hits_m[i], exclude_ids)
+            if display_name:
+                per = {f"{key} -{self.display_names.get(key, 'Unknown').replace(self.model_display_name, '', 1)}": v
+                       for key, v in per.items()}
+            num_kmers[rid] = self._count_kmers_len(lens[i], step)
+            hits[rid] = per
+        return ModelResult(self.slug(), hits, num_kmers, sparse_sampling_step=step)
+
+    # ------------------------------------------------------------ k-mer counts
+    def _count_kmers_len(self, length: int, step: int) -> int:
+        return math.ceil((length - self.k + 1) / step)   # reference :462
+
+    def _count_kmers(self, sequence_input, step: int = 1) -> int:
+        """Total sampled k-mers of a sequence / record / list / iterator (:411-469)."""
+        if is_record(sequence_input):
+            return self._count_kmers_len(len(seq_text(sequence_input.seq)), step)
+        if isinstance(sequence_input, (str, bytes)) or type(sequence_input).__name__ == "Seq":
+            return self._count_kmers_len(len(seq_text(sequence_input)), step)
+        if isinstance(sequence_input, (list, tuple)) or hasattr(sequence_input, "__next__"):
+            total = 0
+            for s in sequence_input:
+                text = seq_text(s.seq) if is_record(s) else seq_text(s)
+                total += self._count_kmers_len(len(text), step)
+            return total
+        raise ValueError(
+            "Invalid sequence input, must be a Seq object, a list of Seq objects, a"
+            " SeqIO FastaIterator, or a SeqIO FastqPhredIterator")
+
+    # ------------------------------------------------------------ persistence
+    def save(self) -> None:
+        json_path = self.base_path / f"{self.slug()}.json"
+        (self.base_path / self.slug()).mkdir(exist_ok=True, parents=True)
+        json_path.write_text(json.dumps(self.to_dict(), indent=4), encoding="utf-8")
+
+    @staticmethod
+    def load(path: Path) -> "ProbabilisticFilterModel":
+        meta = json.loads(Path(path).read_text(encoding="utf-8"))
+        model = ProbabilisticFilterModel(
+            meta["k"], meta["model_display_name"], meta["author"], meta["author_email"],
+            meta["model_type"], Path(path).parent, meta["fpr"], meta["num_hashes"],
+            meta["training_accessions"])
+        model.display_names = meta["display_names"]
+        model._open_index()
+        return model
+
+    def _open_index(self) -> None:
+        index_path = Path(self.get_cobs_index_path())
+        if not index_path.exists():
+            raise FileNotFoundError(f"Index file not found at {index_path}")
+        self.index = Bank.open(index_path, XS_BANK_COBS_CLASSIC, device=self.device)
+
+    def close(self) -> None:
+        if self.index is not None:
+            self.index.close()
+            self.index = None
+
+
+def _batches(lens: list[int]) -> Iterable[tuple[int, int]]:
+    """Split reads into C-ABI calls of bounded size (reads are never split)."""
+    lo, size = 0, 0
+    for i, n in enumerate(lens):
+        if i > lo and (size + n > MAX_BATCH_BYTES or i - lo >= MAX_BATCH_READS):
+            yield lo, i
+            lo, size = i, 0
+        size += n
+    if lo < len(lens):
+        yield lo, len(lens)
