@@ -79,7 +79,7 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
         want_h, want_n = ob.query(reads, step=step)
         got_h, got_n = gb.query(reads, step=step)
         assert np.array_equal(got_n, want_n), f"num_kmers differ (step {step})"
-        assert np.array_equal(got_h, want_h), f"hits differ (step {step})"
+        assert np.array_equal(got_h, want_h), _explain(got_h, want_h, reads)
         tot, nk = gb.query_totals(reads, step=step)
         assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64))
         assert nk == int(want_n.sum())
@@ -208,3 +208,12 @@ def test_mlst_sum_matches_numpy(xs):
         want[owner[c], m] += hits[c, m]
     assert np.array_equal(got, want)
     gb.close()
+
+
+def _explain(got, want, reads):
+    bad = np.flatnonzero((np.asarray(got) != np.asarray(want)).reshape(len(reads), -1).any(axis=1))
+    rows = []
+    for i in bad[:5]:
+        r = reads[i]
+        rows.append(f"read {i} len={len(r)} head={r[:30]!r} got={np.asarray(got)[i][:8]} want={np.asarray(want)[i][:8]}")
+    return f"{bad.size} rows differ: " + "; ".join(rows)

@@ -299,7 +299,9 @@ __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
          r += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t s = nseg[r], b = unit_ofs[r];
         for (uint64_t u = 0; u < s; ++u) unit_read[b + u] = (uint32_t)r;
-        if (s > 1 && hits_zero)
+        // rows the probe does not store whole: no k-mers (never visited) or
+        // several units (accumulated atomically)
+        if (s != 1 && hits_zero)
             for (uint64_t d = 0; d < D; ++d) hits_zero[r * D + d] = 0;
         if (r == n - 1) *n_units = b + s;
     }
