@@ -100,7 +100,7 @@ struct xs_bank {
     std::mutex mu;
     // workspace
     DevBuf seqs, offs, fwd, rc, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials,
-        totals, tmp;
+        totals, tmp, chunks;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -123,6 +123,7 @@ struct xs_bank {
         v.h = h;
         v.page = page;
         v.D = D;
+        v.sig0 = sig.empty() ? 0 : sig[0];
         return v;
     }
     BloomView bloom_view() const {
@@ -378,14 +379,16 @@ int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, u
     if (int rc = b->rc.ensure(nb)) return rc;
     if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->unit_ofs.ensure((in.n + 1) * 8)) return rc;
-    if (int rc = b->n_units.ensure(16)) return rc;
+    if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
     const uint64_t unit_bound = in.n + in.seq_bytes / kSegKmers + 1;
     if (int rc = b->unit_read.ensure(unit_bound * 4)) return rc;
     const size_t tb = scan_temp_bytes(in.n ? in.n : 1);
     if (int rc = b->scan_tmp.ensure(tb)) return rc;
+    if (int rc = b->chunks.ensure(strand_chunk_slots(in.seq_bytes) * 4)) return rc;
+    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(),
+                        b->chunks.as<uint32_t>(), s));
     HIPCHK(launch_strands(in.seqs, in.offs, in.n, in.seq_bytes, mode, b->fwd.as<uint8_t>(),
-                          b->rc.as<uint8_t>(), s));
-    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(), s));
+                          b->rc.as<uint8_t>(), b->chunks.as<uint32_t>(), s));
     HIPCHK(launch_scan(b->scan_tmp.p, b->scan_tmp.cap, b->nseg.as<uint64_t>(),
                        b->unit_ofs.as<uint64_t>(), in.n, s));
     HIPCHK(launch_scatter_units(b->nseg.as<uint64_t>(), b->unit_ofs.as<uint64_t>(), in.n,
@@ -396,22 +399,17 @@ int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, u
     rv->offs = in.offs;
     rv->unit_read = b->unit_read.as<uint32_t>();
     rv->unit_ofs = b->unit_ofs.as<uint64_t>();
-    rv->n_units = b->n_units.as<uint64_t>();
+    rv->queue = b->n_units.as<uint64_t>();
     rv->n = in.n;
     rv->k = b->k;
     rv->step = step;
     return XS_OK;
 }
 
-int probe_grid(xs_bank* b, const Inputs& in) {
-    int wpb = 4;
-    size_t lds;
-    if (b->kind != XS_BANK_RBLOOM) probe_blocks(b->D, &wpb, &lds);
-    const uint64_t unit_bound = in.n + in.seq_bytes / kSegKmers + 1;
-    uint64_t g = (unit_bound + wpb - 1) / wpb;
-    const uint64_t cap = 256ull * 8 * 4 / (uint64_t)wpb;
-    if (g > cap) g = cap;
-    return (int)(g ? g : 1);
+int probe_grid(xs_bank* b) {
+    HIPCHK(hipSetDevice(b->device));
+    const int g = b->kind == XS_BANK_RBLOOM ? probe_grid_bloom() : probe_grid_cobs(b->cobs_view(), b->k);
+    return g > 0 ? g : 1;
 }
 
 // Enqueue one query on device buffers.  d_totals: D+1 entries (or 2 for rbloom).
@@ -422,7 +420,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     ReadView rv;
     if (int rc = prepare_units(b, in, step, d_nk, d_hits, cols, s, &rv)) return rc;
-    const int blocks = probe_grid(b, in);
+    const int blocks = probe_grid(b);
     uint64_t* partials = nullptr;
     const uint64_t pcols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
     if (d_totals) {
@@ -597,7 +595,7 @@ int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32
 static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipStream_t s) {
     ReadView rv;
     if (int rc = prepare_units(b, in, 1, nullptr, nullptr, 0, s, &rv)) return rc;
-    const int blocks = probe_grid(b, in);
+    const int blocks = probe_grid(b);
     if (b->kind == XS_BANK_RBLOOM)
         HIPCHK(launch_build_bloom(rv, b->bloom_view(), b->image.as<uint32_t>(), blocks, s));
     else

@@ -39,6 +39,7 @@ struct CobsView {
     uint32_t h;
     uint64_t page;            // file bytes per row (docs per group = 8*page)
     uint64_t D;
+    uint64_t sig0;            // host copy of groups[0].sig (fast-path selection)
 };
 
 struct BloomView {
@@ -55,24 +56,28 @@ struct ReadView {
     const uint64_t* offs;      // n+1
     const uint32_t* unit_read; // units -> read
     const uint64_t* unit_ofs;  // first unit of each read (n)
-    const uint64_t* n_units;   // device scalar
+    uint64_t* queue;           // device: [0] = #units, [1] = next unit to hand out
     uint64_t n;
     uint32_t k;
     uint32_t step;
 };
 
 // ---- launchers (xs_kernels.hip) -------------------------------------------
+uint64_t strand_chunk_slots(uint64_t nbytes);
 hipError_t launch_strands(const uint8_t* seqs, const uint64_t* offs, uint64_t n, uint64_t nbytes,
-                          int mode, uint8_t* fwd_out, uint8_t* rc_out, hipStream_t s);
+                          int mode, uint8_t* fwd_out, uint8_t* rc_out, const uint32_t* chunk_first,
+                          hipStream_t s);
 hipError_t launch_units(const uint64_t* offs, uint64_t n, uint32_t k, uint32_t step,
-                        uint64_t* nk_out, uint64_t* nseg, hipStream_t s);
+                        uint64_t* nk_out, uint64_t* nseg, uint32_t* chunk_first, hipStream_t s);
 size_t scan_temp_bytes(uint64_t n);
 hipError_t launch_scan(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out,
                        uint64_t n, hipStream_t s);
 hipError_t launch_scatter_units(const uint64_t* nseg, const uint64_t* unit_ofs, uint64_t n,
-                                uint32_t* unit_read, uint64_t* n_units, uint32_t* hits_zero,
+                                uint32_t* unit_read, uint64_t* queue, uint32_t* hits_zero,
                                 uint64_t D, hipStream_t s);
 int probe_blocks(uint64_t D, int* waves_per_block, size_t* lds_bytes);
+int probe_grid_cobs(const CobsView& bv, uint32_t k);
+int probe_grid_bloom();
 hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* hits,
                              uint64_t* partials, int blocks, hipStream_t s);
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,

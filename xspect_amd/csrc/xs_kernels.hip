@@ -18,6 +18,8 @@
 //   rbloom `kmer in bf`                    probabilistic_single_filter_model.py:122-124
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "xs_internal.h"
 
 // v_writelane_b32: this clang exposes only readlane as a builtin; bind the
@@ -239,38 +241,83 @@ __device__ __forceinline__ void strand_tables(int mode, uint8_t* tf, uint8_t* tr
     }
 }
 
-constexpr uint64_t kStrandChunk = 4096;
+
+// One thread per output dword: the forward strand byte p is tf[seq[p]], the
+// reverse-complement strand byte p is tr[seq[mirror(p)]] with mirror(p) =
+// offs[r] + offs[r+1] - 1 - p inside read r.  Both strands share the read
+// offsets, so the reverse complement of k-mer [p, p+k) of read r is the rc
+// window [offs[r+1] - (p - offs[r]) - k, ... + k).
+constexpr uint32_t kStrandIters = 16;
+constexpr uint64_t kStrandChunk = 256ull * 4 * kStrandIters;  // bytes per block iteration
+constexpr uint32_t kStrandMaxReads = 2048;                    // offsets staged in LDS
 
 __global__ void __launch_bounds__(256) strands_kernel(const uint8_t* __restrict__ seqs,
                                                       const uint64_t* __restrict__ offs,
                                                       uint64_t n, int mode,
-                                                      uint8_t* __restrict__ fwd,
-                                                      uint8_t* __restrict__ rc) {
+                                                      uint32_t* __restrict__ fwd,
+                                                      uint32_t* __restrict__ rc,
+                                                      const uint32_t* __restrict__ chunk_first) {
     __shared__ uint8_t tf[256], tr[256];
-    __shared__ uint64_t s_r0;
+    __shared__ uint64_t s_off[kStrandMaxReads + 1];
     strand_tables(mode, tf, tr);
     const uint64_t lo = offs[0], hi = offs[n];
-    const uint64_t nchunks = (hi - lo + kStrandChunk - 1) / kStrandChunk;
+    const uint64_t lo4 = lo & ~3ull;
+    const bool aligned = (reinterpret_cast<uintptr_t>(seqs) & 3) == 0;
+    const uint64_t nchunks = (hi - lo4 + kStrandChunk - 1) / kStrandChunk;
     for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const uint64_t start = lo + ch * kStrandChunk;
-        const uint64_t end = min(start + kStrandChunk, hi);
+        const uint64_t start = lo4 + ch * kStrandChunk;
         __syncthreads();
-        if (threadIdx.x == 0) {  // last read r with offs[r] <= start
-            uint64_t a = 0, b = n;  // offs[a] <= start < offs[b]
-            while (b - a > 1) {
-                const uint64_t m = (a + b) >> 1;
-                if (offs[m] <= start) a = m; else b = m;
+        const uint64_t r0 = chunk_first[ch];
+        const uint64_t r1 = ch + 1 < nchunks ? chunk_first[ch + 1] : n - 1;
+        const uint64_t nr = r1 - r0 + 1;  // reads overlapping the chunk (+ at most one)
+        const bool staged = nr <= kStrandMaxReads;
+        if (staged)
+            for (uint64_t i = threadIdx.x; i <= nr; i += blockDim.x) s_off[i] = offs[r0 + i];
+        __syncthreads();
+        uint64_t r = r0, rs = offs[r0], re = offs[r0 + 1];
+        for (uint32_t it = 0; it < kStrandIters; ++it) {
+            const uint64_t p0 = start + ((uint64_t)it * 256 + threadIdx.x) * 4;
+            if (p0 >= hi) break;
+            if (p0 >= lo) {
+                if (staged) {  // read containing p0: last staged offset <= p0
+                    uint32_t a = 0, b = (uint32_t)nr;
+                    while (b - a > 1) {
+                        const uint32_t m = (a + b) >> 1;
+                        if (s_off[m] <= p0) a = m; else b = m;
+                    }
+                    r = r0 + a;
+                    rs = s_off[a];
+                    re = s_off[a + 1];
+                } else {
+                    while (re <= p0) { ++r; rs = re; re = offs[r + 1]; }
+                }
             }
-            s_r0 = a;
-        }
-        __syncthreads();
-        uint64_t r = s_r0;
-        uint64_t re = offs[r + 1];
-        for (uint64_t i = start + threadIdx.x; i < end; i += blockDim.x) {
-            while (re <= i) { ++r; re = offs[r + 1]; }
-            const uint8_t x = seqs[i];
-            if (fwd) fwd[i] = tf[x];
-            rc[offs[r] + re - 1 - i] = tr[x];
+            uint32_t fw = 0, rw = 0;
+            const uint64_t m0 = rs + re - 1 - p0;  // mirror of p0 inside read r
+            if (aligned && p0 >= lo && p0 + 4 <= re && ((m0 - 3) & ~3ull) + 8 <= hi) {
+                // whole dword inside one read: one forward load, two mirror loads
+                const uint32_t x = *reinterpret_cast<const uint32_t*>(seqs + p0);
+                const uint64_t a = m0 - 3;
+                const uint32_t* pm = reinterpret_cast<const uint32_t*>(seqs + (a & ~3ull));
+                const uint32_t y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pm[1], pm[0], (uint32_t)(a & 3)));
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    fw |= (uint32_t)tf[(x >> (8 * b)) & 0xFF] << (8 * b);
+                    rw |= (uint32_t)tr[(y >> (8 * b)) & 0xFF] << (8 * b);
+                }
+            } else {
+                uint64_t rr = r, rrs = rs, rre = re;
+#pragma unroll
+                for (uint32_t b = 0; b < 4; ++b) {
+                    const uint64_t p = p0 + b;
+                    if (p < lo || p >= hi) continue;
+                    while (rre <= p) { ++rr; rrs = rre; rre = offs[rr + 1]; }
+                    fw |= (uint32_t)tf[seqs[p]] << (8 * b);
+                    rw |= (uint32_t)tr[seqs[rrs + rre - 1 - p]] << (8 * b);
+                }
+            }
+            fwd[p0 >> 2] = fw;
+            rc[p0 >> 2] = rw;
         }
     }
 }
@@ -280,20 +327,32 @@ __device__ __forceinline__ uint64_t num_kmers(uint64_t len, uint32_t k, uint32_t
     return len >= k ? (len - k + step) / step : 0;  // ceil((len-k+1)/step)
 }
 
+// Per read: sampled k-mer count and #units; also the first read of every
+// strands chunk (the read holding byte max(chunk start, offs[0])).
 __global__ void units_kernel(const uint64_t* __restrict__ offs, uint64_t n, uint32_t k,
                              uint32_t step, uint64_t* __restrict__ nk_out,
-                             uint64_t* __restrict__ nseg) {
+                             uint64_t* __restrict__ nseg, uint32_t* __restrict__ chunk_first) {
+    const uint64_t lo = offs[0], lo4 = lo & ~3ull;
     for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
          r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t nk = num_kmers(offs[r + 1] - offs[r], k, step);
+        const uint64_t a = offs[r], b = offs[r + 1];
+        const uint64_t nk = num_kmers(b - a, k, step);
         if (nk_out) nk_out[r] = nk;
         nseg[r] = (nk + kSegKmers - 1) / kSegKmers;
+        if (chunk_first && b > a) {
+            if (a <= lo && lo < b) chunk_first[0] = (uint32_t)r;
+            uint64_t c = (a - lo4 + kStrandChunk - 1) / kStrandChunk;
+            if (c < 1) c = 1;
+            for (; lo4 + c * kStrandChunk < b; ++c) chunk_first[c] = (uint32_t)r;
+        }
     }
 }
 
+// queue[0] = number of units, queue[1] = next unit to hand out (zeroed here,
+// before the probe kernel of the same stream starts).
 __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
                                      const uint64_t* __restrict__ unit_ofs, uint64_t n,
-                                     uint32_t* __restrict__ unit_read, uint64_t* n_units,
+                                     uint32_t* __restrict__ unit_read, uint64_t* queue,
                                      uint32_t* __restrict__ hits_zero, uint64_t D) {
     for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
          r += (uint64_t)gridDim.x * blockDim.x) {
@@ -303,119 +362,288 @@ __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
         // several units (accumulated atomically)
         if (s != 1 && hits_zero)
             for (uint64_t d = 0; d < D; ++d) hits_zero[r * D + d] = 0;
-        if (r == n - 1) *n_units = b + s;
+        if (r == n - 1) {
+            queue[0] = b + s;
+            queue[1] = 0;
+        }
     }
 }
 
+// Hand out kGrab units per atomic to balance ragged reads across waves.
+constexpr uint32_t kGrab = 4;
+
+__device__ __forceinline__ uint64_t grab_units(uint64_t* queue, int lane) {
+    uint64_t base = 0;
+    if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long*>(queue + 1), (unsigned long long)kGrab);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // ------------------------------------------------------------------ counting
-// Adds the per-doc bit counts of this tile's 64 masks (one per lane) for docs
-// [cd0, cd0 + nd) (nd <= 128) to the wave's LDS counters.  Doc cd0+32q+b is
-// bit b of mask word q.  A ballot per doc transposes the 64 masks; its
-// popcount is that doc's count for the tile.
-__device__ __forceinline__ void count_chunk(const uint4& m, uint32_t nd, int lane, uint32_t* acc) {
-    uint32_t tv0 = 0, tv1 = 0;
-    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+// Column popcount of a 32x32 bit matrix held one row per lane of each 32-lane
+// half: five exchange stages (lane ^ 16, 8, 4, 2, 1) transpose the matrix, so
+// lane c then holds column c (bit r = row r's bit c), whose popcount is the
+// number of rows (k-mers) with bit c (doc) set.  Stage s swaps the s-wide bit
+// blocks between partner lanes: 1 shuffle + 1 rotate + 1 bit-select.
+struct Xpose {
+    uint32_t msk[5];  // bfi select: keep own bits (m_s, or ~m_s on the upper lane of a pair)
+    uint32_t rot[4];  // rotate-right that aligns the partner's block (stages 8..1)
+};
+
+__device__ __forceinline__ void xpose_init(int lane, Xpose& X) {
+    const uint32_t ss[5] = {16, 8, 4, 2, 1};
+    const uint32_t mm[5] = {0x0000FFFFu, 0x00FF00FFu, 0x0F0F0F0Fu, 0x33333333u, 0x55555555u};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        if ((uint32_t)(q * 32) >= nd) break;
-#pragma unroll
-        for (int b = 0; b < 32; ++b) {
-            const uint32_t bi = q * 32 + b;
-            if (bi >= nd) break;
-            const int pc = __popcll(__ballot((w[q] >> b) & 1u));
-            if (bi < 64) tv0 = xs_writelane_i32(pc, bi, tv0);
-            else tv1 = xs_writelane_i32(pc, bi - 64, tv1);
-        }
+    for (int i = 0; i < 5; ++i) {
+        const bool upper = (lane & ss[i]) != 0;
+        X.msk[i] = upper ? ~mm[i] : mm[i];
+        if (i > 0) X.rot[i - 1] = upper ? ss[i] : 32 - ss[i];
     }
-    if ((uint32_t)lane < nd) acc[lane] += tv0;
-    if ((uint32_t)lane + 64 < nd) acc[64 + lane] += tv1;
+}
+
+__device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+
+__device__ __forceinline__ uint32_t column_popc32(uint32_t x, const Xpose& X) {
+    uint32_t y;
+    y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);                 // lane ^ 16
+    x = bsel(X.msk[0], x, __builtin_amdgcn_alignbit(y, y, 16));
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8 = lane ^ 8
+    x = bsel(X.msk[1], x, __builtin_amdgcn_alignbit(y, y, X.rot[0]));
+    y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x101F);                 // lane ^ 4
+    x = bsel(X.msk[2], x, __builtin_amdgcn_alignbit(y, y, X.rot[1]));
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2301 = lane ^ 2
+    x = bsel(X.msk[3], x, __builtin_amdgcn_alignbit(y, y, X.rot[2]));
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1032 = lane ^ 1
+    x = bsel(X.msk[4], x, __builtin_amdgcn_alignbit(y, y, X.rot[3]));
+    return (uint32_t)__popc(x);
+}
+
+// Sum of lane l and lane l ^ 32 (the two halves' counts of the same doc).
+__device__ __forceinline__ uint32_t fold_halves(uint32_t v) {
+    return v + (uint32_t)__shfl_xor((int)v, 32, 64);
 }
 
 __device__ __forceinline__ uint4 and4(uint4 a, uint4 b) {
     return make_uint4(a.x & b.x, a.y & b.y, a.z & b.z, a.w & b.w);
 }
 
-// ------------------------------------------------------------------ COBS probe
-// One wavefront per unit (<= kSegKmers k-mers of one read), one lane per k-mer.
+// Canonical k-mer of read position p (byte offset o0 of a read of length len).
+template <int KT>
+__device__ __forceinline__ void kmer_at(const ReadView& rv, uint64_t o0, uint64_t len, uint64_t p,
+                                        uint32_t k, Kmer& c) {
+    uint32_t f[8], q[8];
+    load_window<KT>(rv.fwd, o0 + p, k, f);
+    load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
+    canonical_select(f, q, c);
+}
+
+// ------------------------------------------------------------------ COBS probe (fast)
+// Classic bank with D <= 128 docs: one 16-byte row per hash, counters in
+// registers.  One wavefront per unit (<= kSegKmers k-mers of one read), one
+// lane per k-mer; units are handed out kGrab at a time.
+struct FastBank {
+    const uint8_t* rows;
+    uint64_t sig, magic;
+    uint32_t D, nwords;  // nwords = ceil(D/32)
+    uint32_t image_bytes;
+};
+
+// Row gather policies (XSPECT_AMD_LOADPOL): 0 global_load_dwordx4; buffer_load
+// with cache-policy aux 1: none, 2: nt, 3: sc1, 4: sc0 sc1 (L1 bypass forms).
+template <int POL>
+__device__ __forceinline__ uint4 load_row(const FastBank& fb, uint32_t off) {
+    if constexpr (POL == 0) {
+        return *reinterpret_cast<const uint4*>(fb.rows + off);
+    } else {
+        constexpr int aux = POL == 1 ? 0 : POL == 2 ? 2 : POL == 3 ? 16 : 17;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(fb.rows), (short)0,
+                                                            (int)fb.image_bytes, 0x00020000);
+        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, aux);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    }
+}
+
+template <int KT, int HT, int POL>
+__global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv, FastBank fb,
+                                                                    uint32_t* __restrict__ hits,
+                                                                    uint64_t* __restrict__ partials) {
+    __shared__ uint64_t s_tot[kProbeThreads / kWave][128];
+    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    s_tot[wid][lane] = 0;
+    s_tot[wid][lane + 64] = 0;
+    Xpose X;
+    xpose_init(lane, X);
+    const uint32_t k = KT ? KT : rv.k;
+    const uint32_t step = rv.step;
+    const uint32_t D = fb.D, nwords = fb.nwords;
+    const uint64_t U = rv.queue[0];
+    uint64_t kmer_total = 0;
+
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, step);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            kmer_total += cnt;
+            uint32_t a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                uint4 m = make_uint4(0u, 0u, 0u, 0u);
+                if (tb + lane < cnt) {
+                    Kmer c;
+                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    Xxh64Pre pre;
+                    xxh64_pre<KT>(c, k, pre);
+                    uint32_t off[HT];
+#pragma unroll
+                    for (int j = 0; j < HT; ++j)
+                        off[j] = (uint32_t)fastmod(xxh64_seed<KT>(c, pre, k, (uint64_t)j), fb.sig, fb.magic) * 16u;
+                    m = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+                    for (int j = 0; j < HT; ++j)
+                        m = and4(m, load_row<POL>(fb, off[j]));
+                }
+                a0 += column_popc32(m.x, X);
+                if (nwords > 1) a1 += column_popc32(m.y, X);
+                if (nwords > 2) a2 += column_popc32(m.z, X);
+                if (nwords > 3) a3 += column_popc32(m.w, X);
+            }
+            // lane c < 32 holds doc 32q + c of word q after folding the halves
+            const bool whole = nk <= kSegKmers;
+            const uint32_t acc[4] = {a0, a1, a2, a3};
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) {
+                if (q >= nwords) break;
+                const uint32_t v = fold_halves(acc[q]);
+                const uint32_t d = q * 32 + (uint32_t)lane;
+                if (lane < 32 && d < D) {
+                    s_tot[wid][d] += v;
+                    if (hits) {
+                        if (whole) hits[(uint64_t)r * D + d] = v;
+                        else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                    }
+                }
+            }
+        }
+    }
+    if (partials) {
+        if (lane == 0) s_kmers[wid] = kmer_total;
+        __syncthreads();
+        const int wpb = blockDim.x >> 6;
+        uint64_t* out = partials + (uint64_t)blockIdx.x * (D + 1);
+        for (uint32_t d = threadIdx.x; d < D; d += blockDim.x) {
+            uint64_t s = 0;
+            for (int w = 0; w < wpb; ++w) s += s_tot[w][d];
+            out[d] = s;
+        }
+        if (threadIdx.x == 0) {
+            uint64_t s = 0;
+            for (int w = 0; w < wpb; ++w) s += s_kmers[w];
+            out[D] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ COBS probe (general)
+// Any D (LDS counters), compact doc groups, up to kMaxChunks 16-byte chunks per
+// row.  Same unit scheme and column-popcount counting as the fast kernel.
 template <int KT, int HT>
 __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, CobsView bv,
                                                                    uint32_t* __restrict__ hits,
                                                                    uint64_t* __restrict__ partials,
                                                                    uint32_t dpad) {
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int wpb = blockDim.x >> 6;
-    uint32_t* acc = smem + (size_t)wid * 2 * dpad;
-    uint32_t* tot = acc + dpad;
-    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
+    uint32_t* acc = smem + (size_t)wid * 2 * dpad;  // per unit
+    uint32_t* tot = acc + dpad;                     // per wave
     for (uint32_t d = lane; d < 2 * dpad; d += 64) acc[d] = 0;
+    Xpose X;
+    xpose_init(lane, X);
 
     const uint32_t k = KT ? KT : rv.k;
     const uint32_t h = HT ? HT : bv.h;
     const uint32_t step = rv.step;
     const uint64_t D = bv.D;
-    const uint64_t U = *rv.n_units;
+    const uint64_t U = rv.queue[0];
     uint64_t kmer_total = 0;
 
-    for (uint64_t u = (uint64_t)blockIdx.x * wpb + wid; u < U; u += (uint64_t)gridDim.x * wpb) {
-        const uint32_t r = rv.unit_read[u];
-        const uint64_t seg = u - rv.unit_ofs[r];
-        const uint64_t o0 = rv.offs[r];
-        const uint64_t len = rv.offs[r + 1] - o0;
-        const uint64_t nk = num_kmers(len, k, step);
-        const uint64_t t0 = seg * kSegKmers;
-        const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
-        const bool whole = nk <= kSegKmers;
-        kmer_total += cnt;
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, step);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            const bool whole = nk <= kSegKmers;
+            kmer_total += cnt;
 
-        for (uint32_t tb = 0; tb < cnt; tb += 64) {
-            const bool act = tb + lane < cnt;
-            uint64_t hv[HT ? HT : kMaxHashes];
-            if (act) {
-                const uint64_t p = (t0 + tb + lane) * step;  // k-mer start within the read
-                uint32_t f[8], q[8];
-                load_window<KT>(rv.fwd, o0 + p, k, f);
-                load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
-                Kmer c;
-                canonical_select(f, q, c);
-                Xxh64Pre pre;
-                xxh64_pre<KT>(c, k, pre);
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                const bool act = tb + lane < cnt;
+                uint64_t hv[HT ? HT : kMaxHashes];
+                if (act) {
+                    Kmer c;
+                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    Xxh64Pre pre;
+                    xxh64_pre<KT>(c, k, pre);
 #pragma unroll
-                for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
-                    if (j < h) hv[j] = xxh64_seed<KT>(c, pre, k, j);
-            }
-            for (uint32_t g = 0; g < bv.G; ++g) {
-                const GroupDesc gd = bv.groups[g];
-                const uint64_t doc0 = (uint64_t)g * 8 * bv.page;
-                const uint64_t dlim = min(D, doc0 + 8 * bv.page);
-                uint64_t ro[HT ? HT : kMaxHashes];
+                    for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
+                        if (j < h) hv[j] = xxh64_seed<KT>(c, pre, k, j);
+                }
+                for (uint32_t g = 0; g < bv.G; ++g) {
+                    const GroupDesc gd = bv.groups[g];
+                    const uint64_t doc0 = (uint64_t)g * 8 * bv.page;
+                    const uint64_t dlim = min(D, doc0 + 8 * bv.page);
+                    uint64_t ro[HT ? HT : kMaxHashes];
 #pragma unroll
-                for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
-                    if (j < h) ro[j] = act ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
-                for (uint32_t cc = 0; cc < bv.nchunks; ++cc) {
-                    const uint64_t cd0 = doc0 + (uint64_t)cc * 128;
-                    if (cd0 >= dlim) break;
-                    uint4 m = make_uint4(0u, 0u, 0u, 0u);
-                    if (act) {
-                        m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
+                        if (j < h) ro[j] = act ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
+                    for (uint32_t cc = 0; cc < bv.nchunks; ++cc) {
+                        const uint64_t cd0 = doc0 + (uint64_t)cc * 128;
+                        if (cd0 >= dlim) break;
+                        uint4 m = make_uint4(0u, 0u, 0u, 0u);
+                        if (act) {
+                            m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
-                        for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
-                            if (j < h)
-                                m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                            for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
+                                if (j < h)
+                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                        }
+                        const uint32_t nd = (uint32_t)min((uint64_t)128, dlim - cd0);
+                        const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+                        for (uint32_t q = 0; q < 4; ++q) {
+                            if (q * 32 >= nd) break;
+                            const uint32_t v = fold_halves(column_popc32(w[q], X));
+                            if (lane < 32 && q * 32 + lane < nd) acc[cd0 + q * 32 + lane] += v;
+                        }
                     }
-                    count_chunk(m, (uint32_t)min((uint64_t)128, dlim - cd0), lane, acc + cd0);
                 }
             }
-        }
-        // unit done: move counters to the hit matrix and the wave totals
-        for (uint64_t d = lane; d < D; d += 64) {
-            const uint32_t v = acc[d];
-            acc[d] = 0;
-            tot[d] += v;
-            if (hits) {
-                if (whole) hits[(uint64_t)r * D + d] = v;
-                else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+            for (uint64_t d = lane; d < D; d += 64) {
+                const uint32_t v = acc[d];
+                acc[d] = 0;
+                tot[d] += v;
+                if (hits) {
+                    if (whole) hits[(uint64_t)r * D + d] = v;
+                    else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                }
             }
         }
     }
@@ -439,17 +667,15 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 // ------------------------------------------------------------------ rbloom probe
 template <int KT>
 __device__ __forceinline__ bool bloom_member(const Kmer& c, uint32_t k, const BloomView& bv) {
-    const uint64_t hsh = xxh3_kmer<KT>(c, k);
-    uint64_t sl = hsh, sh = 0;
+    uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
     bool in = true;
     for (uint32_t j = 0; j < bv.K; ++j) {
         const uint64_t p = sl * kLcgMl;
         const uint64_t nl = p + kLcgCl;
         const uint64_t carry = nl < p;
-        const uint64_t nh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
+        sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
         sl = nl;
-        sh = nh;
-        const uint64_t idx = fastmod(nh, bv.mbits, bv.magic);
+        const uint64_t idx = fastmod(sh, bv.mbits, bv.magic);
         in = in && ((bv.bits[idx >> 5] >> (idx & 31)) & 1u);
     }
     return in;
@@ -465,36 +691,37 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
     __shared__ uint64_t s_hits[kProbeThreads / kWave], s_kmers[kProbeThreads / kWave];
     const uint32_t k = KT ? KT : rv.k;
     const uint32_t step = rv.step;
-    const uint64_t U = *rv.n_units;
+    const uint64_t U = rv.queue[0];
     uint64_t hit_total = 0, kmer_total = 0;
 
-    for (uint64_t u = (uint64_t)blockIdx.x * wpb + wid; u < U; u += (uint64_t)gridDim.x * wpb) {
-        const uint32_t r = rv.unit_read[u];
-        const uint64_t seg = u - rv.unit_ofs[r];
-        const uint64_t o0 = rv.offs[r];
-        const uint64_t len = rv.offs[r + 1] - o0;
-        const uint64_t nk = num_kmers(len, k, step);
-        const uint64_t t0 = seg * kSegKmers;
-        const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
-        uint32_t c_unit = 0;
-        for (uint32_t tb = 0; tb < cnt; tb += 64) {
-            bool in = false;
-            if (tb + lane < cnt) {
-                const uint64_t p = (t0 + tb + lane) * step;
-                uint32_t f[8], q[8];
-                load_window<KT>(rv.fwd, o0 + p, k, f);
-                load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
-                Kmer c;
-                canonical_select(f, q, c);
-                in = bloom_member<KT>(c, k, bv);
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, step);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            uint32_t c_unit = 0;
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                bool in = false;
+                if (tb + lane < cnt) {
+                    Kmer c;
+                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    in = bloom_member<KT>(c, k, bv);
+                }
+                c_unit += (uint32_t)__popcll(__ballot(in));
             }
-            c_unit += (uint32_t)__popcll(__ballot(in));
-        }
-        kmer_total += cnt;
-        hit_total += c_unit;
-        if (hits && lane == 0) {
-            if (nk <= kSegKmers) hits[r] = c_unit;
-            else if (c_unit) atomicAdd(&hits[r], c_unit);
+            kmer_total += cnt;
+            hit_total += c_unit;
+            if (hits && lane == 0) {
+                if (nk <= kSegKmers) hits[r] = c_unit;
+                else if (c_unit) atomicAdd(&hits[r], c_unit);
+            }
         }
     }
     if (partials) {
@@ -517,37 +744,36 @@ __global__ void __launch_bounds__(kProbeThreads) build_cobs_kernel(ReadView rv,
                                                                    const uint32_t* __restrict__ rec_doc,
                                                                    CobsView bv, uint32_t* rows) {
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int wpb = blockDim.x >> 6;
     const uint32_t k = KT ? KT : rv.k;
     const uint32_t h = HT ? HT : bv.h;
-    const uint64_t U = *rv.n_units;
-    for (uint64_t u = (uint64_t)blockIdx.x * wpb + wid; u < U; u += (uint64_t)gridDim.x * wpb) {
-        const uint32_t r = rv.unit_read[u];
-        const uint64_t seg = u - rv.unit_ofs[r];
-        const uint64_t o0 = rv.offs[r];
-        const uint64_t len = rv.offs[r + 1] - o0;
-        const uint64_t nk = num_kmers(len, k, 1);
-        const uint64_t t0 = seg * kSegKmers;
-        const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
-        const uint64_t doc = rec_doc[r];
-        const uint64_t g = doc / (8 * bv.page), bit = doc % (8 * bv.page);
-        if (doc >= bv.D) continue;
-        const GroupDesc gd = bv.groups[g];
-        for (uint32_t tb = 0; tb < cnt; tb += 64) {
-            if (tb + lane >= cnt) continue;
-            const uint64_t p = t0 + tb + lane;
-            uint32_t f[8], q[8];
-            load_window<KT>(rv.fwd, o0 + p, k, f);
-            load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
-            Kmer c;
-            canonical_select(f, q, c);
-            Xxh64Pre pre;
-            xxh64_pre<KT>(c, k, pre);
-            for (uint32_t j = 0; j < h; ++j) {
-                const uint64_t row = fastmod(xxh64_seed<KT>(c, pre, k, j), gd.sig, gd.magic);
-                const uint64_t byte = gd.base + row * bv.pitch + (bit >> 3);
-                atomicOr(&rows[byte >> 2], 1u << (bit & 31));
+    const uint64_t U = rv.queue[0];
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, 1);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            const uint64_t doc = rec_doc[r];
+            if (doc >= bv.D) continue;
+            const uint64_t g = doc / (8 * bv.page), bit = doc % (8 * bv.page);
+            const GroupDesc gd = bv.groups[g];
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                if (tb + lane >= cnt) continue;
+                Kmer c;
+                kmer_at<KT>(rv, o0, len, t0 + tb + lane, k, c);
+                Xxh64Pre pre;
+                xxh64_pre<KT>(c, k, pre);
+                for (uint32_t j = 0; j < h; ++j) {
+                    const uint64_t row = fastmod(xxh64_seed<KT>(c, pre, k, j), gd.sig, gd.magic);
+                    const uint64_t byte = gd.base + row * bv.pitch + (bit >> 3);
+                    atomicOr(&rows[byte >> 2], 1u << (bit & 31));
+                }
             }
         }
     }
@@ -557,48 +783,56 @@ template <int KT>
 __global__ void __launch_bounds__(kProbeThreads) build_bloom_kernel(ReadView rv, BloomView bv,
                                                                     uint32_t* bits) {
     const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int wpb = blockDim.x >> 6;
     const uint32_t k = KT ? KT : rv.k;
-    const uint64_t U = *rv.n_units;
-    for (uint64_t u = (uint64_t)blockIdx.x * wpb + wid; u < U; u += (uint64_t)gridDim.x * wpb) {
-        const uint32_t r = rv.unit_read[u];
-        const uint64_t seg = u - rv.unit_ofs[r];
-        const uint64_t o0 = rv.offs[r];
-        const uint64_t len = rv.offs[r + 1] - o0;
-        const uint64_t nk = num_kmers(len, k, 1);
-        const uint64_t t0 = seg * kSegKmers;
-        const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
-        for (uint32_t tb = 0; tb < cnt; tb += 64) {
-            if (tb + lane >= cnt) continue;
-            const uint64_t p = t0 + tb + lane;
-            uint32_t f[8], q[8];
-            load_window<KT>(rv.fwd, o0 + p, k, f);
-            load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
-            Kmer c;
-            canonical_select(f, q, c);
-            uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
-            for (uint32_t j = 0; j < bv.K; ++j) {
-                const uint64_t pm = sl * kLcgMl;
-                const uint64_t nl = pm + kLcgCl;
-                const uint64_t carry = nl < pm;
-                sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
-                sl = nl;
-                const uint64_t idx = fastmod(sh, bv.mbits, bv.magic);
-                atomicOr(&bits[idx >> 5], 1u << (idx & 31));
+    const uint64_t U = rv.queue[0];
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, 1);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                if (tb + lane >= cnt) continue;
+                Kmer c;
+                kmer_at<KT>(rv, o0, len, t0 + tb + lane, k, c);
+                uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
+                for (uint32_t j = 0; j < bv.K; ++j) {
+                    const uint64_t pm = sl * kLcgMl;
+                    const uint64_t nl = pm + kLcgCl;
+                    const uint64_t carry = nl < pm;
+                    sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
+                    sl = nl;
+                    const uint64_t idx = fastmod(sh, bv.mbits, bv.magic);
+                    atomicOr(&bits[idx >> 5], 1u << (idx & 31));
+                }
             }
         }
     }
 }
 
 // ------------------------------------------------------------------ misc
-__global__ void reduce_partials_kernel(const uint64_t* __restrict__ partials, int blocks,
-                                       uint64_t cols, uint64_t* __restrict__ totals) {
-    for (uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; c < cols;
-         c += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t s = 0;
-        for (int b = 0; b < blocks; ++b) s += partials[(uint64_t)b * cols + c];
-        totals[c] = s;
+// One block per column: sum of the per-block partial totals.
+__global__ void __launch_bounds__(256) reduce_partials_kernel(const uint64_t* __restrict__ partials,
+                                                              int blocks, uint64_t cols,
+                                                              uint64_t* __restrict__ totals) {
+    __shared__ uint64_t s[256];
+    for (uint64_t c = blockIdx.x; c < cols; c += gridDim.x) {
+        uint64_t v = 0;
+        for (int b = threadIdx.x; b < blocks; b += blockDim.x) v += partials[(uint64_t)b * cols + c];
+        s[threadIdx.x] = v;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+            __syncthreads();
+        }
+        if (threadIdx.x == 0) totals[c] = s[0];
+        __syncthreads();
     }
 }
 
@@ -634,25 +868,43 @@ static inline int grid_for(uint64_t work, int per_block, int cap) {
     return (int)g;
 }
 
+// Resident blocks of `kernel` on the current device (blocks per CU x CUs),
+// minus one block per CU of margin where the occupancy API over-reports
+// (MI355X_MICROARCH.md, residency) — the work queue makes any grid correct;
+// this only avoids a straggling second round.
+template <class K>
+static int resident_grid(K kernel, int threads, size_t lds) {
+    int dev = 0, per_cu = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 1024;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+    return per_cu * prop.multiProcessorCount;
+}
+
+uint64_t strand_chunk_slots(uint64_t nbytes) { return nbytes / kStrandChunk + 3; }
+
 hipError_t launch_strands(const uint8_t* seqs, const uint64_t* offs, uint64_t n, uint64_t nbytes,
-                          int mode, uint8_t* fwd_out, uint8_t* rc_out, hipStream_t s) {
+                          int mode, uint8_t* fwd_out, uint8_t* rc_out, const uint32_t* chunk_first,
+                          hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const int grid = grid_for(nbytes / kStrandChunk + 1, 1, 4096);
-    strands_kernel<<<grid, 256, 0, s>>>(seqs, offs, n, mode, fwd_out, rc_out);
+    const int grid = grid_for(nbytes / kStrandChunk + 1, 1, 8192);
+    strands_kernel<<<grid, 256, 0, s>>>(seqs, offs, n, mode, reinterpret_cast<uint32_t*>(fwd_out),
+                                        reinterpret_cast<uint32_t*>(rc_out), chunk_first);
     return hipGetLastError();
 }
 
 hipError_t launch_units(const uint64_t* offs, uint64_t n, uint32_t k, uint32_t step,
-                        uint64_t* nk_out, uint64_t* nseg, hipStream_t s) {
+                        uint64_t* nk_out, uint64_t* nseg, uint32_t* chunk_first, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    units_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(offs, n, k, step, nk_out, nseg);
+    units_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(offs, n, k, step, nk_out, nseg, chunk_first);
     return hipGetLastError();
 }
 
 size_t scan_temp_bytes(uint64_t n) {
     size_t bytes = 0;
-    hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr, (uint64_t*)nullptr,
-                                     (int)n);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, (const uint64_t*)nullptr,
+                                           (uint64_t*)nullptr, (int)n);
     return bytes;
 }
 
@@ -663,11 +915,11 @@ hipError_t launch_scan(void* temp, size_t temp_bytes, const uint64_t* in, uint64
 }
 
 hipError_t launch_scatter_units(const uint64_t* nseg, const uint64_t* unit_ofs, uint64_t n,
-                                uint32_t* unit_read, uint64_t* n_units, uint32_t* hits_zero,
+                                uint32_t* unit_read, uint64_t* queue, uint32_t* hits_zero,
                                 uint64_t D, hipStream_t s) {
-    if (n == 0) return hipMemsetAsync(n_units, 0, sizeof(uint64_t), s);
+    if (n == 0) return hipMemsetAsync(queue, 0, 2 * sizeof(uint64_t), s);
     scatter_units_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(nseg, unit_ofs, n, unit_read,
-                                                               n_units, hits_zero, D);
+                                                               queue, hits_zero, D);
     return hipGetLastError();
 }
 
@@ -681,8 +933,35 @@ int probe_blocks(uint64_t D, int* waves_per_block, size_t* lds_bytes) {
     return 0;
 }
 
-// 256 CUs x 8 blocks of 4 waves keep 32 waves per CU in flight.
-constexpr int kProbeGridCap = 256 * 8;
+// The fast kernel covers classic banks of <= 128 docs whose image fits 32-bit
+// row offsets, for the (k, h) pairs XspecT trains (species 21/7, MLST 31/1).
+static bool cobs_fast(const CobsView& bv, uint32_t k) {
+    return bv.G == 1 && bv.nchunks == 1 && bv.D <= 128 && bv.sig0 <= (1ull << 28) &&
+           ((k == 21 && bv.h == 7) || (k == 31 && bv.h == 1));
+}
+
+static int load_policy() {
+    static int pol = -1;
+    if (pol < 0) {
+        const char* e = getenv("XSPECT_AMD_LOADPOL");
+        pol = e ? atoi(e) : 0;
+        if (pol < 0 || pol > 4) pol = 0;
+    }
+    return pol;
+}
+
+template <int KT, int HT>
+static hipError_t launch_fast_t(const ReadView& rv, const FastBank& fb, uint32_t* hits,
+                                uint64_t* partials, int blocks, hipStream_t s) {
+    switch (load_policy()) {
+        case 1: probe_cobs_fast<KT, HT, 1><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
+        case 2: probe_cobs_fast<KT, HT, 2><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
+        case 3: probe_cobs_fast<KT, HT, 3><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
+        case 4: probe_cobs_fast<KT, HT, 4><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
+        default: probe_cobs_fast<KT, HT, 0><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
+    }
+    return hipGetLastError();
+}
 
 template <int KT, int HT>
 static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t* hits,
@@ -692,17 +971,49 @@ static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t
     return hipGetLastError();
 }
 
+// Grid of the probe kernel launch_probe_cobs picks for this bank (partials
+// are sized by it).  Cached per variant; every device of a run is an MI355X.
+int probe_grid_cobs(const CobsView& bv, uint32_t k) {
+    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0};
+    if (cobs_fast(bv, k)) {
+        if (k == 21)
+            return fast21 ? fast21 : (fast21 = resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0));
+        return fast31 ? fast31 : (fast31 = resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0));
+    }
+    int wpb;
+    size_t lds;
+    if (probe_blocks(bv.D, &wpb, &lds) != 0) return 0;
+    const int slot = wpb == 4 ? 0 : wpb == 2 ? 1 : 2;
+    if (!generic[slot]) generic[slot] = resident_grid(probe_cobs_kernel<0, 0>, wpb * kWave, lds);
+    return generic[slot];
+}
+
 hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* hits,
                              uint64_t* partials, int blocks, hipStream_t s) {
+    if (cobs_fast(bv, rv.k)) {
+        FastBank fb;
+        fb.rows = bv.rows;
+        fb.sig = bv.sig0;
+        fb.magic = barrett_magic(bv.sig0);
+        fb.D = (uint32_t)bv.D;
+        fb.nwords = (uint32_t)((bv.D + 31) / 32);
+        fb.image_bytes = (uint32_t)min(bv.sig0 * 16ull, 0xFFFFFFFFull);
+        if (rv.k == 21) return launch_fast_t<21, 7>(rv, fb, hits, partials, blocks, s);
+        return launch_fast_t<31, 1>(rv, fb, hits, partials, blocks, s);
+    }
     int wpb;
     size_t lds;
     if (probe_blocks(bv.D, &wpb, &lds) != 0) return hipErrorInvalidValue;
     const uint32_t dpad = (uint32_t)((bv.D + 127) / 128 * 128);
     if (rv.k == 21 && bv.h == 7) return launch_cobs_t<21, 7>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
     if (rv.k == 31 && bv.h == 1) return launch_cobs_t<31, 1>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
-    if (rv.k == 21 && bv.h == 1) return launch_cobs_t<21, 1>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
-    if (rv.k == 31 && bv.h == 7) return launch_cobs_t<31, 7>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
     return launch_cobs_t<0, 0>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
+}
+
+int probe_grid_bloom() {
+    static int cache = 0;
+    if (!cache) cache = resident_grid(probe_bloom_kernel<21>, kProbeThreads, 0);
+    return cache;
 }
 
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
@@ -714,7 +1025,7 @@ hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t*
 
 hipError_t launch_reduce_partials(const uint64_t* partials, int blocks, uint64_t cols,
                                   uint64_t* totals, hipStream_t s) {
-    reduce_partials_kernel<<<grid_for(cols, 256, 1024), 256, 0, s>>>(partials, blocks, cols, totals);
+    reduce_partials_kernel<<<grid_for(cols, 1, 4096), 256, 0, s>>>(partials, blocks, cols, totals);
     return hipGetLastError();
 }
 
