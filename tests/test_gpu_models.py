@@ -1,0 +1,229 @@
+"""The drop-in model classes on the GPU, checked against the oracle (GPU).
+
+Mirrors the reference's model tests (tests/test_probabilistic_filter_model.py,
+test_probabilistic_single_filter_model.py, test_probabilistic_filter_svm_model.py,
+test_probabilistic_filter_mlst_model.py) with synthetic genomes in place of
+the NCBI / PubMLST downloads, and expected hits from the CPU oracle.
+"""
+from __future__ import annotations
+
+import json
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from xspect_amd.file_io import Record, get_record_iterator, write_fasta
+from xspect_amd.synth import make_genomes
+
+pytestmark = pytest.mark.gpu
+
+K = 21
+
+
+@pytest.fixture(scope="module")
+def genomes():
+    return make_genomes(4, 30_000, seed=11)
+
+
+@pytest.fixture
+def species_dir(tmp_path, genomes):
+    d = tmp_path / "species"
+    d.mkdir()
+    names = ["GCF_000006945.2_ASM694v2_genomic", "GCF_000018445.1_ASM1844v1_genomic",
+             "GCF_000069245.1_ASM6924v1_genomic", "GCF_000099999.1_X_genomic"]
+    for i, n in enumerate(names):
+        g = genomes[i].tobytes().decode()
+        # two contigs per species, the second with lower-case and N runs
+        write_fasta([Record(f"c{i}a", g[:20_000]), Record(f"c{i}b", g[20_000:25_000].lower() + "NNNN" + g[25_000:])],
+                    d / f"{n}.fna", width=80)
+    return d
+
+
+def _oracle_species(oracle_mod, species_dir, k=K, h=7, fpr=0.01):
+    files = sorted(species_dir.iterdir())
+    seqs, docs = [], []
+    for d, f in enumerate(files):
+        for r in get_record_iterator(f):
+            seqs.append(r.seq)
+            docs.append(d)
+    terms = [sum(max(0, len(s) - k + 1) for s, dd in zip(seqs, docs) if dd == d) for d in range(len(files))]
+    sig = oracle_mod.signature_size(max(terms), h, fpr)
+    ob = oracle_mod.CobsBank.empty([sig], (len(files) + 7) // 8, len(files), h, k)
+    ob.build(seqs, docs)
+    return ob, [f.stem.split(".")[0] for f in files]
+
+
+def _expected_hits(ob, names, seqs, step=1, exclude=None):
+    h, nk = ob.query(seqs, step=step)
+    out = []
+    for row in h:
+        order = np.argsort(-row.astype(np.int64), kind="stable")
+        d = {names[i]: int(row[i]) for i in order}
+        if exclude:
+            d = {a: b for a, b in d.items() if a not in exclude}
+        out.append(d)
+    return out, nk
+
+
+def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mod):
+    from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
+
+    base = tmp_path / "xspect_data"
+    model = ProbabilisticFilterModel(K, "Test Filter", "John Doe", "j@x", "Species", base)
+    model.fit(species_dir)
+    assert model.display_names["GCF_000006945"] == "GCF_000006945.2_ASM694v2_genomic"
+    assert (base / "test-filter-species" / "index.cobs_classic").exists()
+    ob, names = _oracle_species(oracle_mod, species_dir)
+    assert np.array_equal(model.index.download(), ob.rows), "GPU-built index differs from oracle"
+
+    g0 = genomes[0].tobytes().decode()
+    read = g0[1000:1080]  # an 80 bp read of doc 0 -> 60 k-mers (reference :73-93)
+    hits = model.calculate_hits(read)
+    assert hits["GCF_000006945"] == 60 and list(hits)[0] == "GCF_000006945"
+    for step in range(1, 5):
+        assert model.calculate_hits(read, step=step)["GCF_000006945"] == -(-60 // step)
+
+    rng = np.random.default_rng(1)
+    recs = [Record(f"read_{i}", g0[s:s + 150]) for i, s in enumerate(rng.integers(0, 29_000, 50))]
+    recs += [Record("mixed", genomes[1].tobytes().decode()[:5000] + "ACGTN" * 10)]
+    res = model.predict(recs, exclude_ids=["GCF_000099999"])
+    want, nk = _expected_hits(ob, names, [r.seq for r in recs], exclude=["GCF_000099999"])
+    assert list(res.hits) == [r.id for r in recs]
+    for r, w in zip(recs, want):
+        assert res.hits[r.id] == w and list(res.hits[r.id]) == list(w)
+    assert res.num_kmers == {r.id: int(n) for r, n in zip(recs, nk)}
+
+    # Path input, display names, step
+    fa = tmp_path / "reads.fasta"
+    write_fasta(recs, fa)
+    res2 = model.predict(fa, step=3, display_name=True)
+    w3, _ = _expected_hits(ob, names, [r.seq for r in recs], step=3)
+    key = "GCF_000006945 -GCF_000006945.2_ASM694v2_genomic"
+    assert res2.hits["read_0"][key] == w3[0]["GCF_000006945"]
+
+    model.save()
+    loaded = ProbabilisticFilterModel.load(base / "test-filter-species.json")
+    assert loaded.to_dict() == model.to_dict()
+    res3 = loaded.predict(recs)
+    assert res3.get_total_hits() == model.predict(recs).get_total_hits()
+    with pytest.raises(ValueError):
+        loaded.predict([Record("short", "ACGT")])
+
+
+def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
+    from xspect_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+
+    svm_dir = tmp_path / "svm"
+    for i in range(4):
+        for j in range(2):
+            g = genomes[i].tobytes().decode()
+            write_fasta([Record("x", g[j * 7000:j * 7000 + 9000])], svm_dir / f"label{i}" / f"acc{i}{j}.fasta")
+    base = tmp_path / "xspect_data"
+    model = ProbabilisticFilterSVMModel(K, "Acinetobacter", None, None, "Species", base, "rbf", 1.0)
+    model.fit(species_dir, svm_dir, svm_step=1)
+    lines = (base / "acinetobacter-species" / "scores.csv").read_text().splitlines()
+    assert lines[0].startswith("file,GCF_000006945,") and lines[0].endswith(",label_id")
+    for line in lines[1:]:
+        vals = line.split(",")
+        lbl = int(vals[-1][-1])
+        assert float(vals[1 + lbl]) == 1.0       # own genome scores 1.0 (reference :36-59)
+    model.save()
+    loaded = ProbabilisticFilterSVMModel.load(base / "acinetobacter-species.json")
+    g2 = genomes[2].tobytes().decode()
+    res = loaded.predict([Record("q", g2[2000:12_000])], step=5)
+    assert res.prediction == "label2"
+    vec = ProbabilisticFilterSVMModel.svm_vector(loaded.predict([Record("q", g2[2000:12_000])], step=5))
+    assert len(vec) == 4 and vec[2] == 1.0
+
+
+def test_genus_bloom_model(tmp_path, genomes, oracle_mod):
+    from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+
+    fa = tmp_path / "concatenated_assembly.fna"
+    write_fasta([Record("a", genomes[0].tobytes().decode()), Record("b", genomes[1].tobytes().decode())], fa)
+    base = tmp_path / "xspect_data"
+    m = ProbabilisticSingleFilterModel(K, "Test Filter", "J", "j@x", "Species", base)
+    m.fit(fa, "Acinetobacter baumannii")
+    assert m.display_names == {"concatenated_assembly": "Acinetobacter baumannii"}
+    total = 2 * genomes.shape[1]
+    nbytes, kh = oracle_mod.BloomFilter.params(total - K + 1, 0.01)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), kh, K)
+    bf.build([genomes[0].tobytes(), genomes[1].tobytes()])
+    assert np.array_equal(m.bf.download(), bf.bits)
+    g0 = genomes[0].tobytes().decode()
+    q = g0[500:522]  # 22 bp -> 2 k-mers, both inserted (reference :42-45)
+    assert m.calculate_hits(q) == {"concatenated_assembly": 2}
+    rng = np.random.default_rng(3)
+    reads = [g0[s:s + 150] for s in rng.integers(0, 29_000, 20)] + \
+            ["".join(rng.choice(list("ACGTacgtN"), 150)) for _ in range(20)]
+    res = m.predict([Record(f"r{i}", s) for i, s in enumerate(reads)])
+    want, _ = bf.query(reads)
+    assert [res.hits[f"r{i}"]["concatenated_assembly"] for i in range(len(reads))] == want.tolist()
+    m.save()
+    m2 = ProbabilisticSingleFilterModel.load(base / (m.slug() + ".json"))
+    assert m2.to_dict() == m.to_dict()
+    assert m2.calculate_hits(q) == {"concatenated_assembly": 2}
+
+
+def _scheme(tmp_path, rng, loci=3, alleles=40):
+    root = tmp_path / "alleles"
+    base_seqs = {}
+    for li in range(loci):
+        base = "".join(rng.choice(list("ACGT"), 450 + 10 * li))
+        base_seqs[li] = base
+        for a in range(1, alleles + 1):
+            s = list(base)
+            for p in rng.choice(len(s), size=int(rng.integers(0, 12)), replace=False):
+                s[p] = "ACGT"[(("ACGT".index(s[p])) + 1) % 4]
+            write_fasta([Record(f"L{li}_{a}", "".join(s))], root / f"Oxf_L{li}" / f"Allele_ID_{a}.fasta")
+    return root
+
+
+def test_mlst_model(tmp_path, oracle_mod):
+    from xspect_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+
+    rng = np.random.default_rng(5)
+    root = _scheme(tmp_path, rng)
+    base = tmp_path / "xspect_data"
+    m = ProbabilisticFilterMlstSchemeModel(K, "MLST (Oxford)", base, "https://example/schemes/1", "abaumannii")
+    m.strain_type_resolver = lambda flat, url: "ST" + "-".join(str(v) for v in flat.values())
+    m.fit(root, page_size=2)  # 16 alleles per doc group -> 3 groups per locus
+    assert len(m.indices) == 3 and all(v == 40 for v in m.loci.values())
+    # an allele scores its own k-mer count at its locus (reference :82-99, 401 for cpn60 #4)
+    allele = next(get_record_iterator(root / "Oxf_L0" / "Allele_ID_4.fasta")).seq
+    res = m.predict(Record("<unknown id>", allele)).hits["test"]
+    st = res[0]["Strain type"]["Oxf_L0"]
+    assert max(st.values()) == len(allele) - K + 1
+    # the compact bank of locus 0 equals the oracle's, and so do its hit rows
+    bank0 = m.indices[0]
+    assert bank0.info.num_groups == 3
+    seqs = {n: next(get_record_iterator(root / "Oxf_L0" / f"{n}.fasta")).seq for n in bank0.doc_names}
+    order = bank0.doc_names
+    terms = [len(seqs[n]) - K + 1 for n in order]
+    assert terms == sorted(terms)
+    sig = [oracle_mod.signature_size(max(terms[g * 16:(g + 1) * 16]), 1, 0.001) for g in range(3)]
+    ob = oracle_mod.CobsBank.empty(sig, 2, 40, 1, K)
+    ob.build([seqs[n] for n in order], list(range(40)))
+    assert np.array_equal(bank0.download(), ob.rows)
+    q = [seqs[n][10:200] for n in order[:10]] + [allele]
+    assert np.array_equal(bank0.query(q)[0], ob.query(q)[0])
+    # long path: a 12 kbp contig made of alleles of every locus
+    contig = "".join(next(get_record_iterator(root / f"Oxf_L{li}" / "Allele_ID_7.fasta")).seq + "A" * 3000
+                     for li in range(3))
+    out = m.calculate_hits(contig)
+    assert "ST_Name" in out[0]["Strain type"]
+    for li in range(3):
+        top = out[0]["Strain type"][f"Oxf_L{li}"]
+        assert list(top.values())[0] >= 400
+    m.save()
+    m2 = ProbabilisticFilterMlstSchemeModel.load(base / "abaumannii-mlst-oxford-mlst.json")
+    assert m2.loci == m.loci and len(m2.indices) == 3
+    m2.strain_type_resolver = m.strain_type_resolver
+    assert m2.calculate_hits(contig) == out
+    fa = tmp_path / "contigs.fasta"
+    write_fasta([Record("c1", contig), Record("c2", allele)], fa)
+    mr = m2.predict(fa)
+    assert mr.hits["c1"] == out
+    with pytest.raises(ValueError):
+        m2.predict([Record("x", allele)])

@@ -1,0 +1,180 @@
+"""Host-side logic of the drop-in surface (CPU only, no device calls)."""
+from __future__ import annotations
+
+import math
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from xspect_amd import distributed
+from xspect_amd.bank import bloom_parameters, cobs_signature_size
+from xspect_amd.file_io import Record, get_record_iterator, prepare_input_output_paths, write_fasta
+from xspect_amd.packing import pack_fixed, pack_sequences
+from xspect_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel, _batches, cobs_result_order
+from xspect_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+from xspect_amd.util import slugify
+
+
+def _model(tmp_path, **kw):
+    args = dict(k=21, model_display_name="Test Filter", author="John Doe",
+                author_email="john.doe@example.com", model_type="Species", base_path=tmp_path)
+    args.update(kw)
+    return ProbabilisticFilterModel(**args)
+
+
+def test_slugs_match_reference_tests(tmp_path):
+    # tests/test_probabilistic_filter_model.py:125 and test_probabilistic_filter_mlst_model.py:61
+    assert _model(tmp_path).slug() == "test-filter-species"
+    m = ProbabilisticFilterMlstSchemeModel(21, "MLST (Oxford)", tmp_path, "", "abaumannii")
+    assert m.slug() == "abaumannii-mlst-oxford-mlst"
+    assert slugify("Acinetobacter") == "acinetobacter"
+    assert slugify("A  b--c's 1,000") == "a-b-cs-1000"
+
+
+def test_constructor_validation(tmp_path):
+    with pytest.raises(ValueError):
+        _model(tmp_path, k=0)
+    with pytest.raises(ValueError):
+        _model(tmp_path, model_display_name="")
+    with pytest.raises(ValueError):
+        _model(tmp_path, model_type="")
+    with pytest.raises(ValueError):
+        _model(tmp_path, base_path=str(tmp_path))
+    m = _model(tmp_path)
+    assert (m.fpr, m.num_hashes, m.index) == (0.01, 7, None)
+    d = m.to_dict()
+    assert d["model_class"] == "ProbabilisticFilterModel" and d["num_hashes"] == 7
+    s = ProbabilisticFilterSVMModel(21, "T", None, None, "Species", tmp_path, "rbf", 1.0)
+    assert s.to_dict()["kernel"] == "rbf" and s.to_dict()["C"] == 1.0
+    g = ProbabilisticSingleFilterModel(21, "T", None, None, "Genus", tmp_path)
+    assert g.num_hashes == 1
+    mlst = ProbabilisticFilterMlstSchemeModel(21, "S", tmp_path, "u", "org")
+    assert (mlst.fpr, mlst.num_hashes, mlst.model_type) == (0.001, 1, "MLST")
+
+
+def test_count_kmers_known_answer(tmp_path, golden):
+    ka = golden("reference_known_answers.json")["salmonella_80bp"]
+    m = _model(tmp_path)
+    assert m._count_kmers(ka["seq"]) == 60
+    assert m._count_kmers(Record("r", ka["seq"])) == 60
+    assert m._count_kmers([ka["seq"], ka["seq"]], step=2) == 60
+    for step, want in ka["hits_self_by_step"].items():
+        assert m._count_kmers(ka["seq"], step=int(step)) == want
+    with pytest.raises(ValueError):
+        m._count_kmers(42)
+
+
+def test_input_validation_before_device(tmp_path):
+    m = _model(tmp_path)
+    with pytest.raises(ValueError, match="Invalid sequence input"):
+        m.predict(42)
+    with pytest.raises(ValueError, match="longer than k"):
+        m.predict([Record("a", "ACGT" * 5)])  # 20 bp <= k
+    with pytest.raises(ValueError, match="Bio.Seq"):
+        m.calculate_hits(Record("a", "ACGT" * 10))
+    with pytest.raises(ValueError, match="longer than k"):
+        m.calculate_hits("A" * 21)
+    with pytest.raises(NotImplementedError):
+        m.predict([Record("a", "A" * 30)], validation=True)
+
+
+def test_splitter_known_answer_and_oracle(golden, oracle_mod):
+    ka = golden("reference_known_answers.json")["splitter"]
+    m = ProbabilisticFilterMlstSchemeModel(ka["k"], "Test Filter", Path("."), "", "Test Organism")
+    parts = m.sequence_splitter(ka["seq"], ka["allele_len"])
+    assert len(parts) == ka["num_parts"]
+    rng = np.random.default_rng(0)
+    for n in [10_000, 12_345, 999_999, 1_000_000, 1_234_567]:
+        seq = "".join(rng.choice(list("ACGT"), n))
+        m31 = ProbabilisticFilterMlstSchemeModel(31, "S", Path("."), "", "o")
+        assert m31.sequence_splitter(seq, 450) == oracle_mod.sequence_splitter(seq, 450, 31)
+
+
+def test_has_sufficient_score():
+    # tests/test_probabilistic_filter_mlst_model.py:145-177 with Oxford-like sizes
+    m = ProbabilisticFilterMlstSchemeModel(21, "S", Path("."), "", "o")
+    sizes = [402, 305, 483, 456, 457, 372, 456]
+    ok = {"Scores": {"Oxf_cpn60": 265}}
+    bad = {"Scores": {"Oxf_cpn60": 100}}
+    assert m.has_sufficient_score(ok, sizes)
+    assert not m.has_sufficient_score(bad, sizes)
+    assert not m.has_sufficient_score({"a": {}}, sizes)
+
+
+def test_cobs_result_order_is_score_desc_then_index():
+    row = np.array([3, 7, 7, 0, 3], dtype=np.uint32)
+    assert cobs_result_order(row).tolist() == [1, 2, 0, 4, 3]
+
+
+def test_packing_and_batches():
+    pr = pack_sequences(["ACGT", b"", "GG"])
+    assert pr.offsets.tolist() == [0, 4, 4, 6] and pr.buf[:6].tobytes() == b"ACGTGG"
+    pf = pack_fixed(np.frombuffer(b"AAAACCCC", dtype=np.uint8).reshape(2, 4))
+    assert pf.offsets.tolist() == [0, 4, 8] and pf.n == 2
+    import xspect_amd.probabilistic_filter_model as pfm
+    old = pfm.MAX_BATCH_BYTES
+    pfm.MAX_BATCH_BYTES = 10
+    try:
+        assert list(_batches([4, 4, 4, 20, 1])) == [(0, 2), (2, 3), (3, 4), (4, 5)]
+    finally:
+        pfm.MAX_BATCH_BYTES = old
+    assert list(_batches([])) == []
+
+
+def test_fasta_fastq_io(tmp_path):
+    fa = tmp_path / "x.fasta"
+    fa.write_text(">r1 desc\nACGT\nAC\n>r2\n\nGG\n")
+    recs = list(get_record_iterator(fa))
+    assert [(r.id, r.seq) for r in recs] == [("r1", "ACGTAC"), ("r2", "GG")]
+    fq = tmp_path / "x.fq"
+    fq.write_text("@a 1\nACGT\n+\nIIII\n@b\nGG\n+b\nII\n")
+    assert [(r.id, r.seq) for r in get_record_iterator(fq)] == [("a", "ACGT"), ("b", "GG")]
+    with pytest.raises(ValueError):
+        get_record_iterator(tmp_path / "missing.fasta")
+    with pytest.raises(ValueError):
+        get_record_iterator(str(fa))
+    bad = tmp_path / "x.txt"
+    bad.write_text("")
+    with pytest.raises(ValueError):
+        get_record_iterator(bad)
+    write_fasta(recs, tmp_path / "o" / "y.fna", width=3)
+    assert [(r.id, r.seq) for r in get_record_iterator(tmp_path / "o" / "y.fna")] == [("r1", "ACGTAC"), ("r2", "GG")]
+
+
+def test_prepare_input_output_paths(tmp_path):
+    (tmp_path / "a.fasta").write_text(">a\nA\n")
+    (tmp_path / "b.fq").write_text("@b\nA\n+\nI\n")
+    (tmp_path / "c.txt").write_text("")
+    ins, fn = prepare_input_output_paths(tmp_path)
+    assert [p.name for p in ins] == ["a.fasta", "b.fq"]
+    assert fn(1, tmp_path / "out" / "res.json").name == "res_2.json"
+    ins, fn = prepare_input_output_paths(tmp_path / "a.fasta")
+    assert fn(0, tmp_path / "res.json").name == "res.json"
+    with pytest.raises(ValueError):
+        prepare_input_output_paths(tmp_path / "nope")
+
+
+def test_bank_parameter_formulas(oracle_mod):
+    for n, h, f in [(4_000_000, 7, 0.01), (600, 1, 0.001)]:
+        assert cobs_signature_size(n, h, f) == oracle_mod.signature_size(n, h, f)
+    assert bloom_parameters(10_000, 0.01) == oracle_mod.BloomFilter.params(10_000, 0.01)
+    with pytest.raises(ValueError):
+        bloom_parameters(0, 0.01)
+
+
+def test_shard_ranges_cover_exactly():
+    for n in [0, 1, 7, 100, 1001]:
+        for w in [1, 2, 3, 8]:
+            rs = [distributed.shard_range(n, r, w) for r in range(w)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
+            assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+
+
+def test_slice_reads():
+    pr = pack_sequences(["AAA", "CC", "GGGG", "T"])
+    s = distributed.slice_reads(pr, 1, 3)
+    assert s.offsets.tolist() == [0, 2, 6] and s.buf[:6].tobytes() == b"CCGGGG"

@@ -1,0 +1,99 @@
+"""Classification entry points over the GPU models (mirror of ``src/xspect/classify.py``).
+
+Model files are found where XspecT keeps them (``definitions.py:10-46``,
+``model_management.py:27-77``): ``<root>/models/<slug>.json`` with
+``<root>`` = ``~/xspect-data`` or ``./xspect-data`` (or ``$XSPECT_DATA``).
+"""
+from __future__ import annotations
+
+import json
+import os
+from pathlib import Path
+
+from .file_io import prepare_input_output_paths
+from .util import slugify
+
+
+def xspect_root() -> Path:
+    env = os.environ.get("XSPECT_DATA")
+    if env:
+        return Path(env)
+    home = Path.home() / "xspect-data"
+    if home.exists():
+        return home
+    cwd = Path.cwd() / "xspect-data"
+    if cwd.exists():
+        return cwd
+    home.mkdir(parents=True, exist_ok=True)
+    return home
+
+
+def model_dir() -> Path:
+    p = xspect_root() / "models"
+    p.mkdir(parents=True, exist_ok=True)
+    return p
+
+
+def genus_model_path(genus: str) -> Path:
+    return model_dir() / (slugify(genus) + "-genus.json")
+
+
+def species_model_path(genus: str) -> Path:
+    return model_dir() / (slugify(genus) + "-species.json")
+
+
+def mlst_model_path(organism: str, scheme: str) -> Path:
+    return model_dir() / (slugify(organism + "-" + scheme + "-mlst") + ".json")
+
+
+def is_svm_model(model_json: Path) -> bool:
+    if not model_json.exists():
+        raise ValueError(f"Model at {model_json} does not exist.")
+    return json.loads(model_json.read_text(encoding="utf-8")).get("model_class") == \
+        "ProbabilisticFilterSVMModel"
+
+
+def classify_genus(model_genus: str, input_path: Path, output_path: Path, step: int = 1):
+    from .probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+
+    model = ProbabilisticSingleFilterModel.load(genus_model_path(model_genus))
+    inputs, out_path = prepare_input_output_paths(Path(input_path))
+    for idx, current in enumerate(inputs):
+        result = model.predict(current, step=step)
+        result.input_source = current.name
+        path = out_path(idx, Path(output_path))
+        result.save(path)
+        print(f"Saved result as {path.name}")
+
+
+def classify_species(model_genus: str, input_path: Path, output_path: Path, step: int = 1,
+                     display_name: bool = False, validation: bool = False,
+                     exclude_ids: list[str] | None = None):
+    from .probabilistic_filter_model import ProbabilisticFilterModel
+    from .probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+
+    path = species_model_path(model_genus)
+    cls = ProbabilisticFilterSVMModel if is_svm_model(path) else ProbabilisticFilterModel
+    model = cls.load(path)
+    inputs, out_path = prepare_input_output_paths(Path(input_path))
+    for idx, current in enumerate(inputs):
+        result = model.predict(current, exclude_ids=exclude_ids, step=step,
+                               display_name=display_name, validation=validation)
+        result.input_source = current.name
+        path_out = out_path(idx, Path(output_path))
+        result.save(path_out)
+        print(f"Saved result as {path_out.name}")
+
+
+def classify_mlst(input_path: Path, organism: str, mlst_scheme: str, output_path: Path,
+                  limit: bool):
+    from .probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+
+    model = ProbabilisticFilterMlstSchemeModel.load(mlst_model_path(organism, mlst_scheme))
+    inputs, out_path = prepare_input_output_paths(Path(input_path))
+    for idx, current in enumerate(inputs):
+        result = model.predict(current, step=1, limit=limit)
+        result.input_source = current.name
+        path = out_path(idx, Path(output_path))
+        result.save(path)
+        print(f"Saved result as {path.name}")
