@@ -97,7 +97,7 @@ int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32
  * rec_doc[r] (ignored for rbloom; may be NULL there). */
 int xs_bank_build(xs_bank* bank, const char* seqs, const uint64_t* offsets,
                   const uint32_t* rec_doc, uint64_t n_rec);
-/* Same with device-resident buffers, enqueued on `stream` (NULL = bank stream). */
+/* Same with device-resident buffers, enqueued on `stream` (NULL = the null stream). */
 int xs_bank_build_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes,
                          const uint64_t* d_offsets, const uint32_t* d_rec_doc, uint64_t n_rec,
                          void* stream);
@@ -114,6 +114,8 @@ int xs_bank_upload(xs_bank* bank, const void* host, uint64_t nbytes);
 int xs_bank_set_term_size(xs_bank* bank, uint32_t term_size);
 
 int xs_bank_info(const xs_bank* bank, xs_bank_info_t* out);
+/* Signature size of each doc group (num_groups entries; COBS banks only). */
+int xs_bank_signature_sizes(const xs_bank* bank, uint64_t* out, uint64_t n);
 const char* xs_bank_doc_name(const xs_bank* bank, uint64_t i);
 
 /* Probe n reads (host buffers): read r = seqs[offsets[r] .. offsets[r+1]).
@@ -128,7 +130,8 @@ int xs_query(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t 
 int xs_query_totals(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n,
                     uint32_t step, uint64_t* totals_out, uint64_t* total_kmers_out);
 
-/* Device-resident variant, asynchronous on `stream` (NULL = bank stream).
+/* Device-resident variant, asynchronous on `stream` (NULL = the null stream,
+ * ordered with all blocking streams; pass torch.cuda.current_stream().cuda_stream).
  * d_seqs holds seq_bytes bytes; d_offsets n+1 uint64.  Any of d_hits (n x D
  * uint32), d_num_kmers (n uint64) and d_totals (D+1 uint64: per-doc totals then
  * the k-mer total) may be NULL.  The bank must live on the current device. */

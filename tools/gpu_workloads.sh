@@ -1,0 +1,12 @@
+# gpu tests, then every bench workload (default config first, with CPU baseline)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+echo "== tests"; timeout -k 10 600 python -m pytest tests -m gpu -q -x > gpurun_out/gpu_tests.log 2>&1 || { tail -30 gpurun_out/gpu_tests.log; exit 5; }
+tail -1 gpurun_out/gpu_tests.log
+for w in species genus mlst multigenus; do
+  echo "== bench $w"
+  timeout -k 10 600 python bench.py --workload $w > gpurun_out/bench_$w.json 2> gpurun_out/bench_$w.err || { tail -20 gpurun_out/bench_$w.err; exit 6; }
+  python -c "import json;d=json.load(open('gpurun_out/bench_$w.json'));r=d['roofline'];c=d['cpu_baseline'] or {};print('value %.3e probes/s  step %.2f ms  probe %.2f ms x%d  %.0f GB/s frac %.3f  cpu %.3e mism %s'%(d['value'],d['ms_per_step'],r['probe_ms_avg'],r['probe_launches'],r['achieved'],r['frac'],c.get('value',0),c.get('parity_sample_mismatches')))"
+done

@@ -1,11 +1,12 @@
 // randgather.hip — ceiling of random 16-byte row gathers on this GPU.
 //
-// Each lane draws pseudo-random row indices (splitmix64) into a table of
-// `rows` 16-byte rows and ANDs NL rows per "k-mer" (NL loads in flight per
-// lane, as the probe kernel issues its h = 7 row loads).  Reports gathered
-// rows/s and GB/s at 64 B per row (one HBM/MALL transaction per row).
-//   hipcc -O3 --offload-arch=gfx950 tools/randgather.hip -o /tmp/randgather
-//   /tmp/randgather [table_MB ...]
+// Each lane draws pseudo-random row indices into a table of `rows` 16-byte
+// rows and ANDs 7 rows per "k-mer" (7 loads in flight per lane, as the probe
+// kernel issues its h = 7 row loads).  Sweeps the table size, the allocation
+// kind (hipMalloc / fine-grained / uncached: decides the L2 fill size) and the
+// load cache policy (plain, sc1, nt).  Reports rows/s and GB/s at 64 B/row.
+//   hipcc -O3 --offload-arch=gfx950 tools/randgather.hip -o tools/randgather
+//   ./tools/randgather [table_MB ...]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -21,16 +22,12 @@
         }                                                                                   \
     } while (0)
 
-__device__ __forceinline__ uint64_t mix(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
-}
-
-template <int NL>
+template <int NL, int POL>
 __global__ void __launch_bounds__(256) gather(const uint4* __restrict__ tab, uint64_t rows,
                                               uint64_t iters, uint32_t* out) {
     const uint64_t tid = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(tab), (short)0,
+                                                        (int)min(rows * 16, 0xFFFFFFF0ull), 0x00020000);
     uint32_t acc = 0;
     for (uint64_t it = 0; it < iters; ++it) {
         uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
@@ -43,7 +40,14 @@ __global__ void __launch_bounds__(256) gather(const uint4* __restrict__ tab, uin
         }
 #pragma unroll
         for (int j = 0; j < NL; ++j) {
-            const uint4 v = tab[idx[j]];
+            uint4 v;
+            if constexpr (POL == 0) {
+                v = tab[idx[j]];
+            } else {
+                constexpr int aux = POL == 1 ? 16 : 2;  // 1: sc1, 2: nt
+                const auto r = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(idx[j] * 16u), 0, aux);
+                v = make_uint4(r[0], r[1], r[2], r[3]);
+            }
             m.x &= v.x; m.y &= v.y; m.z &= v.z; m.w &= v.w;
         }
         acc += m.x ^ m.y ^ m.z ^ m.w;
@@ -51,48 +55,62 @@ __global__ void __launch_bounds__(256) gather(const uint4* __restrict__ tab, uin
     if (acc == 0x12345678u) out[0] = acc;  // keep the loads live
 }
 
+template <int POL>
+static float run(const uint4* tab, uint64_t rows, int grid, uint64_t iters, uint32_t* out) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    gather<7, POL><<<grid, 256>>>(tab, rows, 2, out);  // warm
+    CHK(hipDeviceSynchronize());
+    CHK(hipEventRecord(a));
+    gather<7, POL><<<grid, 256>>>(tab, rows, iters, out);
+    CHK(hipEventRecord(b));
+    CHK(hipEventSynchronize(b));
+    float ms = 0;
+    CHK(hipEventElapsedTime(&ms, a, b));
+    CHK(hipEventDestroy(a));
+    CHK(hipEventDestroy(b));
+    return ms;
+}
+
 int main(int argc, char** argv) {
     std::vector<double> sizes;
     for (int i = 1; i < argc; ++i) sizes.push_back(atof(argv[i]));
-    if (sizes.empty()) sizes = {16, 64, 200, 614, 2048, 8192};
-    int dev = 0;
+    if (sizes.empty()) sizes = {64, 614, 4096};
     hipDeviceProp_t prop;
-    CHK(hipGetDeviceProperties(&prop, dev));
+    CHK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
     uint32_t* out;
     CHK(hipMalloc(&out, 4));
+    const char* kinds[3] = {"hipMalloc", "finegrained", "uncached"};
+    const unsigned flags[3] = {0, hipDeviceMallocFinegrained, hipDeviceMallocUncached};
+    const char* pols[3] = {"plain", "sc1", "nt"};
     printf("{\"cus\": %d, \"results\": [\n", cus);
     bool first = true;
     for (double mb : sizes) {
         const uint64_t bytes = (uint64_t)(mb * 1048576.0) / 16 * 16;
         const uint64_t rows = bytes / 16;
-        uint4* tab;
-        CHK(hipMalloc(&tab, bytes));
-        CHK(hipMemset(tab, 0xA5, bytes));
-        for (int blocks_per_cu : {4, 8}) {
-            const int grid = cus * blocks_per_cu;
+        for (int kind = 0; kind < 3; ++kind) {
+            uint4* tab = nullptr;
+            if (kind == 0) CHK(hipMalloc(&tab, bytes));
+            else CHK(hipExtMallocWithFlags((void**)&tab, bytes, flags[kind]));
+            CHK(hipMemset(tab, 0xA5, bytes));
+            CHK(hipDeviceSynchronize());
+            const int grid = cus * 4;
             const uint64_t threads = (uint64_t)grid * 256;
             const uint64_t iters = 64;
-            hipEvent_t a, b;
-            CHK(hipEventCreate(&a));
-            CHK(hipEventCreate(&b));
-            gather<7><<<grid, 256>>>(tab, rows, 4, out);  // warm
-            CHK(hipDeviceSynchronize());
-            CHK(hipEventRecord(a));
-            gather<7><<<grid, 256>>>(tab, rows, iters, out);
-            CHK(hipEventRecord(b));
-            CHK(hipEventSynchronize(b));
-            float ms = 0;
-            CHK(hipEventElapsedTime(&ms, a, b));
-            const double loads = (double)threads * iters * 7;
-            printf("%s  {\"table_MB\": %.0f, \"blocks_per_cu\": %d, \"ms\": %.3f, \"Grows_per_s\": %.2f, "
-                   "\"GBps_at_64B\": %.0f}", first ? "" : ",\n", mb, blocks_per_cu, ms,
-                   loads / ms / 1e6, loads * 64 / ms / 1e6);
-            first = false;
-            CHK(hipEventDestroy(a));
-            CHK(hipEventDestroy(b));
+            for (int pol = 0; pol < 3; ++pol) {
+                const float ms = pol == 0 ? run<0>(tab, rows, grid, iters, out)
+                               : pol == 1 ? run<1>(tab, rows, grid, iters, out)
+                                          : run<2>(tab, rows, grid, iters, out);
+                const double loads = (double)threads * iters * 7;
+                printf("%s  {\"table_MB\": %.0f, \"alloc\": \"%s\", \"policy\": \"%s\", \"ms\": %.3f, "
+                       "\"Grows_per_s\": %.2f, \"GBps_at_64B\": %.0f}", first ? "" : ",\n", mb, kinds[kind],
+                       pols[pol], ms, loads / ms / 1e6, loads * 64 / ms / 1e6);
+                first = false;
+            }
+            CHK(hipFree(tab));
         }
-        CHK(hipFree(tab));
     }
     printf("\n]}\n");
     return 0;

@@ -72,6 +72,7 @@ SIGNATURES = {
     "xs_bank_upload": (_int, [_vp, _vp, _u64]),
     "xs_bank_set_term_size": (_int, [_vp, _u32]),
     "xs_bank_info": (_int, [_vp, ctypes.POINTER(BankInfo)]),
+    "xs_bank_signature_sizes": (_int, [_vp, _vp, _u64]),
     "xs_bank_doc_name": (ctypes.c_char_p, [_vp, _u64]),
     "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),

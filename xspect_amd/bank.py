@@ -126,6 +126,13 @@ class Bank:
             self._names = [lib.xs_bank_doc_name(self.handle, i).decode() for i in range(self.num_docs)]
         return self._names
 
+    def signature_sizes(self) -> list[int]:
+        """Rows of every doc group (COBS banks)."""
+        g = int(self.info.num_groups)
+        out = np.zeros(g, dtype=np.uint64)
+        check(load().xs_bank_signature_sizes(self.handle, _ptr(out), g))
+        return [int(x) for x in out]
+
     def payload_bytes(self) -> int:
         inf = self.info
         if inf.kind == XS_BANK_RBLOOM:

@@ -635,7 +635,7 @@ int xs_bank_build_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes,
     HIPCHK(hipSetDevice(b->device));
     if (n_rec == 0) return XS_OK;
     Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n_rec};
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : b->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
     return build_impl(b, in, d_rec_doc, s);
 }
 
@@ -687,6 +687,15 @@ int xs_bank_info(const xs_bank* b, xs_bank_info_t* o) {
     o->bloom_bits = b->kind == XS_BANK_RBLOOM ? b->nbytes * 8 : 0;
     o->device_bytes = b->dev_bytes;
     o->device_row_pitch = b->pitch;
+    return XS_OK;
+}
+
+int xs_bank_signature_sizes(const xs_bank* b, uint64_t* out, uint64_t n) {
+    if (!b || !out) return fail(XS_ERR_ARG, "null argument");
+    if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "rbloom banks have no signature groups");
+    if (n != b->sig.size()) return fail(XS_ERR_ARG, "bank has %zu groups, %llu requested", b->sig.size(),
+                                        (unsigned long long)n);
+    for (uint64_t g = 0; g < n; ++g) out[g] = b->sig[g];
     return XS_OK;
 }
 
@@ -753,7 +762,7 @@ int xs_query_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, const ui
     if (!b || !d_offsets || (!d_seqs && n)) return fail(XS_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(b->mu);
     HIPCHK(hipSetDevice(b->device));
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : b->stream;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
     if (n == 0) {
         if (d_totals) {
             const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;

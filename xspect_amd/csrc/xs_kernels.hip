@@ -614,22 +614,31 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 #pragma unroll
                     for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
                         if (j < h) ro[j] = act ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
-                    for (uint32_t cc = 0; cc < bv.nchunks; ++cc) {
-                        const uint64_t cd0 = doc0 + (uint64_t)cc * 128;
-                        if (cd0 >= dlim) break;
-                        uint4 m = make_uint4(0u, 0u, 0u, 0u);
-                        if (act) {
-                            m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    // all chunk loads of the group's h rows in flight, then count
+                    const uint32_t nch = (uint32_t)min((uint64_t)bv.nchunks, (dlim - doc0 + 127) / 128);
+                    uint4 mk[kMaxChunks];
+#pragma unroll
+                    for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
+                        mk[cc] = make_uint4(0u, 0u, 0u, 0u);
+                        if (cc < nch && act) {
+                            uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                             for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
                                 if (j < h)
                                     m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                            mk[cc] = m;
                         }
+                    }
+#pragma unroll
+                    for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
+                        if (cc >= nch) break;
+                        const uint64_t cd0 = doc0 + (uint64_t)cc * 128;
                         const uint32_t nd = (uint32_t)min((uint64_t)128, dlim - cd0);
-                        const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+                        const uint32_t w[4] = {mk[cc].x, mk[cc].y, mk[cc].z, mk[cc].w};
 #pragma unroll
                         for (uint32_t q = 0; q < 4; ++q) {
                             if (q * 32 >= nd) break;
+                            if (__ballot(w[q] != 0u) == 0ull) continue;  // no k-mer of the tile hits these docs
                             const uint32_t v = fold_halves(column_popc32(w[q], X));
                             if (lane < 32 && q * 32 + lane < nd) acc[cd0 + q * 32 + lane] += v;
                         }
@@ -665,23 +674,33 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 }
 
 // ------------------------------------------------------------------ rbloom probe
-template <int KT>
+// All K bit indices first, then all K dword loads in flight at once (the
+// reference stops at the first zero bit; the answer is the same).
+template <int KT, int KB>
 __device__ __forceinline__ bool bloom_member(const Kmer& c, uint32_t k, const BloomView& bv) {
+    constexpr int NK = KB ? KB : (int)kMaxHashes;
+    const uint32_t K = KB ? KB : bv.K;
     uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
-    bool in = true;
-    for (uint32_t j = 0; j < bv.K; ++j) {
-        const uint64_t p = sl * kLcgMl;
-        const uint64_t nl = p + kLcgCl;
-        const uint64_t carry = nl < p;
-        sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
-        sl = nl;
-        const uint64_t idx = fastmod(sh, bv.mbits, bv.magic);
-        in = in && ((bv.bits[idx >> 5] >> (idx & 31)) & 1u);
+    uint64_t idx[NK];
+#pragma unroll
+    for (int j = 0; j < NK; ++j) {
+        if ((uint32_t)j < K) {
+            const uint64_t p = sl * kLcgMl;
+            const uint64_t nl = p + kLcgCl;
+            const uint64_t carry = nl < p;
+            sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
+            sl = nl;
+            idx[j] = fastmod(sh, bv.mbits, bv.magic);
+        }
     }
-    return in;
+    uint32_t all = 1;
+#pragma unroll
+    for (int j = 0; j < NK; ++j)
+        if ((uint32_t)j < K) all &= bv.bits[idx[j] >> 5] >> (idx[j] & 31);
+    return all & 1u;
 }
 
-template <int KT>
+template <int KT, int KB>
 __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv, BloomView bv,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials) {
@@ -712,7 +731,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
                 if (tb + lane < cnt) {
                     Kmer c;
                     kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
-                    in = bloom_member<KT>(c, k, bv);
+                    in = bloom_member<KT, KB>(c, k, bv);
                 }
                 c_unit += (uint32_t)__popcll(__ballot(in));
             }
@@ -1012,14 +1031,14 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
 
 int probe_grid_bloom() {
     static int cache = 0;
-    if (!cache) cache = resident_grid(probe_bloom_kernel<21>, kProbeThreads, 0);
+    if (!cache) cache = resident_grid(probe_bloom_kernel<21, 7>, kProbeThreads, 0);
     return cache;
 }
 
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
                               uint64_t* partials, int blocks, hipStream_t s) {
-    if (rv.k == 21) probe_bloom_kernel<21><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
-    else probe_bloom_kernel<0><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    if (rv.k == 21 && bv.K == 7) probe_bloom_kernel<21, 7><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    else probe_bloom_kernel<0, 0><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
     return hipGetLastError();
 }
 
