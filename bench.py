@@ -118,7 +118,7 @@ class Workload:
         else:  # mlst
             reads, loci_info = self._mlst(args, dev, s)
             self.config.update(loci=len(self.banks), **loci_info)
-            self.kernel = "probe_cobs_kernel<31,1> (compact)"
+            self.kernel = "probe_cobs_slots<31,1,12> (compact, 3 groups x 4 chunks)"
         self.reads = reads
         self.n = reads.shape[0]
         self.seq_bytes = reads.size

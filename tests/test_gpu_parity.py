@@ -63,6 +63,8 @@ CLASSIC_CASES = [
     (1000, 21, 7, [3_001]),
     (13, 32, 4, [2_048]),
     (40, 17, 9, [1_231]),
+    (2048, 31, 1, [9_001]),   # 16 chunks: widest slot kernel
+    (2100, 21, 7, [4_001]),   # 17 chunks: general kernel
 ]
 
 
@@ -87,7 +89,7 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
 
 
 @pytest.mark.parametrize("D,k,h,page,G", [(600, 31, 1, 64, 2), (20, 21, 7, 1, 3), (1500, 21, 2, 64, 3),
-                                          (70, 25, 3, 3, 3)])
+                                          (70, 25, 3, 3, 3), (2600, 31, 1, 64, 6), (1430, 31, 1, 64, 3)])
 def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
     assert (G - 1) * 8 * page < D <= G * 8 * page
     rng = np.random.default_rng(D)

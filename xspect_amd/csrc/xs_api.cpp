@@ -158,9 +158,6 @@ int validate_geometry(xs_bank* b) {
     for (auto s : b->sig)
         if (s == 0) return fail(XS_ERR_FORMAT, "zero signature size");
     b->pitch = (b->page + 15) / 16 * 16;
-    if (b->pitch / 16 > kMaxChunks)
-        return fail(XS_ERR_UNSUPPORTED, "page of %llu bytes exceeds %u docs per group",
-                    (unsigned long long)b->page, kMaxChunks * 128);
     int wpb;
     size_t lds;
     if (probe_blocks(b->D, &wpb, &lds) != 0)

@@ -554,7 +554,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
 }
 
 // ------------------------------------------------------------------ COBS probe (general)
-// Any D (LDS counters), compact doc groups, up to kMaxChunks 16-byte chunks per
+// Any D the LDS counters hold, compact doc groups, any row width (chunks in batches of kMaxChunks 16-byte
 // row.  Same unit scheme and column-popcount counting as the fast kernel.
 template <int KT, int HT>
 __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, CobsView bv,
@@ -614,8 +614,10 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 #pragma unroll
                     for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
                         if (j < h) ro[j] = act ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
-                    // all chunk loads of the group's h rows in flight, then count
-                    const uint32_t nch = (uint32_t)min((uint64_t)bv.nchunks, (dlim - doc0 + 127) / 128);
+                    // kMaxChunks chunk loads of the group's h rows in flight, then count
+                    const uint32_t nch_all = (uint32_t)min((uint64_t)bv.nchunks, (dlim - doc0 + 127) / 128);
+                    for (uint32_t cb = 0; cb < nch_all; cb += kMaxChunks) {
+                    const uint32_t nch = min(kMaxChunks, nch_all - cb);
                     uint4 mk[kMaxChunks];
 #pragma unroll
                     for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
@@ -625,14 +627,14 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 #pragma unroll
                             for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
                                 if (j < h)
-                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + (cb + cc) * 16));
                             mk[cc] = m;
                         }
                     }
 #pragma unroll
                     for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
                         if (cc >= nch) break;
-                        const uint64_t cd0 = doc0 + (uint64_t)cc * 128;
+                        const uint64_t cd0 = doc0 + (uint64_t)(cb + cc) * 128;
                         const uint32_t nd = (uint32_t)min((uint64_t)128, dlim - cd0);
                         const uint32_t w[4] = {mk[cc].x, mk[cc].y, mk[cc].z, mk[cc].w};
 #pragma unroll
@@ -640,9 +642,11 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
                             if (q * 32 >= nd) break;
                             if (__ballot(w[q] != 0u) == 0ull) continue;  // no k-mer of the tile hits these docs
                             const uint32_t v = fold_halves(column_popc32(w[q], X));
-                            if (lane < 32 && q * 32 + lane < nd) acc[cd0 + q * 32 + lane] += v;
+                            // return-free ds_add: no read-modify-write latency chain
+                            if (lane < 32 && q * 32 + lane < nd && v) atomicAdd(&acc[cd0 + q * 32 + lane], v);
                         }
                     }
+                    }  // chunk batch
                 }
             }
             for (uint64_t d = lane; d < D; d += 64) {
@@ -665,6 +669,146 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
             for (int w = 0; w < wpb; ++w) s += smem[(size_t)w * 2 * dpad + dpad + d];
             out[d] = s;
         }
+        if (threadIdx.x == 0) {
+            uint64_t s = 0;
+            for (int w = 0; w < wpb; ++w) s += s_kmers[w];
+            out[D] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ COBS probe (slots)
+// Banks whose rows span at most NS 16-byte chunks over all doc groups
+// (classic D <= 16*128, compact schemes such as an MLST locus: 3 groups x 4
+// chunks).  Every chunk of every group's h rows is in flight before any
+// counting; per-doc counts of the unit live in registers, two 16-bit counters
+// per VGPR (a unit has <= 256 k-mers, so one lane-half count is <= 128);
+// block totals go to LDS with return-free ds_add.
+template <int KT, int HT, int NS>
+__global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv, CobsView bv,
+                                                                     uint32_t* __restrict__ hits,
+                                                                     uint64_t* __restrict__ partials,
+                                                                     uint32_t dpad) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_tot[];  // [dpad] per block
+    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    for (uint32_t d = threadIdx.x; d < dpad; d += blockDim.x) s_tot[d] = 0;
+    __syncthreads();
+    Xpose X;
+    xpose_init(lane, X);
+
+    constexpr int NH = HT ? HT : (int)kMaxHashes;
+    const uint32_t k = KT ? KT : rv.k;
+    const uint32_t h = HT ? HT : bv.h;
+    const uint32_t step = rv.step;
+    const uint64_t D = bv.D;
+    const uint32_t cpg = bv.nchunks;       // chunks per group row
+    const uint32_t nslots = bv.G * cpg;    // <= NS (host-checked)
+    const uint64_t gdocs = 8 * bv.page;    // docs per group
+    const uint64_t U = rv.queue[0];
+    uint64_t kmer_total = 0;
+
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, step);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            kmer_total += cnt;
+            uint32_t acc[2 * NS];
+#pragma unroll
+            for (int i = 0; i < 2 * NS; ++i) acc[i] = 0;
+
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                const bool act = tb + lane < cnt;
+                uint64_t hv[NH];
+#pragma unroll
+                for (int j = 0; j < NH; ++j) hv[j] = 0;
+                if (act) {
+                    Kmer c;
+                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    Xxh64Pre pre;
+                    xxh64_pre<KT>(c, k, pre);
+#pragma unroll
+                    for (int j = 0; j < NH; ++j)
+                        if ((uint32_t)j < h) hv[j] = xxh64_seed<KT>(c, pre, k, (uint64_t)j);
+                }
+                uint4 mk[NS];
+                uint64_t ro[NH];
+#pragma unroll
+                for (int j = 0; j < NH; ++j) ro[j] = 0;
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    mk[i] = make_uint4(0u, 0u, 0u, 0u);
+                    if ((uint32_t)i < nslots) {
+                        const uint32_t g = (uint32_t)i / cpg;  // wave-uniform
+                        const uint32_t cc = (uint32_t)i - g * cpg;
+                        if (cc == 0) {
+                            const GroupDesc gd = bv.groups[g];
+#pragma unroll
+                            for (int j = 0; j < NH; ++j)
+                                if ((uint32_t)j < h) ro[j] = gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch;
+                        }
+                        if (act) {
+                            uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+                            for (int j = 0; j < NH; ++j)
+                                if ((uint32_t)j < h)
+                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                            mk[i] = m;
+                        }
+                    }
+                }
+                // (guards, not break: a runtime exit keeps the loop rolled and mk[] in scratch)
+#pragma unroll
+                for (int i = 0; i < NS; ++i) {
+                    if ((uint32_t)i < nslots) {
+                        const uint32_t w[4] = {mk[i].x, mk[i].y, mk[i].z, mk[i].w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (__ballot(w[q] != 0u) != 0ull)  // some k-mer of the tile hits these docs
+                                acc[2 * i + (q >> 1)] += column_popc32(w[q], X) << (16 * (q & 1));
+                    }
+                }
+            }
+            // lane c < 32 holds doc 32q + c of chunk i after folding the halves
+            const bool whole = nk <= kSegKmers;
+#pragma unroll
+            for (int i = 0; i < NS; ++i) {
+                if ((uint32_t)i >= nslots) continue;
+                const uint32_t g = (uint32_t)i / cpg;
+                const uint32_t cc = (uint32_t)i - g * cpg;
+                const uint64_t glim = min(D, (uint64_t)g * gdocs + gdocs);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t d0 = (uint64_t)g * gdocs + cc * 128 + q * 32;
+                    if (d0 >= glim) continue;
+                    const uint32_t v = fold_halves((acc[2 * i + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
+                    const uint64_t d = d0 + (uint64_t)lane;
+                    if (lane < 32 && d < glim) {
+                        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[d]), (unsigned long long)v);
+                        if (hits) {
+                            if (whole) hits[(uint64_t)r * D + d] = v;
+                            else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) s_kmers[wid] = kmer_total;
+    __syncthreads();
+    if (partials) {
+        const int wpb = blockDim.x >> 6;
+        uint64_t* out = partials + (uint64_t)blockIdx.x * (D + 1);
+        for (uint64_t d = threadIdx.x; d < D; d += blockDim.x) out[d] = s_tot[d];
         if (threadIdx.x == 0) {
             uint64_t s = 0;
             for (int w = 0; w < wpb; ++w) s += s_kmers[w];
@@ -990,14 +1134,50 @@ static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t
     return hipGetLastError();
 }
 
+// Slot kernel variant for banks whose rows span <= 16 chunks over all groups
+// (0: none).  D <= 16 * 128 follows, so LDS totals need <= 16 KB.
+static int slots_for(const CobsView& bv) {
+    const uint64_t n = (uint64_t)bv.G * bv.nchunks;
+    return n <= 4 ? 4 : n <= 8 ? 8 : n <= 12 ? 12 : n <= 16 ? 16 : 0;
+}
+
+using SlotsFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*, uint32_t);
+
+template <int KT, int HT>
+static SlotsFn slots_fn(int ns) {
+    switch (ns) {
+        case 4: return probe_cobs_slots<KT, HT, 4>;
+        case 8: return probe_cobs_slots<KT, HT, 8>;
+        case 12: return probe_cobs_slots<KT, HT, 12>;
+        default: return probe_cobs_slots<KT, HT, 16>;
+    }
+}
+
+static int kh_variant(uint32_t k, uint32_t h) { return (k == 21 && h == 7) ? 0 : (k == 31 && h == 1) ? 1 : 2; }
+
+static SlotsFn pick_slots(uint32_t k, uint32_t h, int ns) {
+    switch (kh_variant(k, h)) {
+        case 0: return slots_fn<21, 7>(ns);
+        case 1: return slots_fn<31, 1>(ns);
+        default: return slots_fn<0, 0>(ns);
+    }
+}
+
+static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128 * 128) * sizeof(uint64_t); }
+
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
-    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0};
+    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][4] = {};
     if (cobs_fast(bv, k)) {
         if (k == 21)
             return fast21 ? fast21 : (fast21 = resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0));
         return fast31 ? fast31 : (fast31 = resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0));
+    }
+    if (const int ns = slots_for(bv)) {
+        // LDS is 16 KB at most: residency is set by registers, not by D
+        int& g = slots[kh_variant(k, bv.h)][ns / 4 - 1];
+        return g ? g : (g = resident_grid(pick_slots(k, bv.h, ns), kProbeThreads, 16384));
     }
     int wpb;
     size_t lds;
@@ -1019,6 +1199,12 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
         fb.image_bytes = (uint32_t)min(bv.sig0 * 16ull, 0xFFFFFFFFull);
         if (rv.k == 21) return launch_fast_t<21, 7>(rv, fb, hits, partials, blocks, s);
         return launch_fast_t<31, 1>(rv, fb, hits, partials, blocks, s);
+    }
+    if (const int ns = slots_for(bv)) {
+        const size_t lds = slots_lds(bv);
+        pick_slots(rv.k, bv.h, ns)<<<blocks, kProbeThreads, lds, s>>>(rv, bv, hits, partials,
+                                                                    (uint32_t)(lds / sizeof(uint64_t)));
+        return hipGetLastError();
     }
     int wpb;
     size_t lds;
