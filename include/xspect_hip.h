@@ -156,6 +156,36 @@ int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float*
 
 void xs_bank_close(xs_bank* bank);
 
+/* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
+ * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path
+ * probabilistic_filter_model.py:316-330).  Records come out packed the way
+ * xs_query takes them.  Semantics: see xspect_amd/csrc/xs_fastx.cpp. */
+#define XS_FASTX_FASTA 1
+#define XS_FASTX_FASTQ 2
+#define XS_FASTX_PINNED 1 /* flag: batch sequence/offset buffers in pinned host memory */
+
+typedef struct xs_fastx xs_fastx;
+
+typedef struct xs_fastx_batch {
+    uint64_t n;                  /* records in this batch (0: end of file) */
+    uint64_t seq_bytes;          /* bytes of seqs */
+    const char* seqs;            /* record r = seqs[offsets[r] .. offsets[r+1]) */
+    const uint64_t* offsets;     /* n+1 entries, offsets[0] = 0 */
+    const char* ids;             /* record ids (first header token), packed */
+    const uint64_t* id_offsets;  /* n+1 entries */
+    uint64_t text_offset;        /* file bytes consumed so far */
+    uint64_t text_bytes;         /* file size */
+} xs_fastx_batch;
+
+/* threads <= 0: up to 16.  The file is memory-mapped until xs_fastx_close. */
+int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx** out);
+/* Parse the next batch: about max_text_bytes of file text, cut at a record
+ * start (one record at least).  The batch's buffers stay valid until the
+ * SECOND following call, so batch i can be probed while batch i+1 is parsed.
+ * Malformed records return XS_ERR_FORMAT with Biopython's message. */
+int xs_fastx_next(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_batch* out);
+void xs_fastx_close(xs_fastx* reader);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,7 +66,7 @@ def _expected_hits(ob, names, seqs, step=1, exclude=None):
     return out, nk
 
 
-def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mod):
+def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mod, monkeypatch):
     from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
 
     base = tmp_path / "xspect_data"
@@ -101,6 +101,17 @@ def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mo
     w3, _ = _expected_hits(ob, names, [r.seq for r in recs], step=3)
     key = "GCF_000006945 -GCF_000006945.2_ASM694v2_genomic"
     assert res2.hits["read_0"][key] == w3[0]["GCF_000006945"]
+
+    # FASTQ path streamed in many native batches == the same records in memory
+    import xspect_amd.file_io as fio
+    fq = tmp_path / "reads.fq"
+    fq.write_text("".join(f"@{r.id} d\n{r.seq}\n+\n{'I' * len(r.seq)}\n" for r in recs))
+    monkeypatch.setattr(fio, "DEFAULT_BATCH_TEXT", 1500)
+    res4 = model.predict(fq, exclude_ids=["GCF_000099999"])
+    assert res4.hits == res.hits and res4.num_kmers == res.num_kmers
+    ids, hm, nkm = model.predict_matrix(fq)
+    assert ids == [r.id for r in recs] and hm.shape == (len(recs), len(names))
+    monkeypatch.undo()
 
     model.save()
     loaded = ProbabilisticFilterModel.load(base / "test-filter-species.json")

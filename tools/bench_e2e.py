@@ -1,0 +1,123 @@
+"""End-to-end file -> hits timing of the species path.
+
+Writes a synthetic FASTQ of --reads x 150 bp reads (seeded genomes of the
+bench's config-2 bank), then times:
+  parse      native reader alone (xs_fastx_next over the whole file)
+  e2e        ProbabilisticFilterModel-style streaming: read_batches -> Bank.query
+             (H2D, probe, D2H of the n x D hit matrix), parse overlapped
+  e2e_tot    same, but per-doc totals only (xs_query_totals, no hit matrix)
+  py_parse   the pure-Python restatement of Bio.SeqIO (oracle/fastx.py) on a
+             bounded sample, scaled: what a record-at-a-time host path costs
+Prints one JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reads", type=int, default=1_000_000)
+    ap.add_argument("--docs", type=int, default=100)
+    ap.add_argument("--genome-len", type=int, default=4_000_000)
+    ap.add_argument("--batch-mb", type=int, default=256)
+    ap.add_argument("--dir", default=None)
+    args = ap.parse_args()
+
+    import torch
+    from xspect_amd.bank import Bank, cobs_signature_size
+    from xspect_amd.file_io import FastxReader, read_batches
+    from xspect_amd.synth import make_genomes, make_reads
+
+    k = 21
+    dev = torch.device("cuda", 0)
+    genomes = make_genomes(args.docs, args.genome_len, seed=42)
+    sig = cobs_signature_size(args.genome_len - k + 1, 7, 0.01)
+    bank = Bank.create_cobs(k, 7, [sig], args.docs, [f"sp{i:03d}" for i in range(args.docs)], device=0)
+    g = torch.from_numpy(genomes.reshape(-1)).to(dev)
+    go = torch.arange(args.docs + 1, dtype=torch.int64, device=dev) * args.genome_len
+    bank.build_device(g, genomes.size, go, args.docs, torch.arange(args.docs, dtype=torch.int32, device=dev),
+                      stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    del g
+
+    reads, _ = make_reads(genomes, args.reads, 150, seed=42)
+    tmp = Path(args.dir or tempfile.mkdtemp(prefix="xs_e2e_"))
+    fq = tmp / "reads.fastq"
+    qual = b"I" * 150
+    with open(fq, "wb") as fh:
+        for i in range(reads.shape[0]):
+            fh.write(b"@r%d\n%s\n+\n%s\n" % (i, reads[i].tobytes(), qual))
+    size = fq.stat().st_size
+    mb = args.batch_mb << 20
+    res = {"file_bytes": size, "reads": int(reads.shape[0]), "docs": args.docs, "batch_mb": args.batch_mb}
+
+    # parse only
+    t = time.perf_counter()
+    n = 0
+    with FastxReader(fq) as rd:
+        for b in rd.batches(mb):
+            n += b.n
+    dt = time.perf_counter() - t
+    assert n == reads.shape[0]
+    res["parse_s"] = dt
+    res["parse_GBps"] = size / dt / 1e9
+
+    for pinned in (False, True):
+        # warm
+        for b in read_batches(fq, mb, pinned=pinned):
+            bank.query(b.packed)
+            break
+        t = time.perf_counter()
+        n = 0
+        for b in read_batches(fq, mb, pinned=pinned):
+            h, nk = bank.query(b.packed)
+            n += b.n
+        dt = time.perf_counter() - t
+        res[f"e2e_hits_s{'_pinned' if pinned else ''}"] = dt
+        res[f"e2e_hits_reads_per_s{'_pinned' if pinned else ''}"] = n / dt
+        t = time.perf_counter()
+        for b in read_batches(fq, mb, pinned=pinned):
+            bank.query_totals(b.packed)
+        dt = time.perf_counter() - t
+        res[f"e2e_totals_s{'_pinned' if pinned else ''}"] = dt
+        res[f"e2e_totals_reads_per_s{'_pinned' if pinned else ''}"] = n / dt
+
+    # record-at-a-time Python parse on a bounded sample, scaled to the file
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import fastx as ofx  # test/bench-only restatement of Bio.SeqIO
+    sample = fq.read_bytes()[: 40 << 20]
+    sample = sample[: sample.rfind(b"\n@") + 1]
+    t = time.perf_counter()
+    recs = ofx.parse_fastq(sample)
+    dt = time.perf_counter() - t
+    res["py_parse_sample_bytes"] = len(sample)
+    res["py_parse_GBps"] = len(sample) / dt / 1e9
+    res["py_parse_s_scaled"] = dt * size / len(sample)
+    res["py_parse_records"] = len(recs)
+
+    # hits agree with the packed-in-memory path on the first batch
+    with FastxReader(fq) as rd:
+        b = rd.next_batch(mb)
+        h1, _ = bank.query(b.packed)
+    from xspect_amd.packing import pack_fixed
+    h2, _ = bank.query(pack_fixed(reads[: b.n]))
+    res["first_batch_hits_equal"] = bool(np.array_equal(h1, h2))
+    print(json.dumps(res))
+    if not args.dir:
+        fq.unlink()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,6 +24,10 @@ XS_BANK_COBS_CLASSIC = 0
 XS_BANK_COBS_COMPACT = 1
 XS_BANK_RBLOOM = 2
 
+XS_FASTX_FASTA = 1
+XS_FASTX_FASTQ = 2
+XS_FASTX_PINNED = 1
+
 
 class XsError(RuntimeError):
     """A failed libxspect_hip call (message from xs_last_error)."""
@@ -48,6 +52,19 @@ class BankInfo(ctypes.Structure):
         ("bloom_bits", ctypes.c_uint64),
         ("device_bytes", ctypes.c_uint64),
         ("device_row_pitch", ctypes.c_uint64),
+    ]
+
+
+class FastxBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("seq_bytes", ctypes.c_uint64),
+        ("seqs", ctypes.c_void_p),
+        ("offsets", ctypes.c_void_p),
+        ("ids", ctypes.c_void_p),
+        ("id_offsets", ctypes.c_void_p),
+        ("text_offset", ctypes.c_uint64),
+        ("text_bytes", ctypes.c_uint64),
     ]
 
 
@@ -83,6 +100,9 @@ SIGNATURES = {
     "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_close": (None, [_vp]),
+    "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
+    "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),
+    "xs_fastx_close": (None, [_vp]),
 }
 
 _LIB = None

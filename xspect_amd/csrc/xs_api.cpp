@@ -473,6 +473,11 @@ xs_bank* new_bank(int device, int kind) {
 
 }  // namespace
 
+int xs::set_error(int code, const char* msg) {
+    g_err = msg;
+    return code;
+}
+
 extern "C" {
 
 int xs_version(void) { return 100; }

@@ -97,4 +97,7 @@ hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, u
 // Host-side constants shared with the kernels.
 inline uint64_t barrett_magic(uint64_t d) { return d ? (~0ull) / d : 0; }
 
+// Set the thread-local message xs_last_error() returns; returns `code`.
+int set_error(int code, const char* msg);
+
 }  // namespace xs

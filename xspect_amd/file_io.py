@@ -1,18 +1,30 @@
-"""FASTA/FASTQ records without Biopython (host side of the probe path).
+"""FASTA/FASTQ input of the probe path, parsed natively.
 
 Mirrors what the hot path consumes from ``src/xspect/file_io.py:47-79``
-(``get_record_iterator``: Bio.SeqIO parse by file extension).  A record has
-``.id`` (first whitespace token of the header, as Bio.SeqIO) and ``.seq``.
-Bio.SeqRecord objects are accepted anywhere a record is expected.
+(``get_record_iterator``: Bio.SeqIO parse by file extension).  Files are read
+by the multithreaded reader in libxspect_hip.so (``xs_fastx_*``), which yields
+batches already packed for the probe call; ``get_record_iterator`` builds
+``Record`` objects (``.id`` = first header token, ``.seq``) from them for
+callers that want records.  Bio.SeqRecord objects are accepted anywhere a
+record is expected.
 """
 from __future__ import annotations
 
+import ctypes
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Iterator
 
+import numpy as np
+
+from ._lib import (XS_ERR_FORMAT, XS_FASTX_FASTA, XS_FASTX_FASTQ, XS_FASTX_PINNED, FastxBatch, check,
+                   load)
+from .packing import PackedReads
+
 FASTA_ENDINGS = ["fasta", "fna", "fa", "ffn", "frn"]  # definitions.py:6
 FASTQ_ENDINGS = ["fastq", "fq"]                       # definitions.py:7
+# File text per native reader batch.
+DEFAULT_BATCH_TEXT = 256 << 20
 
 
 @dataclass
@@ -38,65 +50,145 @@ def seq_text(obj) -> str:
     return str(obj)
 
 
-def _fasta(path: Path) -> Iterator[Record]:
-    rid, desc, chunks = None, "", []
-    with open(path, "r", encoding="utf-8") as fh:
-        for line in fh:
-            if line.startswith(">"):
-                if rid is not None:
-                    yield Record(rid, "".join(chunks), desc)
-                desc = line[1:].rstrip("\r\n")
-                rid = desc.split(None, 1)[0] if desc.strip() else ""
-                chunks = []
-            elif rid is not None:
-                chunks.append(line.strip())
-    if rid is not None:
-        yield Record(rid, "".join(chunks), desc)
+class SeqBatch:
+    """One batch of the native reader: packed sequences (zero-copy views of
+    the reader's buffers, valid until the reader's second following call)
+    and the record ids."""
+
+    def __init__(self, fb):
+        n = int(fb.n)
+        self.n = n
+        self.text_offset = int(fb.text_offset)
+        self.text_bytes = int(fb.text_bytes)
+        if n:
+            offs = np.ctypeslib.as_array(ctypes.cast(fb.offsets, ctypes.POINTER(ctypes.c_uint64)), (n + 1,))
+            # +1: the reader keeps 64 defined bytes past the end (the guard byte
+            # PackedReads carries)
+            buf = np.ctypeslib.as_array(ctypes.cast(fb.seqs, ctypes.POINTER(ctypes.c_uint8)),
+                                        (int(fb.seq_bytes) + 1,))
+            ioffs = np.ctypeslib.as_array(ctypes.cast(fb.id_offsets, ctypes.POINTER(ctypes.c_uint64)), (n + 1,))
+            self._ids_raw = ctypes.string_at(fb.ids, int(ioffs[n])) if ioffs[n] else b""
+            self._ioffs = ioffs.copy()
+        else:
+            offs = np.zeros(1, dtype=np.uint64)
+            buf = np.zeros(1, dtype=np.uint8)
+            self._ids_raw, self._ioffs = b"", np.zeros(1, dtype=np.uint64)
+        self.packed = PackedReads(buf, offs)
+
+    def ids(self) -> list[str]:
+        raw, o = self._ids_raw, self._ioffs.tolist()
+        if raw.isascii():
+            s = raw.decode("ascii")
+            return [s[o[i]:o[i + 1]] for i in range(self.n)]
+        return [raw[o[i]:o[i + 1]].decode("utf-8", errors="replace") for i in range(self.n)]
+
+    def lengths(self) -> np.ndarray:
+        return self.packed.lengths()
+
+    def records(self) -> list[Record]:
+        buf, o = self.packed.buf, self.packed.offsets.tolist()
+        raw = buf[:o[-1]].tobytes() if self.n else b""
+        return [Record(rid, raw[o[i]:o[i + 1]].decode("ascii", errors="replace"))
+                for i, rid in enumerate(self.ids())]
 
 
-def _fastq(path: Path) -> Iterator[Record]:
-    with open(path, "r", encoding="utf-8") as fh:
+def fastx_format(path: Path) -> int:
+    """XS_FASTX_* of a path by its ending (file_io.py:72-79), else ValueError."""
+    ending = Path(path).suffix[1:]
+    if ending in FASTA_ENDINGS:
+        return XS_FASTX_FASTA
+    if ending in FASTQ_ENDINGS:
+        return XS_FASTX_FASTQ
+    raise ValueError("Invalid file format, must be a fasta or fastq file")
+
+
+class FastxReader:
+    """Native multithreaded FASTA/FASTQ reader (xs_fastx_* in xspect_hip.h)."""
+
+    def __init__(self, path: Path, threads: int = 0, pinned: bool = False):
+        self.path = Path(path)
+        fmt = fastx_format(self.path)
+        self._lib = load()
+        h = ctypes.c_void_p()
+        check(self._lib.xs_fastx_open(str(self.path).encode(), fmt, threads,
+                                      XS_FASTX_PINNED if pinned else 0, ctypes.byref(h)))
+        self._h = h
+
+    def next_batch(self, max_bytes: int = DEFAULT_BATCH_TEXT) -> SeqBatch:
+        """Next batch (n == 0 at end of file).  Malformed records raise ValueError."""
+        fb = FastxBatch()
+        rc = self._lib.xs_fastx_next(self._h, max_bytes, ctypes.byref(fb))
+        if rc == XS_ERR_FORMAT:
+            raise ValueError(self._lib.xs_last_error().decode())
+        check(rc)
+        return SeqBatch(fb)
+
+    def batches(self, max_bytes: int = DEFAULT_BATCH_TEXT) -> Iterator[SeqBatch]:
         while True:
-            head = fh.readline()
-            if not head:
+            b = self.next_batch(max_bytes)
+            if b.n == 0:
                 return
-            if not head.strip():
-                continue
-            if not head.startswith("@"):
-                raise ValueError(f"{path}: records in FASTQ files should start with '@'")
-            desc = head[1:].rstrip("\r\n")
-            seq_lines = []
-            line = fh.readline()
-            while line and not line.startswith("+"):
-                seq_lines.append(line.strip())
-                line = fh.readline()
-            seq = "".join(seq_lines)
-            qual = []
-            got = 0
-            while got < len(seq):
-                q = fh.readline()
-                if not q:
-                    raise ValueError(f"{path}: truncated FASTQ record {desc!r}")
-                q = q.strip()
-                qual.append(q)
-                got += len(q)
-            yield Record(desc.split(None, 1)[0] if desc.strip() else "", seq, desc)
+            yield b
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.xs_fastx_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def read_batches(path: Path, max_bytes: int | None = None, threads: int = 0,
+                 pinned: bool = False) -> Iterator[SeqBatch]:
+    """Batches of a FASTA/FASTQ file, parsing batch i+1 while the caller works on
+    batch i (the native reader releases the GIL).  A yielded batch's buffers
+    stay valid until the generator is advanced again.  max_bytes: file text
+    per batch (None: DEFAULT_BATCH_TEXT)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    max_bytes = DEFAULT_BATCH_TEXT if max_bytes is None else max_bytes
+
+    with FastxReader(path, threads, pinned) as rd, ThreadPoolExecutor(1) as pool:
+        fut = pool.submit(rd.next_batch, max_bytes)
+        while True:
+            b = fut.result()
+            if b.n == 0:
+                return
+            # the reader double-buffers: parsing i+1 leaves batch i intact
+            fut = pool.submit(rd.next_batch, max_bytes)
+            yield b
+
+
+def _native_records(path: Path) -> Iterator[Record]:
+    for b in read_batches(path):
+        yield from b.records()
 
 
 def get_record_iterator(file_path: Path) -> Iterator[Record]:
     """Record iterator of a FASTA/FASTQ file (error messages as file_io.py:66-79)."""
+    check_input_path(file_path)
+    return _native_records(file_path)
+
+
+def check_input_path(file_path) -> int:
+    """The input checks of get_record_iterator (file_io.py:66-79); XS_FASTX_* format."""
     if not isinstance(file_path, Path):
         raise ValueError("Path must be a Path object")
     if not file_path.exists():
         raise ValueError("File does not exist")
     if not file_path.is_file():
         raise ValueError("Path must be a file")
-    ending = file_path.suffix[1:]
-    if ending in FASTA_ENDINGS:
-        return _fasta(file_path)
-    if ending in FASTQ_ENDINGS:
-        return _fastq(file_path)
-    raise ValueError("Invalid file format, must be a fasta or fastq file")
+    return fastx_format(file_path)
 
 
 def write_fasta(records, path: Path, width: int = 0) -> None:

@@ -19,7 +19,8 @@ import numpy as np
 
 from .bank import Bank, cobs_signature_size
 from ._lib import XS_BANK_COBS_CLASSIC
-from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, get_record_iterator, is_record, seq_text)
+from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, check_input_path, get_record_iterator, is_record,
+                      read_batches, seq_text)
 from .packing import PackedReads, pack_sequences
 from .result import ModelResult
 from .util import default_device, slugify
@@ -137,13 +138,13 @@ class ProbabilisticFilterModel:
             self.display_names[doc] = display_names.get(f.stem, f.stem)
             names.append(doc)
         # signature size from the largest document's term count
-        terms = [sum(max(0, len(r.seq) - self.k + 1) for r in get_record_iterator(f)) for f in files]
+        terms = [sum(int(np.maximum(b.lengths().astype(np.int64) - self.k + 1, 0).sum())
+                     for b in read_batches(f)) for f in files]
         sig = cobs_signature_size(max(max(terms), 1), self.num_hashes, self.fpr)
         bank = Bank.create_cobs(self.k, self.num_hashes, [sig], len(files), names, device=self.device)
         for d, f in enumerate(files):
-            recs = [seq_text(r.seq) for r in get_record_iterator(f)]
-            if recs:
-                bank.build(pack_sequences(recs), np.full(len(recs), d, dtype=np.uint32))
+            for b in read_batches(f):
+                bank.build(b.packed, np.full(b.n, d, dtype=np.uint32))
         path = Path(self.get_cobs_index_path())
         bank.save(path)
         if self.index is not None:
@@ -184,6 +185,8 @@ class ProbabilisticFilterModel:
     def _matrix(self, sequence_input, step: int):
         if step < 1:
             raise ValueError("step must be >= 1")
+        if isinstance(sequence_input, Path):
+            return self._matrix_file(sequence_input, step)
         records = self._collect(sequence_input)
         ids = [r.id for r in records]
         texts = [seq_text(r.seq) for r in records]
@@ -200,6 +203,30 @@ class ProbabilisticFilterModel:
             hits[lo:hi] = h
             nk[lo:hi] = n
         return ids, lens, hits, nk
+
+    def _matrix_file(self, path: Path, step: int):
+        """A FASTA/FASTQ file streamed through the native reader: batch i+1 is
+        parsed while batch i is probed, and no per-record objects are built
+        (the reference iterates Bio.SeqIO records, :316-330)."""
+        check_input_path(path)
+        if self.index is None:
+            raise ValueError("The model has not been trained yet")
+        ids: list[str] = []
+        lens, hits, nks = [], [], []
+        for batch in read_batches(path):
+            L = batch.lengths()
+            if (L <= self.k).any():
+                raise ValueError("Invalid sequence, must be longer than k")
+            h, n = self._query(batch.packed, step)
+            ids += batch.ids()
+            lens.append(L)
+            hits.append(h)
+            nks.append(n)
+        D = self.index.num_docs
+        hits_m = np.concatenate(hits) if hits else np.zeros((0, D), dtype=np.uint32)
+        nk = np.concatenate(nks) if nks else np.zeros(0, dtype=np.uint64)
+        lens_l = np.concatenate(lens).tolist() if lens else []
+        return ids, lens_l, hits_m, nk
 
     def _collect(self, sequence_input) -> list:
         if is_record(sequence_input):

@@ -17,7 +17,7 @@ import numpy as np
 
 from ._lib import XS_BANK_RBLOOM
 from .bank import Bank, bloom_parameters
-from .file_io import get_record_iterator, is_record, seq_text
+from .file_io import check_input_path, is_record, read_batches, seq_text
 from .packing import pack_sequences
 from .probabilistic_filter_model import ProbabilisticFilterModel
 
@@ -40,18 +40,12 @@ class ProbabilisticSingleFilterModel(ProbabilisticFilterModel):
             training_accessions: list[str] | None = None) -> None:
         """Bloom(total_length - k + 1, fpr) over every k-mer of the file (:63-96)."""
         self.training_accessions = training_accessions
-        total_length = sum(len(r.seq) for r in get_record_iterator(file_path))
+        check_input_path(file_path)
+        total_length = sum(int(b.packed.nbytes) for b in read_batches(file_path))
         nbytes, nhash = bloom_parameters(total_length - self.k + 1, self.fpr)
         bank = Bank.create_bloom(self.k, nbytes, nhash, device=self.device)
-        batch, size = [], 0
-        for rec in get_record_iterator(file_path):
-            batch.append(seq_text(rec.seq))
-            size += len(batch[-1])
-            if size > (1 << 28):
-                bank.build(pack_sequences(batch))
-                batch, size = [], 0
-        if batch:
-            bank.build(pack_sequences(batch))
+        for b in read_batches(file_path):
+            bank.build(b.packed)
         self.display_names[file_path.stem] = display_name
         bank.save(self.bloom_path())
         if self.bf is not None:
