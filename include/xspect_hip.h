@@ -139,6 +139,19 @@ int xs_query_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes,
                     const uint64_t* d_offsets, uint64_t n, uint32_t step, uint32_t* d_hits,
                     uint64_t* d_num_kmers, uint64_t* d_totals, void* stream);
 
+/* Per-read best doc without materialising the hit matrix on the host:
+ * best_doc[r] = the doc with the most hits of read r, or XS_BEST_AMBIGUOUS when
+ * two or more docs share the maximum (the per-read call of the reference's
+ * benchmark, scripts/benchmark/main.nf:417-436); best_hits[r] = that maximum.
+ * best_hits, num_kmers_out and totals_out (D+1 entries, as xs_query_totals
+ * then the k-mer total) may be NULL. */
+#define XS_BEST_AMBIGUOUS 0xFFFFFFFFu
+int xs_query_best(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                  uint32_t* best_doc, uint32_t* best_hits, uint64_t* num_kmers_out, uint64_t* totals_out);
+/* The same reduction over a device hit matrix (n x num_docs uint32) on `stream`. */
+int xs_best_device(const uint32_t* d_hits, uint64_t n, uint64_t num_docs, uint32_t* d_best_doc,
+                   uint32_t* d_best_hits, void* stream);
+
 /* MLST chunk scoring (probabilistic_filter_mlst_model.py:237-256): for chunk
  * hit rows hits[c][d] whose owner is seq_of_chunk[c] (non-decreasing), sum
  * hits[c][d] into scores[seq][d] only where hits[c][d] > threshold
@@ -155,6 +168,17 @@ int xs_bank_last_probe_ms(xs_bank* bank, float* ms);
 int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float* max_ms);
 
 void xs_bank_close(xs_bank* bank);
+
+/* ---- Result output (src/xspect/models/result.py:151-202, json.dumps(indent=4)).
+ * Appends the "hits", "scores" (with "total") and "num_kmers" sections of a
+ * ModelResult JSON for an n x num_docs hit matrix to `path`; the caller writes
+ * the fields before and after.  ids_json / labels_json: packed JSON string
+ * literals (quotes included) with n+1 / num_docs+1 offsets; doc_mask
+ * (num_docs bytes, 1 = keep) may be NULL.  threads <= 0: 16. */
+int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, const uint32_t* hits,
+                             const uint64_t* num_kmers, const char* ids_json, const uint64_t* ids_off,
+                             const char* labels_json, const uint64_t* labels_off, const uint8_t* doc_mask,
+                             int threads);
 
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
  * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path

@@ -146,6 +146,17 @@ def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
     assert res.prediction == "label2"
     vec = ProbabilisticFilterSVMModel.svm_vector(loaded.predict([Record("q", g2[2000:12_000])], step=5))
     assert len(vec) == 4 and vec[2] == 1.0
+    # columnar result: same prediction, same JSON bytes as ModelResult.save
+    reads = [Record(f"q{i}", g2[s:s + 150]) for i, s in enumerate(range(0, 30_000, 997))]
+    fa = tmp_path / "q.fasta"
+    write_fasta(reads, fa)
+    col = loaded.predict_columnar(fa, exclude_ids=["GCF_000006945"], display_name=True)
+    ref = loaded.predict(reads, exclude_ids=["GCF_000006945"], display_name=True)
+    assert col.prediction == ref.prediction
+    col.input_source = ref.input_source = "q.fasta"
+    col.save(tmp_path / "col.json")
+    ref.save(tmp_path / "ref.json")
+    assert (tmp_path / "col.json").read_bytes() == (tmp_path / "ref.json").read_bytes()
 
 
 def test_genus_bloom_model(tmp_path, genomes, oracle_mod):

@@ -219,3 +219,33 @@ def _explain(got, want, reads):
         r = reads[i]
         rows.append(f"read {i} len={len(r)} head={r[:30]!r} got={np.asarray(got)[i][:8]} want={np.asarray(want)[i][:8]}")
     return f"{bad.size} rows differ: " + "; ".join(rows)
+
+
+def test_query_best_matches_hit_matrix(xs, oracle_mod):
+    """xs_query_best / xs_best_device == argmax of the hit matrix, ties -> ambiguous."""
+    torch = pytest.importorskip("torch")
+    for D, k, h, sig in [(100, 21, 7, [20_011]), (3, 31, 1, [997]), (1500, 21, 2, [3_001])]:
+        ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D)
+        rng = np.random.default_rng(D)
+        reads = [s[o:o + 150] for s in seqs for o in (0, 300)] + _reads(rng, 200, k)
+        reads = [r for r in reads if len(r) > 0]
+        hits, nk = ob.query(reads)
+        hits = hits.reshape(len(reads), D)
+        m = hits.max(axis=1)
+        ties = (hits == m[:, None]).sum(axis=1)
+        want = np.where(ties == 1, hits.argmax(axis=1), 0xFFFFFFFF).astype(np.uint32)
+        best, bh, gnk, tot = gb.query_best(reads, want_totals=True)
+        assert np.array_equal(best, want) and np.array_equal(bh, m) and np.array_equal(gnk, nk)
+        assert np.array_equal(tot[:D], hits.sum(axis=0)) and int(tot[D]) == int(nk.sum())
+        dh = torch.from_numpy(hits.astype(np.int32)).cuda()
+        db = torch.empty(len(reads), dtype=torch.int32, device="cuda")
+        dbh = torch.empty(len(reads), dtype=torch.int32, device="cuda")
+        xs.best_device(dh, len(reads), D, db, dbh, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(db.cpu().numpy().view(np.uint32), want)
+        assert np.array_equal(dbh.cpu().numpy().view(np.uint32), m)
+        gb.close()
+    b = xs.Bank.create_bloom(21, 4096, 7)
+    best, bh, nk, tot = b.query_best([], want_totals=True)
+    assert best.size == 0 and tot.tolist() == [0, 0]
+    b.close()

@@ -6,6 +6,9 @@ bench's config-2 bank), then times:
   e2e        ProbabilisticFilterModel-style streaming: read_batches -> Bank.query
              (H2D, probe, D2H of the n x D hit matrix), parse overlapped
   e2e_tot    same, but per-doc totals only (xs_query_totals, no hit matrix)
+  e2e_best   read_batches -> Bank.query_best (per-read best doc on the device)
+  json       MatrixResult.save (native writer) of the whole file's result, and
+             the per-read-dict ModelResult.save on a 20k-read sample, scaled
   py_parse   the pure-Python restatement of Bio.SeqIO (oracle/fastx.py) on a
              bounded sample, scaled: what a record-at-a-time host path costs
 Prints one JSON line.
@@ -93,6 +96,45 @@ def main():
         dt = time.perf_counter() - t
         res[f"e2e_totals_s{'_pinned' if pinned else ''}"] = dt
         res[f"e2e_totals_reads_per_s{'_pinned' if pinned else ''}"] = n / dt
+
+    # per-read best doc, hit matrix kept on the device
+    t = time.perf_counter()
+    n = 0
+    for b in read_batches(fq, mb, pinned=True):
+        best, bh, nk, tot = bank.query_best(b.packed, want_totals=True)
+        n += b.n
+    dt = time.perf_counter() - t
+    res["e2e_best_s_pinned"] = dt
+    res["e2e_best_reads_per_s_pinned"] = n / dt
+
+    # result JSON: columnar writer (whole file) vs per-read dicts (sample, scaled)
+    from xspect_amd.result import MatrixResult
+    ids, hs, nks = [], [], []
+    for b in read_batches(fq, mb):
+        h, nk = bank.query(b.packed)
+        ids += b.ids()
+        hs.append(h)
+        nks.append(nk)
+    hits = np.concatenate(hs)
+    nk = np.concatenate(nks)
+    labels = bank.doc_names
+    mr = MatrixResult("synthetic-species", ids, labels, hits, nk, input_source=fq.name)
+    out = tmp / "result.json"
+    t = time.perf_counter()
+    mr.save(out)
+    dt = time.perf_counter() - t
+    res["json_columnar_s"] = dt
+    res["json_bytes"] = out.stat().st_size
+    m = 20_000
+    small = MatrixResult("synthetic-species", ids[:m], labels, hits[:m], nk[:m], input_source=fq.name)
+    t = time.perf_counter()
+    small.to_model_result().save(tmp / "small_dicts.json")
+    dt = time.perf_counter() - t
+    res["json_dicts_s_scaled"] = dt * len(ids) / m
+    small.save(tmp / "small_columnar.json")
+    res["json_small_identical"] = (tmp / "small_dicts.json").read_bytes() == (tmp / "small_columnar.json").read_bytes()
+    for f in (out, tmp / "small_dicts.json", tmp / "small_columnar.json"):
+        f.unlink()
 
     # record-at-a-time Python parse on a bounded sample, scaled to the file
     sys.path.insert(0, str(ROOT / "oracle"))

@@ -24,6 +24,8 @@ XS_BANK_COBS_CLASSIC = 0
 XS_BANK_COBS_COMPACT = 1
 XS_BANK_RBLOOM = 2
 
+XS_BEST_AMBIGUOUS = 0xFFFFFFFF
+
 XS_FASTX_FASTA = 1
 XS_FASTX_FASTQ = 2
 XS_FASTX_PINNED = 1
@@ -94,12 +96,16 @@ SIGNATURES = {
     "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "xs_query_best": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "xs_best_device": (_int, [_vp, _u64, _u64, _vp, _vp, _vp]),
     "xs_mlst_sum": (_int, [_vp, _vp, _vp, _u64, _u64, _u32, _vp]),
     "xs_bank_set_profiling": (_int, [_vp, _int]),
     "xs_bank_last_probe_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_close": (None, [_vp]),
+    "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _vp, ctypes.c_char_p, _vp,
+                                        ctypes.c_char_p, _vp, _vp, _int]),
     "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),
     "xs_fastx_close": (None, [_vp]),

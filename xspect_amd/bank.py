@@ -191,6 +191,20 @@ class Bank:
                                      _ptr(tot), ctypes.byref(nk)))
         return tot, int(nk.value)
 
+    def query_best(self, reads: PackedReads | Iterable, step: int = 1, want_totals: bool = False):
+        """Per-read best doc (XS_BEST_AMBIGUOUS on ties), its hit count, num_kmers,
+        and optionally the D+1 totals; the hit matrix stays on the device."""
+        pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
+        if step < 1:
+            raise ValueError("step must be >= 1")
+        best = np.empty(pr.n, dtype=np.uint32)
+        bh = np.empty(pr.n, dtype=np.uint32)
+        nk = np.empty(pr.n, dtype=np.uint64)
+        tot = np.empty(self.num_docs + 1, dtype=np.uint64) if want_totals else None
+        check(load().xs_query_best(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step, _ptr(best),
+                                   _ptr(bh), _ptr(nk), _ptr(tot) if tot is not None else None))
+        return best, bh, nk, tot
+
     def query_device(self, seqs, seq_bytes: int, offsets, n: int, step: int = 1, hits=None,
                      num_kmers=None, totals=None, stream: int | None = None) -> None:
         """Enqueue a query on device buffers (torch tensors or raw device pointers)."""
@@ -238,6 +252,11 @@ class Bank:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def best_device(hits, n: int, num_docs: int, best, best_hits=None, stream: int | None = None) -> None:
+    """xs_best_device: per-read best doc of a device hit matrix (n x num_docs uint32)."""
+    check(load().xs_best_device(_dptr(hits), n, num_docs, _dptr(best), _dptr(best_hits), stream))
 
 
 def _dptr(x) -> int | None:

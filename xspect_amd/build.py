@@ -10,7 +10,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 SO_PATH = PKG / "libxspect_hip.so"
-SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_kernels.hip"]
+SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_json.cpp", CSRC / "xs_kernels.hip"]
 HEADERS = [CSRC / "xs_internal.h", ROOT / "include" / "xspect_hip.h"]
 ARCH = os.environ.get("XSPECT_AMD_ARCH", "gfx950")
 

@@ -59,7 +59,8 @@ def classify_genus(model_genus: str, input_path: Path, output_path: Path, step: 
     model = ProbabilisticSingleFilterModel.load(genus_model_path(model_genus))
     inputs, out_path = prepare_input_output_paths(Path(input_path))
     for idx, current in enumerate(inputs):
-        result = model.predict(current, step=step)
+        # columnar result: same JSON as ModelResult.save, no per-read dicts
+        result = model.predict_columnar(current, step=step)
         result.input_source = current.name
         path = out_path(idx, Path(output_path))
         result.save(path)
@@ -77,8 +78,13 @@ def classify_species(model_genus: str, input_path: Path, output_path: Path, step
     model = cls.load(path)
     inputs, out_path = prepare_input_output_paths(Path(input_path))
     for idx, current in enumerate(inputs):
-        result = model.predict(current, exclude_ids=exclude_ids, step=step,
-                               display_name=display_name, validation=validation)
+        if validation:
+            result = model.predict(current, exclude_ids=exclude_ids, step=step,
+                                   display_name=display_name, validation=validation)
+        else:
+            # columnar result: same JSON as ModelResult.save, no per-read dicts
+            result = model.predict_columnar(current, exclude_ids=exclude_ids, step=step,
+                                            display_name=display_name)
         result.input_source = current.name
         path_out = out_path(idx, Path(output_path))
         result.save(path_out)

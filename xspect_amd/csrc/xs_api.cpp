@@ -100,7 +100,7 @@ struct xs_bank {
     std::mutex mu;
     // workspace
     DevBuf seqs, offs, fwd, rc, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials,
-        totals, tmp, chunks;
+        totals, tmp, chunks, best;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -732,6 +732,47 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
     if (hits_out) HIPCHK(hipMemcpyAsync(hits_out, d_hits, n * cols * 4, hipMemcpyDeviceToHost, b->stream));
     if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                  uint32_t* best_doc, uint32_t* best_hits, uint64_t* num_kmers_out, uint64_t* totals_out) {
+    if (!b || !offsets || ((!seqs || !best_doc) && n)) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    if (n == 0) {
+        if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
+        return XS_OK;
+    }
+    Inputs in;
+    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
+    if (int rc = b->hits.ensure(n * cols * 4)) return rc;
+    if (int rc = b->nk.ensure(n * 8)) return rc;
+    if (int rc = b->best.ensure(n * 8)) return rc;
+    if (totals_out) {
+        if (int rc = b->totals.ensure((cols + 1) * 8)) return rc;
+    }
+    uint32_t* d_hits = b->hits.as<uint32_t>();
+    uint32_t* d_best = b->best.as<uint32_t>();
+    uint32_t* d_bhits = d_best + n;
+    uint64_t* d_tot = totals_out ? b->totals.as<uint64_t>() : nullptr;
+    if (int rc = run_query(b, in, step, d_hits, b->nk.as<uint64_t>(), d_tot, b->stream)) return rc;
+    HIPCHK(launch_best_doc(d_hits, n, cols, d_best, d_bhits, b->stream));
+    HIPCHK(hipMemcpyAsync(best_doc, d_best, n * 4, hipMemcpyDeviceToHost, b->stream));
+    if (best_hits) HIPCHK(hipMemcpyAsync(best_hits, d_bhits, n * 4, hipMemcpyDeviceToHost, b->stream));
+    if (num_kmers_out)
+        HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
+    if (totals_out) HIPCHK(hipMemcpyAsync(totals_out, d_tot, (cols + 1) * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_best_device(const uint32_t* d_hits, uint64_t n, uint64_t num_docs, uint32_t* d_best_doc,
+                   uint32_t* d_best_hits, void* stream) {
+    if ((!d_hits || !d_best_doc) && n) return fail(XS_ERR_ARG, "null argument");
+    if (num_docs == 0) return fail(XS_ERR_ARG, "num_docs must be >= 1");
+    HIPCHK(launch_best_doc(d_hits, n, num_docs, d_best_doc, d_best_hits, static_cast<hipStream_t>(stream)));
     return XS_OK;
 }
 

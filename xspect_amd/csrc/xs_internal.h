@@ -97,6 +97,11 @@ hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, u
 // Host-side constants shared with the kernels.
 inline uint64_t barrett_magic(uint64_t d) { return d ? (~0ull) / d : 0; }
 
+// best_doc_kernel's value for reads whose maximum is shared (= XS_BEST_AMBIGUOUS).
+constexpr uint32_t kBestAmbiguous = 0xFFFFFFFFu;
+hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_t* best,
+                           uint32_t* best_hits, hipStream_t s);
+
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
 

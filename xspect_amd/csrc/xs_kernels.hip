@@ -1023,6 +1023,47 @@ __global__ void mlst_sum_kernel(const uint32_t* __restrict__ hits,
     }
 }
 
+// ------------------------------------------------------------------ per-read best doc
+// The doc with the most hits of each read, or kBestAmbiguous when several docs
+// share the maximum: the per-read call of scripts/benchmark/main.nf:417-436
+// ("ambiguous" on ties), made on the device so the n x D matrix stays in HBM.
+// One wavefront per read; lanes stride over the docs.
+__global__ void __launch_bounds__(256) best_doc_kernel(const uint32_t* __restrict__ hits, uint64_t n,
+                                                       uint64_t D, uint32_t* __restrict__ best,
+                                                       uint32_t* __restrict__ best_hits) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t r = wave; r < n; r += waves) {
+        const uint32_t* row = hits + r * D;
+        uint32_t m = 0, arg = kBestAmbiguous, cnt = 0;
+        for (uint64_t d = (uint64_t)lane; d < D; d += 64) {
+            const uint32_t v = row[d];
+            if (cnt == 0 || v > m) {
+                m = v;
+                arg = (uint32_t)d;
+                cnt = 1;
+            } else if (v == m) {
+                ++cnt;
+            }
+        }
+        uint32_t wm = m;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) wm = max(wm, (uint32_t)__shfl_xor((int)wm, o, 64));
+        uint32_t c = (cnt && m == wm) ? cnt : 0;
+        uint32_t a = c ? arg : kBestAmbiguous;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            c += (uint32_t)__shfl_xor((int)c, o, 64);
+            a = min(a, (uint32_t)__shfl_xor((int)a, o, 64));
+        }
+        if (lane == 0) {
+            best[r] = c == 1 ? a : kBestAmbiguous;
+            if (best_hits) best_hits[r] = wm;
+        }
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline int grid_for(uint64_t work, int per_block, int cap) {
     uint64_t g = (work + per_block - 1) / per_block;
@@ -1265,6 +1306,13 @@ hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, u
     if (n_chunks == 0 || D == 0) return hipSuccess;
     mlst_sum_kernel<<<grid_for(n_chunks * D, 256, 4096), 256, 0, s>>>(hits, seq_of_chunk, n_chunks,
                                                                       D, threshold, scores);
+    return hipGetLastError();
+}
+
+hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_t* best,
+                           uint32_t* best_hits, hipStream_t s) {
+    if (n == 0 || D == 0) return hipSuccess;
+    best_doc_kernel<<<grid_for(n, 4, 16384), 256, 0, s>>>(hits, n, D, best, best_hits);
     return hipGetLastError();
 }
 

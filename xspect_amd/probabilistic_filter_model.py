@@ -22,7 +22,7 @@ from ._lib import XS_BANK_COBS_CLASSIC
 from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, check_input_path, get_record_iterator, is_record,
                       read_batches, seq_text)
 from .packing import PackedReads, pack_sequences
-from .result import ModelResult
+from .result import MatrixResult, ModelResult
 from .util import default_device, slugify
 
 # One C-ABI call handles at most this many sequence bytes / reads.
@@ -241,6 +241,31 @@ class ProbabilisticFilterModel:
                 " fasta/fastq file")
         return recs
 
+    def _doc_labels(self) -> list[str]:
+        """Result label of every doc column of the hit matrix."""
+        return list(self.index.doc_names)
+
+    def _labels(self, display_name: bool) -> list[str]:
+        names = self._doc_labels()
+        if not display_name:
+            return names
+        # reference :299-308: "<key> -<display name minus the model name>"
+        return [f"{key} -{self.display_names.get(key, 'Unknown').replace(self.model_display_name, '', 1)}"
+                for key in names]
+
+    def _doc_mask(self, exclude_ids) -> np.ndarray | None:
+        if not exclude_ids:
+            return None
+        return np.array([name not in exclude_ids for name in self._doc_labels()], dtype=np.uint8)
+
+    def predict_columnar(self, sequence_input, exclude_ids: list[str] = None, step: int = 1,
+                         display_name: bool = False) -> MatrixResult:
+        """The prediction as a MatrixResult: the same numbers as predict() without
+        per-read dictionaries; MatrixResult.save writes the same JSON."""
+        ids, _, hits_m, nk = self._matrix(sequence_input, step)
+        return MatrixResult(self.slug(), ids, self._labels(display_name), hits_m, nk,
+                            sparse_sampling_step=step, doc_mask=self._doc_mask(exclude_ids))
+
     def predict(self, sequence_input, exclude_ids: list[str] = None, step: int = 1,
                 display_name: bool = False, validation: bool = False) -> ModelResult:
         """ModelResult of a record / list / iterator / FASTA-FASTQ path (reference :237-331)."""
@@ -249,17 +274,7 @@ class ProbabilisticFilterModel:
             # downloads (:508-601): outside the probe path, see DESIGN.md.
             raise NotImplementedError("validation (alignment-based misclassification detection) "
                                       "is outside the GPU probe path")
-        ids, lens, hits_m, _ = self._matrix(sequence_input, step)
-        hits: dict[str, dict] = {}
-        num_kmers: dict[str, int] = {}
-        for i, rid in enumerate(ids):
-            per = self._hit_dict(hits_m[i], exclude_ids)
-            if display_name:
-                per = {f"{key} -{self.display_names.get(key, 'Unknown').replace(self.model_display_name, '', 1)}": v
-                       for key, v in per.items()}
-            num_kmers[rid] = self._count_kmers_len(lens[i], step)
-            hits[rid] = per
-        return ModelResult(self.slug(), hits, num_kmers, sparse_sampling_step=step)
+        return self.predict_columnar(sequence_input, exclude_ids, step, display_name).to_model_result()
 
     # ------------------------------------------------------------ k-mer counts
     def _count_kmers_len(self, length: int, step: int) -> int:

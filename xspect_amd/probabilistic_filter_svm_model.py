@@ -17,7 +17,7 @@ from ._lib import XS_BANK_COBS_CLASSIC
 from .bank import Bank
 from .file_io import FASTA_ENDINGS, FASTQ_ENDINGS
 from .probabilistic_filter_model import ProbabilisticFilterModel
-from .result import ModelResult
+from .result import MatrixResult, ModelResult
 
 
 class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
@@ -60,7 +60,7 @@ class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
                 if file.suffix[1:] not in FASTA_ENDINGS + FASTQ_ENDINGS:
                     continue
                 print(f"Calculating {file.name} scores for SVM training...")
-                totals = super().predict(file, step=svm_step).get_scores()["total"]
+                totals = ProbabilisticFilterModel.predict_columnar(self, file, step=svm_step).get_total_scores()
                 values = ",".join(str(v) for _, v in sorted(totals.items()))
                 rows.append(f"{file.stem},{values},{species_folder.name}")
         header = f"file,{','.join(sorted(self.display_names))},label_id"
@@ -72,14 +72,20 @@ class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
         """Total scores sorted by label: the SVM feature row of one input."""
         return [v for _, v in sorted(result.get_scores()["total"].items())]
 
+    def predict_columnar(self, sequence_input, exclude_ids: list[str] = None, step: int = 1,
+                         display_name: bool = False) -> MatrixResult:
+        """Columnar prediction; the SVM label comes from the total scores only (:208-223)."""
+        res = super().predict_columnar(sequence_input, exclude_ids, step, display_name)
+        features = [[v for _, v in sorted(res.get_total_scores().items())]]
+        res.prediction = str(self._get_svm(exclude_ids).predict(features)[0])
+        return res
+
     def predict(self, sequence_input, exclude_ids: list[str] = None, step: int = 1,
                 display_name: bool = False, validation: bool = False) -> ModelResult:
-        res = super().predict(sequence_input, exclude_ids, step, display_name, validation)
-        features = [self.svm_vector(res)]
-        svm = self._get_svm(exclude_ids)
-        res.hits["misclassified"] = res.misclassified
-        return ModelResult(self.slug(), res.hits, res.num_kmers, sparse_sampling_step=step,
-                           prediction=str(svm.predict(features)[0]))
+        if validation:
+            raise NotImplementedError("validation (alignment-based misclassification detection) "
+                                      "is outside the GPU probe path")
+        return self.predict_columnar(sequence_input, exclude_ids, step, display_name).to_model_result()
 
     def _get_svm(self, exclude_ids):
         """SVC(kernel, C) fitted on scores.csv minus excluded labels/columns (:225-274)."""

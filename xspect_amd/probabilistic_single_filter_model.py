@@ -68,6 +68,12 @@ class ProbabilisticSingleFilterModel(ProbabilisticFilterModel):
     def _hit_dict(self, row: np.ndarray, exclude_ids) -> dict:
         return {next(iter(self.display_names)): int(row[0])}
 
+    def _doc_labels(self) -> list[str]:
+        return [next(iter(self.display_names))]
+
+    def _doc_mask(self, exclude_ids):
+        return None  # the genus filter has one label; exclude_ids does not apply
+
     @staticmethod
     def load(path: Path) -> "ProbabilisticSingleFilterModel":
         meta = json.loads(Path(path).read_text(encoding="utf-8"))

@@ -6,8 +6,12 @@ Behavioural mirror of the reference class
 """
 from __future__ import annotations
 
+import ctypes
+import json
 from json import dumps
 from pathlib import Path
+
+import numpy as np
 
 
 class ModelResult:
@@ -87,6 +91,148 @@ class ModelResult:
         path = Path(path)
         path.parent.mkdir(exist_ok=True, parents=True)
         path.write_text(dumps(self.to_dict(), indent=4), encoding="utf-8")
+
+
+def _json_packed(strings: list[str]) -> tuple[bytes, np.ndarray]:
+    """JSON string literals (json.dumps, ensure_ascii) of `strings`, packed + offsets."""
+    enc = [json.dumps(s).encode("ascii") for s in strings]
+    off = np.zeros(len(enc) + 1, dtype=np.uint64)
+    if enc:
+        np.cumsum(np.fromiter(map(len, enc), dtype=np.uint64, count=len(enc)), out=off[1:])
+    return b"".join(enc), off
+
+
+def cobs_order(row: np.ndarray, docs: np.ndarray) -> np.ndarray:
+    """`docs` in COBS result order for one hit row: count descending, ties by doc index."""
+    return docs[np.argsort(-row[docs].astype(np.int64), kind="stable")]
+
+
+class MatrixResult:
+    """Columnar ModelResult: read ids, labels, an n x D hit
+    matrix and per-read k-mer counts, as the probe produces them.
+
+    It holds the numbers ModelResult holds as per-read dictionaries
+    (``src/xspect/models/result.py:7-189``): ``to_model_result()`` builds those
+    dictionaries, and ``save()`` writes the same JSON bytes as
+    ``ModelResult.save`` without them: the per-read sections are formatted
+    natively (xs_write_result_sections), so 10^6-read results take seconds.
+    Per-read labels follow COBS result order (count descending, ties by doc
+    index); ``doc_mask`` drops excluded docs (predict's exclude_ids).
+    Duplicate read ids collapse as they do in the reference's dictionaries:
+    the first position, the last record's values.
+    """
+
+    def __init__(self, model_slug: str, ids: list[str], labels: list[str], hits: np.ndarray,
+                 num_kmers: np.ndarray, sparse_sampling_step: int = 1, prediction: str | None = None,
+                 input_source: str | None = None, doc_mask: np.ndarray | None = None):
+        if "total" in ids:
+            raise ValueError("'total' is a reserved key and cannot be used as a subsequence")
+        hits = np.ascontiguousarray(hits, dtype=np.uint32)
+        num_kmers = np.ascontiguousarray(num_kmers, dtype=np.uint64)
+        if hits.ndim != 2 or hits.shape[0] != len(ids) or hits.shape[1] != len(labels) or \
+                num_kmers.shape != (len(ids),):
+            raise ValueError("hits must be [len(ids), len(labels)] and num_kmers [len(ids)]")
+        if len(set(ids)) != len(ids):
+            last = {rid: i for i, rid in enumerate(ids)}
+            first_order = list(dict.fromkeys(ids))
+            rows = np.array([last[rid] for rid in first_order], dtype=np.int64)
+            ids, hits, num_kmers = first_order, hits[rows], num_kmers[rows]
+        self.model_slug = model_slug
+        self.ids = list(ids)
+        self.labels = list(labels)
+        self.hits = hits
+        self.num_kmers = num_kmers
+        self.sparse_sampling_step = sparse_sampling_step
+        self.prediction = prediction
+        self.input_source = input_source
+        self.doc_mask = None if doc_mask is None else np.ascontiguousarray(doc_mask, dtype=np.uint8)
+        self.misclassified = None
+
+    @property
+    def docs(self) -> np.ndarray:
+        d = np.arange(len(self.labels))
+        return d if self.doc_mask is None else d[self.doc_mask.astype(bool)]
+
+    def _needs_dicts(self) -> bool:
+        # reference quirks outside the columnar writer: a read called
+        # "misclassified" is popped from the hits (result.py:43), equal labels collapse
+        return "misclassified" in self.ids or len(set(self.labels)) != len(self.labels)
+
+    def to_model_result(self) -> ModelResult:
+        docs = self.docs
+        hits = {}
+        for i, rid in enumerate(self.ids):
+            row = self.hits[i]
+            order = cobs_order(row, docs).tolist()
+            hits[rid] = {self.labels[d]: int(row[d]) for d in order}
+        nk = {rid: int(n) for rid, n in zip(self.ids, self.num_kmers.tolist())}
+        return ModelResult(self.model_slug, hits, nk, self.sparse_sampling_step, self.prediction,
+                           self.input_source)
+
+    def get_total_hits(self) -> dict[str, int]:
+        if not self.ids:
+            raise IndexError("list index out of range")
+        tot = self.hits.sum(axis=0, dtype=np.uint64)
+        return {self.labels[d]: int(tot[d]) for d in cobs_order(self.hits[0], self.docs).tolist()}
+
+    def get_total_scores(self) -> dict[str, float]:
+        """get_scores()["total"] without the per-read part."""
+        n_all = int(self.num_kmers.sum())
+        return {label: round(v / n_all, 2) for label, v in self.get_total_hits().items()}
+
+    def best(self) -> tuple[np.ndarray, np.ndarray]:
+        """(best doc or XS_BEST_AMBIGUOUS, max hits) per read, over the kept docs."""
+        docs = self.docs
+        sub = self.hits[:, docs]
+        m = sub.max(axis=1) if docs.size else np.zeros(len(self.ids), dtype=np.uint32)
+        ties = (sub == m[:, None]).sum(axis=1) if docs.size else np.zeros(len(self.ids))
+        arg = docs[sub.argmax(axis=1)] if docs.size else np.zeros(len(self.ids), dtype=np.int64)
+        best = np.where(ties == 1, arg, 0xFFFFFFFF).astype(np.uint32)
+        return best, m.astype(np.uint32)
+
+    def save(self, path: Path) -> None:
+        """Write the JSON ModelResult.save writes (byte-identical)."""
+        path = Path(path)
+        if self._needs_dicts():
+            return self.to_model_result().save(path)
+        if not self.ids:
+            raise IndexError("list index out of range")  # get_total_hits on no reads, as the reference
+        from ._lib import check, load
+        path.parent.mkdir(exist_ok=True, parents=True)
+        head = "{\n    %s: %s,\n    %s: %s,\n    " % (
+            dumps("model_slug"), dumps(self.model_slug), dumps("sparse_sampling_step"),
+            dumps(self.sparse_sampling_step))
+        path.write_text(head, encoding="utf-8")
+        ids_b, ids_off = _json_packed(self.ids)
+        lab_b, lab_off = _json_packed(self.labels)
+        mask = self.doc_mask
+        vp = ctypes.c_void_p
+        check(load().xs_write_result_sections(
+            str(path).encode(), len(self.ids), len(self.labels), vp(self.hits.ctypes.data),
+            vp(self.num_kmers.ctypes.data), ids_b, vp(ids_off.ctypes.data), lab_b, vp(lab_off.ctypes.data),
+            vp(mask.ctypes.data) if mask is not None else None, 0))
+        tail = [("misclassified", self.misclassified), ("input_source", self.input_source)]
+        if self.prediction is not None:
+            tail.append(("prediction", self.prediction))
+        body = ",\n    ".join(f"{dumps(k)}: {dumps(v, indent=4)}" for k, v in tail)
+        with open(path, "a", encoding="utf-8") as fh:
+            fh.write("    " + body + "\n}")
+
+    def save_npz(self, path: Path) -> None:
+        """Columnar dump: ids, labels, hits, num_kmers (+ mask, metadata)."""
+        np.savez(path, ids=np.array(self.ids, dtype=object).astype(str), labels=np.array(self.labels).astype(str),
+                 hits=self.hits, num_kmers=self.num_kmers,
+                 doc_mask=self.doc_mask if self.doc_mask is not None else np.ones(len(self.labels), np.uint8),
+                 meta=np.array(json.dumps({"model_slug": self.model_slug,
+                                           "sparse_sampling_step": self.sparse_sampling_step,
+                                           "prediction": self.prediction, "input_source": self.input_source})))
+
+    @staticmethod
+    def load_npz(path: Path) -> "MatrixResult":
+        z = np.load(path, allow_pickle=False)
+        meta = json.loads(str(z["meta"]))
+        return MatrixResult(meta["model_slug"], z["ids"].tolist(), z["labels"].tolist(), z["hits"], z["num_kmers"],
+                            meta["sparse_sampling_step"], meta["prediction"], meta["input_source"], z["doc_mask"])
 
 
 class MlstResult:
