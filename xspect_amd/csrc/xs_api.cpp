@@ -99,8 +99,8 @@ struct xs_bank {
     hipStream_t stream = nullptr;
     std::mutex mu;
     // workspace
-    DevBuf seqs, offs, fwd, rc, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials,
-        totals, tmp, chunks, best;
+    DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
+        best;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -370,10 +370,6 @@ struct Inputs {
 // Strands + unit decomposition for n device-resident reads.
 int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, uint32_t* hits_zero,
                   uint64_t zero_cols, hipStream_t s, ReadView* rv) {
-    const int mode = b->kind == XS_BANK_RBLOOM ? kStrandBio : kStrandCobs;
-    const uint64_t nb = in.seq_bytes + kPad;
-    if (int rc = b->fwd.ensure(nb)) return rc;
-    if (int rc = b->rc.ensure(nb)) return rc;
     if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->unit_ofs.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
@@ -381,18 +377,14 @@ int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, u
     if (int rc = b->unit_read.ensure(unit_bound * 4)) return rc;
     const size_t tb = scan_temp_bytes(in.n ? in.n : 1);
     if (int rc = b->scan_tmp.ensure(tb)) return rc;
-    if (int rc = b->chunks.ensure(strand_chunk_slots(in.seq_bytes) * 4)) return rc;
-    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(),
-                        b->chunks.as<uint32_t>(), s));
-    HIPCHK(launch_strands(in.seqs, in.offs, in.n, in.seq_bytes, mode, b->fwd.as<uint8_t>(),
-                          b->rc.as<uint8_t>(), b->chunks.as<uint32_t>(), s));
+    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(), s));
     HIPCHK(launch_scan(b->scan_tmp.p, b->scan_tmp.cap, b->nseg.as<uint64_t>(),
                        b->unit_ofs.as<uint64_t>(), in.n, s));
     HIPCHK(launch_scatter_units(b->nseg.as<uint64_t>(), b->unit_ofs.as<uint64_t>(), in.n,
                                 b->unit_read.as<uint32_t>(), b->n_units.as<uint64_t>(), hits_zero,
                                 zero_cols, s));
-    rv->fwd = b->fwd.as<uint8_t>();
-    rv->rc = b->rc.as<uint8_t>();
+    rv->seq = in.seqs;
+    rv->seq_bytes = in.seq_bytes;
     rv->offs = in.offs;
     rv->unit_read = b->unit_read.as<uint32_t>();
     rv->unit_ofs = b->unit_ofs.as<uint64_t>();

@@ -51,8 +51,8 @@ struct BloomView {
 
 // Reads / records laid out for one probe or build call.
 struct ReadView {
-    const uint8_t* fwd;        // forward strand (normalised for COBS)
-    const uint8_t* rc;         // reverse-complement strand, same offsets
+    const uint8_t* seq;        // read bytes as handed over (no padding required)
+    uint64_t seq_bytes;        // size of the seq buffer: loads stop there
     const uint64_t* offs;      // n+1
     const uint32_t* unit_read; // units -> read
     const uint64_t* unit_ofs;  // first unit of each read (n)
@@ -63,12 +63,8 @@ struct ReadView {
 };
 
 // ---- launchers (xs_kernels.hip) -------------------------------------------
-uint64_t strand_chunk_slots(uint64_t nbytes);
-hipError_t launch_strands(const uint8_t* seqs, const uint64_t* offs, uint64_t n, uint64_t nbytes,
-                          int mode, uint8_t* fwd_out, uint8_t* rc_out, const uint32_t* chunk_first,
-                          hipStream_t s);
 hipError_t launch_units(const uint64_t* offs, uint64_t n, uint32_t k, uint32_t step,
-                        uint64_t* nk_out, uint64_t* nseg, uint32_t* chunk_first, hipStream_t s);
+                        uint64_t* nk_out, uint64_t* nseg, hipStream_t s);
 size_t scan_temp_bytes(uint64_t n);
 hipError_t launch_scan(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out,
                        uint64_t n, hipStream_t s);

@@ -1,13 +1,11 @@
 // xs_kernels.hip — gfx950 (MI355X, CDNA4) kernels of the k-mer x filter probe path.
 //
 // Pipeline of one query call (reads already in HBM):
-//   strands  : normalised forward strand + reverse-complement strand of every
-//              read, written once (byte tables in LDS)          [HBM stream]
 //   units    : per-read sampled k-mer count and #units (segments of kSegKmers)
 //   scan     : exclusive scan of #units (hipCUB)
 //   scatter  : unit -> read map; zero hit rows of split reads
 //   probe    : one wavefront per unit, one lane per k-mer: canonical k-mer
-//              from the two strand windows, h x XXH64 (or XXH3-64 + LCG for
+//              built in registers from one read window, h x XXH64 (or XXH3-64 + LCG for
 //              rbloom), h random 16-byte row gathers from the bank, AND, and
 //              per-doc ballot/popcount counting into per-wave LDS counters
 //                                                   [HBM random-read bound]
@@ -209,115 +207,110 @@ __device__ __forceinline__ uint64_t xxh3_kmer(const Kmer& c, uint32_t k) {
     return xxh64_avalanche((uint64_t)comb ^ (uint64_t)(kS32_0 ^ kS32_1));
 }
 
-// ------------------------------------------------------------------ strands
-__device__ __forceinline__ void strand_tables(int mode, uint8_t* tf, uint8_t* tr) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-        uint8_t f = (uint8_t)i, r = (uint8_t)i;
-        if (mode == kStrandCobs) {
-            const uint8_t u = (uint8_t)(i & 0xDF);
-            const bool base = (i >= 'A' && i <= 'Z') || (i >= 'a' && i <= 'z');
-            f = (base && (u == 'A' || u == 'C' || u == 'G' || u == 'T')) ? u : (uint8_t)'N';
-            r = f == 'A' ? 'T' : f == 'T' ? 'A' : f == 'C' ? 'G' : f == 'G' ? 'C' : 'N';
-        } else {
-            // Biopython ambiguous_dna_complement, both cases; others unchanged.
-            const bool lower = i >= 'a' && i <= 'z';
-            const uint8_t u = lower ? (uint8_t)(i - 32) : (uint8_t)i;
-            uint8_t m = 0;
-            switch (u) {
-                case 'A': m = 'T'; break; case 'T': m = 'A'; break;
-                case 'C': m = 'G'; break; case 'G': m = 'C'; break;
-                case 'M': m = 'K'; break; case 'K': m = 'M'; break;
-                case 'R': m = 'Y'; break; case 'Y': m = 'R'; break;
-                case 'W': m = 'W'; break; case 'S': m = 'S'; break;
-                case 'V': m = 'B'; break; case 'B': m = 'V'; break;
-                case 'H': m = 'D'; break; case 'D': m = 'H'; break;
-                case 'X': m = 'X'; break; case 'N': m = 'N'; break;
-                default: break;
-            }
-            if (m) r = lower ? (uint8_t)(m + 32) : m;
-        }
-        tf[i] = f;
-        tr[i] = r;
-    }
+// ------------------------------------------------------------------ k-mer assembly
+// A k-mer is built in registers straight from the read bytes: one unaligned
+// k-byte window load, byte normalisation (COBS) and the reverse complement by
+// a byte-table permute, then the byte-lexicographic min of the two strands.
+//
+// COBS (species, MLST): ACGT/acgt -> ACGT, any other byte -> N (restated
+// canonicalisation; oracle/xs_oracle.c xo_canonical_cobs).
+// rbloom (genus): bytes kept as they are, complement = Biopython's
+// ambiguous_dna_complement in both cases, other bytes unchanged
+// (probabilistic_single_filter_model.py:161-180; xo_canonical_bio).
+
+// 0x80 in every byte of v that is zero (exact, no carries between bytes).
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
+    return ~(((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t bytes_equal(uint32_t x, uint32_t c) { return zero_bytes(x ^ (c * 0x01010101u)); }
+
+// COBS normalisation of 4 bytes.  (b & 0xDF) is one of A/C/G/T only for
+// A/C/G/T/a/c/g/t, so the upper-cased test is exact.
+__device__ __forceinline__ uint32_t cobs_norm4(uint32_t x) {
+    const uint32_t u = x & 0xDFDFDFDFu;
+    const uint32_t ok = bytes_equal(u, 'A') | bytes_equal(u, 'C') | bytes_equal(u, 'G') | bytes_equal(u, 'T');
+    const uint32_t m = (ok >> 7) * 0xFFu;
+    return (u & m) | (0x4E4E4E4Eu & ~m);
 }
 
+// Complement of bytes in {A, C, G, T, N, 0}: b & 7 is 1, 3, 7, 4, 6, 0 for
+// them, and v_perm_b32 looks the complement up in an 8-byte table
+// {0, 'T', -, 'G', 'A', -, 'N', 'C'} (0 stays 0: padding).
+__device__ __forceinline__ uint32_t comp4(uint32_t f) {
+    return __builtin_amdgcn_perm(0x434E0041u, 0x47005400u, f & 0x07070707u);
+}
 
-// One thread per output dword: the forward strand byte p is tf[seq[p]], the
-// reverse-complement strand byte p is tr[seq[mirror(p)]] with mirror(p) =
-// offs[r] + offs[r+1] - 1 - p inside read r.  Both strands share the read
-// offsets, so the reverse complement of k-mer [p, p+k) of read r is the rc
-// window [offs[r+1] - (p - offs[r]) - k, ... + k).
-constexpr uint32_t kStrandIters = 16;
-constexpr uint64_t kStrandChunk = 256ull * 4 * kStrandIters;  // bytes per block iteration
-constexpr uint32_t kStrandMaxReads = 2048;                    // offsets staged in LDS
+// Biopython ambiguous_dna_complement of one byte, both cases; other bytes unchanged.
+__device__ __forceinline__ uint32_t bio_comp_byte(uint32_t b) {
+    const uint32_t lower = (b >= 'a' && b <= 'z') ? 32u : 0u;
+    const uint32_t u = b - lower;
+    uint32_t m = 0;
+    switch (u) {
+        case 'A': m = 'T'; break; case 'T': m = 'A'; break;
+        case 'C': m = 'G'; break; case 'G': m = 'C'; break;
+        case 'M': m = 'K'; break; case 'K': m = 'M'; break;
+        case 'R': m = 'Y'; break; case 'Y': m = 'R'; break;
+        case 'W': m = 'W'; break; case 'S': m = 'S'; break;
+        case 'V': m = 'B'; break; case 'B': m = 'V'; break;
+        case 'H': m = 'D'; break; case 'D': m = 'H'; break;
+        case 'X': m = 'X'; break; case 'N': m = 'N'; break;
+        default: break;
+    }
+    return m ? m + lower : b;
+}
 
-__global__ void __launch_bounds__(256) strands_kernel(const uint8_t* __restrict__ seqs,
-                                                      const uint64_t* __restrict__ offs,
-                                                      uint64_t n, int mode,
-                                                      uint32_t* __restrict__ fwd,
-                                                      uint32_t* __restrict__ rc,
-                                                      const uint32_t* __restrict__ chunk_first) {
-    __shared__ uint8_t tf[256], tr[256];
-    __shared__ uint64_t s_off[kStrandMaxReads + 1];
-    strand_tables(mode, tf, tr);
-    const uint64_t lo = offs[0], hi = offs[n];
-    const uint64_t lo4 = lo & ~3ull;
-    const bool aligned = (reinterpret_cast<uintptr_t>(seqs) & 3) == 0;
-    const uint64_t nchunks = (hi - lo4 + kStrandChunk - 1) / kStrandChunk;
-    for (uint64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-        const uint64_t start = lo4 + ch * kStrandChunk;
-        __syncthreads();
-        const uint64_t r0 = chunk_first[ch];
-        const uint64_t r1 = ch + 1 < nchunks ? chunk_first[ch + 1] : n - 1;
-        const uint64_t nr = r1 - r0 + 1;  // reads overlapping the chunk (+ at most one)
-        const bool staged = nr <= kStrandMaxReads;
-        if (staged)
-            for (uint64_t i = threadIdx.x; i <= nr; i += blockDim.x) s_off[i] = offs[r0 + i];
-        __syncthreads();
-        uint64_t r = r0, rs = offs[r0], re = offs[r0 + 1];
-        for (uint32_t it = 0; it < kStrandIters; ++it) {
-            const uint64_t p0 = start + ((uint64_t)it * 256 + threadIdx.x) * 4;
-            if (p0 >= hi) break;
-            if (p0 >= lo) {
-                if (staged) {  // read containing p0: last staged offset <= p0
-                    uint32_t a = 0, b = (uint32_t)nr;
-                    while (b - a > 1) {
-                        const uint32_t m = (a + b) >> 1;
-                        if (s_off[m] <= p0) a = m; else b = m;
-                    }
-                    r = r0 + a;
-                    rs = s_off[a];
-                    re = s_off[a + 1];
-                } else {
-                    while (re <= p0) { ++r; rs = re; re = offs[r + 1]; }
-                }
-            }
-            uint32_t fw = 0, rw = 0;
-            const uint64_t m0 = rs + re - 1 - p0;  // mirror of p0 inside read r
-            if (aligned && p0 >= lo && p0 + 4 <= re && ((m0 - 3) & ~3ull) + 8 <= hi) {
-                // whole dword inside one read: one forward load, two mirror loads
-                const uint32_t x = *reinterpret_cast<const uint32_t*>(seqs + p0);
-                const uint64_t a = m0 - 3;
-                const uint32_t* pm = reinterpret_cast<const uint32_t*>(seqs + (a & ~3ull));
-                const uint32_t y = __builtin_bswap32(__builtin_amdgcn_alignbyte(pm[1], pm[0], (uint32_t)(a & 3)));
+// Bytes of dword i that belong to a k-mer of length k.
+__device__ __forceinline__ uint32_t tail_mask(int i, int k) {
+    const int valid = k - 4 * i;
+    return valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : ((1u << (8 * valid)) - 1u));
+}
+
+// k bytes of the read buffer at byte offset `off`, as 8 dwords, unmasked.
+// Dwords that start at or past the end of the buffer are not loaded (device
+// buffers handed over by the caller carry no padding).
+template <int KT>
+__device__ __forceinline__ void load_window(const uint8_t* seq, uint64_t seq_bytes, uint64_t off,
+                                            uint32_t k, uint32_t (&w)[8]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(seq) + off;
+    const uint32_t* p = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uintptr_t lim = reinterpret_cast<uintptr_t>(seq) + seq_bytes;
+    const uint32_t nw = KT ? (KT + 3) / 4 : (k + 3) / 4;
+    uint32_t raw[9];
 #pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
-                    fw |= (uint32_t)tf[(x >> (8 * b)) & 0xFF] << (8 * b);
-                    rw |= (uint32_t)tr[(y >> (8 * b)) & 0xFF] << (8 * b);
-                }
-            } else {
-                uint64_t rr = r, rrs = rs, rre = re;
+    for (int i = 0; i < 9; ++i)
+        raw[i] = (i <= (int)nw && reinterpret_cast<uintptr_t>(p + i) < lim) ? p[i] : 0u;
 #pragma unroll
-                for (uint32_t b = 0; b < 4; ++b) {
-                    const uint64_t p = p0 + b;
-                    if (p < lo || p >= hi) continue;
-                    while (rre <= p) { ++rr; rrs = rre; rre = offs[rr + 1]; }
-                    fw |= (uint32_t)tf[seqs[p]] << (8 * b);
-                    rw |= (uint32_t)tr[seqs[rrs + rre - 1 - p]] << (8 * b);
-                }
-            }
-            fwd[p0 >> 2] = fw;
-            rc[p0 >> 2] = rw;
+    for (int i = 0; i < 8; ++i) w[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
+}
+
+// Reverse complement of the k-byte window f (tail zero) when every byte is in
+// {A, C, G, T, N}: complement + byte-reverse the nw dwords, then drop the
+// 4*nw - k leading pad bytes.
+template <int NW>
+__device__ __forceinline__ void rc_perm_nw(const uint32_t (&f)[8], uint32_t sh, uint32_t (&r)[8]) {
+    uint32_t R[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) R[j] = j < NW ? __builtin_bswap32(comp4(f[NW - 1 - j])) : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) r[i] = __builtin_amdgcn_alignbyte(R[i + 1], R[i], sh);
+}
+
+template <int KT>
+__device__ __forceinline__ void rc_perm(const uint32_t (&f)[8], uint32_t k, uint32_t (&r)[8]) {
+    if constexpr (KT != 0) {
+        rc_perm_nw<(KT + 3) / 4>(f, (uint32_t)(4 * ((KT + 3) / 4) - KT), r);
+    } else {
+        const uint32_t nw = (k + 3) / 4, sh = 4 * nw - k;
+        switch (nw) {
+            case 1: rc_perm_nw<1>(f, sh, r); break;
+            case 2: rc_perm_nw<2>(f, sh, r); break;
+            case 3: rc_perm_nw<3>(f, sh, r); break;
+            case 4: rc_perm_nw<4>(f, sh, r); break;
+            case 5: rc_perm_nw<5>(f, sh, r); break;
+            case 6: rc_perm_nw<6>(f, sh, r); break;
+            case 7: rc_perm_nw<7>(f, sh, r); break;
+            default: rc_perm_nw<8>(f, sh, r); break;
         }
     }
 }
@@ -327,24 +320,15 @@ __device__ __forceinline__ uint64_t num_kmers(uint64_t len, uint32_t k, uint32_t
     return len >= k ? (len - k + step) / step : 0;  // ceil((len-k+1)/step)
 }
 
-// Per read: sampled k-mer count and #units; also the first read of every
-// strands chunk (the read holding byte max(chunk start, offs[0])).
+// Per read: sampled k-mer count and #units.
 __global__ void units_kernel(const uint64_t* __restrict__ offs, uint64_t n, uint32_t k,
                              uint32_t step, uint64_t* __restrict__ nk_out,
-                             uint64_t* __restrict__ nseg, uint32_t* __restrict__ chunk_first) {
-    const uint64_t lo = offs[0], lo4 = lo & ~3ull;
+                             uint64_t* __restrict__ nseg) {
     for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
          r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t a = offs[r], b = offs[r + 1];
-        const uint64_t nk = num_kmers(b - a, k, step);
+        const uint64_t nk = num_kmers(offs[r + 1] - offs[r], k, step);
         if (nk_out) nk_out[r] = nk;
         nseg[r] = (nk + kSegKmers - 1) / kSegKmers;
-        if (chunk_first && b > a) {
-            if (a <= lo && lo < b) chunk_first[0] = (uint32_t)r;
-            uint64_t c = (a - lo4 + kStrandChunk - 1) / kStrandChunk;
-            if (c < 1) c = 1;
-            for (; lo4 + c * kStrandChunk < b; ++c) chunk_first[c] = (uint32_t)r;
-        }
     }
 }
 
@@ -429,13 +413,39 @@ __device__ __forceinline__ uint4 and4(uint4 a, uint4 b) {
 }
 
 // Canonical k-mer of read position p (byte offset o0 of a read of length len).
-template <int KT>
+template <int KT, int MODE>
 __device__ __forceinline__ void kmer_at(const ReadView& rv, uint64_t o0, uint64_t len, uint64_t p,
                                         uint32_t k, Kmer& c) {
-    uint32_t f[8], q[8];
-    load_window<KT>(rv.fwd, o0 + p, k, f);
-    load_window<KT>(rv.rc, o0 + (len - p - k), k, q);
-    canonical_select(f, q, c);
+    (void)len;
+    const int kk = KT ? KT : (int)k;
+    uint32_t f[8], r[8];
+    load_window<KT>(rv.seq, rv.seq_bytes, o0 + p, k, f);
+    if constexpr (MODE == kStrandCobs) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) f[i] = cobs_norm4(f[i]) & tail_mask(i, kk);
+        rc_perm<KT>(f, k, r);
+    } else {
+        bool fast = true;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const uint32_t m = tail_mask(i, kk);
+            f[i] &= m;
+            const uint32_t ok = bytes_equal(f[i], 'A') | bytes_equal(f[i], 'C') | bytes_equal(f[i], 'G') |
+                                bytes_equal(f[i], 'T') | bytes_equal(f[i], 'N');
+            fast = fast && ((ok | ~m) & 0x80808080u) == 0x80808080u;
+        }
+        if (fast) {
+            rc_perm<KT>(f, k, r);
+        } else {  // IUPAC / lower case: per-byte table, bytes re-read from the read
+            const uint8_t* s = rv.seq + o0 + p;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] = 0;
+#pragma unroll
+            for (int i = 0; i < (int)kMaxK; ++i)
+                if (i < kk) r[i >> 2] |= bio_comp_byte(s[kk - 1 - i]) << (8 * (i & 3));
+        }
+    }
+    canonical_select(f, r, c);
 }
 
 // ------------------------------------------------------------------ COBS probe (fast)
@@ -500,7 +510,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
                 uint4 m = make_uint4(0u, 0u, 0u, 0u);
                 if (tb + lane < cnt) {
                     Kmer c;
-                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
                     uint32_t off[HT];
@@ -599,7 +609,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
                 uint64_t hv[HT ? HT : kMaxHashes];
                 if (act) {
                     Kmer c;
-                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
 #pragma unroll
@@ -733,7 +743,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
                 for (int j = 0; j < NH; ++j) hv[j] = 0;
                 if (act) {
                     Kmer c;
-                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
 #pragma unroll
@@ -874,7 +884,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
                 bool in = false;
                 if (tb + lane < cnt) {
                     Kmer c;
-                    kmer_at<KT>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kStrandBio>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     in = bloom_member<KT, KB>(c, k, bv);
                 }
                 c_unit += (uint32_t)__popcll(__ballot(in));
@@ -929,7 +939,7 @@ __global__ void __launch_bounds__(kProbeThreads) build_cobs_kernel(ReadView rv,
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
                 if (tb + lane >= cnt) continue;
                 Kmer c;
-                kmer_at<KT>(rv, o0, len, t0 + tb + lane, k, c);
+                kmer_at<KT, kStrandCobs>(rv, o0, len, t0 + tb + lane, k, c);
                 Xxh64Pre pre;
                 xxh64_pre<KT>(c, k, pre);
                 for (uint32_t j = 0; j < h; ++j) {
@@ -963,7 +973,7 @@ __global__ void __launch_bounds__(kProbeThreads) build_bloom_kernel(ReadView rv,
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
                 if (tb + lane >= cnt) continue;
                 Kmer c;
-                kmer_at<KT>(rv, o0, len, t0 + tb + lane, k, c);
+                kmer_at<KT, kStrandBio>(rv, o0, len, t0 + tb + lane, k, c);
                 uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
                 for (uint32_t j = 0; j < bv.K; ++j) {
                     const uint64_t pm = sl * kLcgMl;
@@ -1086,22 +1096,10 @@ static int resident_grid(K kernel, int threads, size_t lds) {
     return per_cu * prop.multiProcessorCount;
 }
 
-uint64_t strand_chunk_slots(uint64_t nbytes) { return nbytes / kStrandChunk + 3; }
-
-hipError_t launch_strands(const uint8_t* seqs, const uint64_t* offs, uint64_t n, uint64_t nbytes,
-                          int mode, uint8_t* fwd_out, uint8_t* rc_out, const uint32_t* chunk_first,
-                          hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    const int grid = grid_for(nbytes / kStrandChunk + 1, 1, 8192);
-    strands_kernel<<<grid, 256, 0, s>>>(seqs, offs, n, mode, reinterpret_cast<uint32_t*>(fwd_out),
-                                        reinterpret_cast<uint32_t*>(rc_out), chunk_first);
-    return hipGetLastError();
-}
-
 hipError_t launch_units(const uint64_t* offs, uint64_t n, uint32_t k, uint32_t step,
-                        uint64_t* nk_out, uint64_t* nseg, uint32_t* chunk_first, hipStream_t s) {
+                        uint64_t* nk_out, uint64_t* nseg, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    units_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(offs, n, k, step, nk_out, nseg, chunk_first);
+    units_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(offs, n, k, step, nk_out, nseg);
     return hipGetLastError();
 }
 
