@@ -688,17 +688,20 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 }
 
 // ------------------------------------------------------------------ COBS probe (slots)
-// Banks whose rows span at most NS 16-byte chunks over all doc groups
-// (classic D <= 16*128, compact schemes such as an MLST locus: 3 groups x 4
-// chunks).  Every chunk of every group's h rows is in flight before any
-// counting; per-doc counts of the unit live in registers, two 16-bit counters
-// per VGPR (a unit has <= 256 k-mers, so one lane-half count is <= 128);
-// block totals go to LDS with return-free ds_add.
-template <int KT, int HT, int NS>
+// Banks whose rows span at most GM groups x CM 16-byte chunks (classic
+// D <= 16*128 as GM = 1; compact schemes such as an MLST locus: 3 groups x 4
+// chunks).  The layout is compile-time, so every slot's group and chunk is a
+// constant; runtime guards only switch slots off.  Every chunk of every
+// group's h rows is in flight before any counting; per-doc counts of the unit
+// live in registers, two 16-bit counters per VGPR (a unit has <= 256 k-mers,
+// so one lane-half count is <= 128); block totals go to LDS with return-free
+// ds_add.
+template <int KT, int HT, int GM, int CM>
 __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv, CobsView bv,
                                                                      uint32_t* __restrict__ hits,
                                                                      uint64_t* __restrict__ partials,
                                                                      uint32_t dpad) {
+    constexpr int NS = GM * CM;
     extern __shared__ __attribute__((aligned(16))) uint64_t s_tot[];  // [dpad] per block
     __shared__ uint64_t s_kmers[kProbeThreads / kWave];
     const int lane = threadIdx.x & 63;
@@ -713,8 +716,8 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
     const uint32_t h = HT ? HT : bv.h;
     const uint32_t step = rv.step;
     const uint64_t D = bv.D;
-    const uint32_t cpg = bv.nchunks;       // chunks per group row
-    const uint32_t nslots = bv.G * cpg;    // <= NS (host-checked)
+    const uint32_t G = bv.G;               // <= GM (host-checked)
+    const uint32_t cpg = bv.nchunks;       // <= CM (host-checked)
     const uint64_t gdocs = 8 * bv.page;    // docs per group
     const uint64_t U = rv.queue[0];
     uint64_t kmer_total = 0;
@@ -751,62 +754,67 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
                         if ((uint32_t)j < h) hv[j] = xxh64_seed<KT>(c, pre, k, (uint64_t)j);
                 }
                 uint4 mk[NS];
-                uint64_t ro[NH];
 #pragma unroll
-                for (int j = 0; j < NH; ++j) ro[j] = 0;
+                for (int g = 0; g < GM; ++g) {
+                    uint64_t ro[NH];
 #pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    mk[i] = make_uint4(0u, 0u, 0u, 0u);
-                    if ((uint32_t)i < nslots) {
-                        const uint32_t g = (uint32_t)i / cpg;  // wave-uniform
-                        const uint32_t cc = (uint32_t)i - g * cpg;
-                        if (cc == 0) {
-                            const GroupDesc gd = bv.groups[g];
+                    for (int j = 0; j < NH; ++j) ro[j] = 0;
+                    if ((uint32_t)g < G) {
+                        const GroupDesc gd = bv.groups[g];
 #pragma unroll
-                            for (int j = 0; j < NH; ++j)
-                                if ((uint32_t)j < h) ro[j] = gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch;
-                        }
-                        if (act) {
-                            uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                        for (int j = 0; j < NH; ++j)
+                            if ((uint32_t)j < h) ro[j] = gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch;
+                    }
+#pragma unroll
+                    for (int cc = 0; cc < CM; ++cc) {
+                        uint4 m = make_uint4(0u, 0u, 0u, 0u);
+                        if ((uint32_t)g < G && (uint32_t)cc < cpg && act) {
+                            m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                             for (int j = 0; j < NH; ++j)
                                 if ((uint32_t)j < h)
                                     m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
-                            mk[i] = m;
+                        }
+                        mk[g * CM + cc] = m;
+                    }
+                }
+#pragma unroll
+                for (int g = 0; g < GM; ++g) {
+#pragma unroll
+                    for (int cc = 0; cc < CM; ++cc) {
+                        if ((uint32_t)g < G && (uint32_t)cc < cpg) {
+                            const int i = g * CM + cc;
+                            const uint32_t w[4] = {mk[i].x, mk[i].y, mk[i].z, mk[i].w};
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                if (__ballot(w[q] != 0u) != 0ull)  // some k-mer of the tile hits these docs
+                                    acc[2 * i + (q >> 1)] += column_popc32(w[q], X) << (16 * (q & 1));
                         }
                     }
                 }
-                // (guards, not break: a runtime exit keeps the loop rolled and mk[] in scratch)
-#pragma unroll
-                for (int i = 0; i < NS; ++i) {
-                    if ((uint32_t)i < nslots) {
-                        const uint32_t w[4] = {mk[i].x, mk[i].y, mk[i].z, mk[i].w};
-#pragma unroll
-                        for (int q = 0; q < 4; ++q)
-                            if (__ballot(w[q] != 0u) != 0ull)  // some k-mer of the tile hits these docs
-                                acc[2 * i + (q >> 1)] += column_popc32(w[q], X) << (16 * (q & 1));
-                    }
-                }
             }
-            // lane c < 32 holds doc 32q + c of chunk i after folding the halves
+            // lane c < 32 holds doc 32q + c of chunk (g, cc) after folding the halves
             const bool whole = nk <= kSegKmers;
 #pragma unroll
-            for (int i = 0; i < NS; ++i) {
-                if ((uint32_t)i >= nslots) continue;
-                const uint32_t g = (uint32_t)i / cpg;
-                const uint32_t cc = (uint32_t)i - g * cpg;
+            for (int g = 0; g < GM; ++g) {
+                if ((uint32_t)g >= G) continue;
                 const uint64_t glim = min(D, (uint64_t)g * gdocs + gdocs);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint64_t d0 = (uint64_t)g * gdocs + cc * 128 + q * 32;
-                    if (d0 >= glim) continue;
-                    const uint32_t v = fold_halves((acc[2 * i + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
-                    const uint64_t d = d0 + (uint64_t)lane;
-                    if (lane < 32 && d < glim) {
-                        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[d]), (unsigned long long)v);
-                        if (hits) {
-                            if (whole) hits[(uint64_t)r * D + d] = v;
-                            else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                for (int cc = 0; cc < CM; ++cc) {
+                    if ((uint32_t)cc >= cpg) continue;
+                    const int i = g * CM + cc;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint64_t d0 = (uint64_t)g * gdocs + cc * 128 + q * 32;
+                        if (d0 >= glim) continue;
+                        const uint32_t v = fold_halves((acc[2 * i + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
+                        const uint64_t d = d0 + (uint64_t)lane;
+                        if (lane < 32 && d < glim) {
+                            if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[d]), (unsigned long long)v);
+                            if (hits) {
+                                if (whole) hits[(uint64_t)r * D + d] = v;
+                                else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                            }
                         }
                     }
                 }
@@ -1173,33 +1181,65 @@ static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t
     return hipGetLastError();
 }
 
-// Slot kernel variant for banks whose rows span <= 16 chunks over all groups
-// (0: none).  D <= 16 * 128 follows, so LDS totals need <= 16 KB.
-static int slots_for(const CobsView& bv) {
-    const uint64_t n = (uint64_t)bv.G * bv.nchunks;
-    return n <= 4 ? 4 : n <= 8 ? 8 : n <= 12 ? 12 : n <= 16 ? 16 : 0;
+// Slot kernel shape (GM groups x CM chunks) for a bank, or {0, 0} when its
+// rows span more than 16 chunks (general kernel).  D <= 16 * 128 follows, so
+// the LDS totals need <= 16 KB.
+struct SlotShape {
+    int gm, cm;
+};
+static SlotShape slots_for(const CobsView& bv) {
+    const uint64_t G = bv.G, c = bv.nchunks;
+    if (G == 1) {
+        if (c <= 4) return {1, 4};
+        if (c <= 8) return {1, 8};
+        if (c <= 12) return {1, 12};
+        if (c <= 16) return {1, 16};
+        return {0, 0};
+    }
+    if (c == 1) return G <= 4 ? SlotShape{4, 1} : G <= 8 ? SlotShape{8, 1} : G <= 16 ? SlotShape{16, 1} : SlotShape{0, 0};
+    if (c == 2) return G <= 4 ? SlotShape{4, 2} : G <= 8 ? SlotShape{8, 2} : SlotShape{0, 0};
+    if (c <= 4) return G <= 2 ? SlotShape{2, 4} : G <= 3 ? SlotShape{3, 4} : G <= 4 ? SlotShape{4, 4} : SlotShape{0, 0};
+    return {0, 0};
 }
 
 using SlotsFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*, uint32_t);
 
 template <int KT, int HT>
-static SlotsFn slots_fn(int ns) {
-    switch (ns) {
-        case 4: return probe_cobs_slots<KT, HT, 4>;
-        case 8: return probe_cobs_slots<KT, HT, 8>;
-        case 12: return probe_cobs_slots<KT, HT, 12>;
-        default: return probe_cobs_slots<KT, HT, 16>;
+static SlotsFn slots_fn_classic(SlotShape s) {
+    switch (s.cm) {
+        case 4: return probe_cobs_slots<KT, HT, 1, 4>;
+        case 8: return probe_cobs_slots<KT, HT, 1, 8>;
+        case 12: return probe_cobs_slots<KT, HT, 1, 12>;
+        default: return probe_cobs_slots<KT, HT, 1, 16>;
     }
+}
+
+template <int KT, int HT>
+static SlotsFn slots_fn(SlotShape s) {
+    if (s.gm == 1) return slots_fn_classic<KT, HT>(s);
+    if (s.cm == 1) return s.gm == 4 ? probe_cobs_slots<KT, HT, 4, 1> : s.gm == 8 ? probe_cobs_slots<KT, HT, 8, 1>
+                                                                                  : probe_cobs_slots<KT, HT, 16, 1>;
+    if (s.cm == 2) return s.gm == 4 ? probe_cobs_slots<KT, HT, 4, 2> : probe_cobs_slots<KT, HT, 8, 2>;
+    return s.gm == 2 ? probe_cobs_slots<KT, HT, 2, 4> : s.gm == 3 ? probe_cobs_slots<KT, HT, 3, 4>
+                                                                  : probe_cobs_slots<KT, HT, 4, 4>;
 }
 
 static int kh_variant(uint32_t k, uint32_t h) { return (k == 21 && h == 7) ? 0 : (k == 31 && h == 1) ? 1 : 2; }
 
-static SlotsFn pick_slots(uint32_t k, uint32_t h, int ns) {
+static SlotsFn pick_slots(uint32_t k, uint32_t h, SlotShape s) {
     switch (kh_variant(k, h)) {
-        case 0: return slots_fn<21, 7>(ns);
-        case 1: return slots_fn<31, 1>(ns);
-        default: return slots_fn<0, 0>(ns);
+        case 0: return s.gm == 1 ? slots_fn_classic<21, 7>(s) : slots_fn<0, 0>(s);  // species banks are classic
+        case 1: return slots_fn<31, 1>(s);
+        default: return slots_fn<0, 0>(s);
     }
+}
+
+static int shape_index(SlotShape s) {  // 0..12, for the grid cache
+    static const int gms[13] = {1, 1, 1, 1, 4, 8, 16, 4, 8, 2, 3, 4, 0};
+    static const int cms[13] = {4, 8, 12, 16, 1, 1, 1, 2, 2, 4, 4, 4, 0};
+    for (int i = 0; i < 12; ++i)
+        if (gms[i] == s.gm && cms[i] == s.cm) return i;
+    return 12;
 }
 
 static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128 * 128) * sizeof(uint64_t); }
@@ -1207,16 +1247,17 @@ static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
-    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][4] = {};
+    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][13] = {};
     if (cobs_fast(bv, k)) {
         if (k == 21)
             return fast21 ? fast21 : (fast21 = resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0));
         return fast31 ? fast31 : (fast31 = resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0));
     }
-    if (const int ns = slots_for(bv)) {
+    const SlotShape sh = slots_for(bv);
+    if (sh.gm) {
         // LDS is 16 KB at most: residency is set by registers, not by D
-        int& g = slots[kh_variant(k, bv.h)][ns / 4 - 1];
-        return g ? g : (g = resident_grid(pick_slots(k, bv.h, ns), kProbeThreads, 16384));
+        int& g = slots[kh_variant(k, bv.h)][shape_index(sh)];
+        return g ? g : (g = resident_grid(pick_slots(k, bv.h, sh), kProbeThreads, 16384));
     }
     int wpb;
     size_t lds;
@@ -1239,9 +1280,10 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
         if (rv.k == 21) return launch_fast_t<21, 7>(rv, fb, hits, partials, blocks, s);
         return launch_fast_t<31, 1>(rv, fb, hits, partials, blocks, s);
     }
-    if (const int ns = slots_for(bv)) {
+    const SlotShape sh = slots_for(bv);
+    if (sh.gm) {
         const size_t lds = slots_lds(bv);
-        pick_slots(rv.k, bv.h, ns)<<<blocks, kProbeThreads, lds, s>>>(rv, bv, hits, partials,
+        pick_slots(rv.k, bv.h, sh)<<<blocks, kProbeThreads, lds, s>>>(rv, bv, hits, partials,
                                                                     (uint32_t)(lds / sizeof(uint64_t)));
         return hipGetLastError();
     }
