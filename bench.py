@@ -276,8 +276,8 @@ def main():
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
-            tr = json.loads(tj.read_text())
-            if tr.get("workload", "species") == args.workload and tr.get("reads") == wl.n:
+            tr = json.loads(tj.read_text()).get(args.workload) or {}
+            if tr.get("reads") == wl.n:  # measured on this workload at this size
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
