@@ -152,6 +152,13 @@ int xs_query_best(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint
 int xs_best_device(const uint32_t* d_hits, uint64_t n, uint64_t num_docs, uint32_t* d_best_doc,
                    uint32_t* d_best_hits, void* stream);
 
+/* Device-side read compaction (the genus -> species hand-off of the fused
+ * pipeline, replacing the filtered FASTA of src/xspect/main.py:116-145):
+ * output read j = input read d_index[j], written at d_out_offsets[j] (m+1
+ * entries, computed by the caller from the kept lengths), on `stream`. */
+int xs_gather_reads_device(const void* d_seqs, const uint64_t* d_offsets, const uint32_t* d_index, uint64_t m,
+                           void* d_out_seqs, const uint64_t* d_out_offsets, void* stream);
+
 /* MLST chunk scoring (probabilistic_filter_mlst_model.py:237-256): for chunk
  * hit rows hits[c][d] whose owner is seq_of_chunk[c] (non-decreasing), sum
  * hits[c][d] into scores[seq][d] only where hits[c][d] > threshold
@@ -199,6 +206,8 @@ typedef struct xs_fastx_batch {
     const uint64_t* id_offsets;  /* n+1 entries */
     uint64_t text_offset;        /* file bytes consumed so far */
     uint64_t text_bytes;         /* file size */
+    const char* descs;           /* record titles (header line minus '>'/'@', right-stripped) */
+    const uint64_t* desc_offsets;/* n+1 entries */
 } xs_fastx_batch;
 
 /* threads <= 0: up to 16.  The file is memory-mapped until xs_fastx_close. */
@@ -209,6 +218,15 @@ int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx
  * Malformed records return XS_ERR_FORMAT with Biopython's message. */
 int xs_fastx_next(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_batch* out);
 void xs_fastx_close(xs_fastx* reader);
+
+/* Write records as Bio.SeqIO.write(record, fh, "fasta") does (the genus
+ * filter's output, src/xspect/file_io.py:166-191): ">" title, then the
+ * sequence in lines of `width` (60) characters.  Records r = index[i] for
+ * i < n (index NULL: r = i) of a packed batch (seqs/offsets, titles/desc_offs,
+ * e.g. an xs_fastx_batch).  append = 0 truncates the file first. */
+int xs_write_fasta(const char* path, int append, const char* seqs, const uint64_t* offsets,
+                   const char* descs, const uint64_t* desc_offsets, const uint32_t* index, uint64_t n,
+                   uint32_t width);
 
 #ifdef __cplusplus
 }

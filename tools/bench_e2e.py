@@ -139,6 +139,47 @@ def main():
     for f in (out, tmp / "small_dicts.json", tmp / "small_columnar.json"):
         f.unlink()
 
+    # fused genus -> species pipeline vs the reference's three passes, on 200k reads
+    from xspect_amd.bank import bloom_parameters
+    from xspect_amd.pipeline import reference_pipeline, run_pipeline
+    from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+    half = args.docs // 2  # the genus filter holds half of the species: about half of the reads pass
+    gsz = genomes[:half].size
+    nb, nh = bloom_parameters(gsz - k + 1, 0.01)
+    gbank = Bank.create_bloom(k, nb, nh, device=0)
+    g = torch.from_numpy(genomes[:half].reshape(-1)).to(dev)
+    go = torch.arange(half + 1, dtype=torch.int64, device=dev) * args.genome_len
+    gbank.build_device(g, gsz, go, half, None, stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    del g
+    genus = ProbabilisticSingleFilterModel(k, "Synthetic", None, None, "Genus", tmp / "models")
+    genus.bf = genus.index = gbank
+    genus.display_names = {"Synthetic": "Synthetic"}
+    species = ProbabilisticFilterModel(k, "Synthetic", None, None, "Species", tmp / "models")
+    species.index = bank
+    species.display_names = {nm: nm for nm in bank.doc_names}
+    R = min(reads.shape[0], 200_000)
+    sub = tmp / "sub.fastq"
+    with open(sub, "wb") as fh:
+        for i in range(R):
+            fh.write(b"@r%d\n%s\n+\n%s\n" % (i, reads[i].tobytes(), qual))
+    quiet = lambda *a: None  # noqa: E731
+    t = time.perf_counter()
+    outf = run_pipeline(genus, species, sub, tmp / "fused", threshold=0.7, run_id="x", log=quiet)
+    res["pipeline_fused_s"] = time.perf_counter() - t
+    t = time.perf_counter()
+    outr = reference_pipeline(genus, species, sub, tmp / "three_pass", threshold=0.7, run_id="x", log=quiet)
+    res["pipeline_three_pass_s"] = time.perf_counter() - t
+    res["pipeline_reads"] = R
+    res["pipeline_kept_reads"] = outf["filtered"][0].read_bytes().count(b">") if outf["filtered"] else 0
+    res["pipeline_identical"] = all(a.read_bytes() == b.read_bytes() for key in ("genus", "filtered", "species")
+                                    for a, b in zip(outf[key], outr[key]))
+    import shutil
+    shutil.rmtree(tmp / "fused")
+    shutil.rmtree(tmp / "three_pass")
+    sub.unlink()
+
     # record-at-a-time Python parse on a bounded sample, scaled to the file
     sys.path.insert(0, str(ROOT / "oracle"))
     import fastx as ofx  # test/bench-only restatement of Bio.SeqIO

@@ -67,6 +67,8 @@ class FastxBatch(ctypes.Structure):
         ("id_offsets", ctypes.c_void_p),
         ("text_offset", ctypes.c_uint64),
         ("text_bytes", ctypes.c_uint64),
+        ("descs", ctypes.c_void_p),
+        ("desc_offsets", ctypes.c_void_p),
     ]
 
 
@@ -97,6 +99,7 @@ SIGNATURES = {
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "xs_query_best": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
+    "xs_gather_reads_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "xs_best_device": (_int, [_vp, _u64, _u64, _vp, _vp, _vp]),
     "xs_mlst_sum": (_int, [_vp, _vp, _vp, _u64, _u64, _u32, _vp]),
     "xs_bank_set_profiling": (_int, [_vp, _int]),
@@ -109,6 +112,7 @@ SIGNATURES = {
     "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),
     "xs_fastx_close": (None, [_vp]),
+    "xs_write_fasta": (_int, [ctypes.c_char_p, _int, _vp, _vp, ctypes.c_char_p, _vp, _vp, _u64, _u32]),
 }
 
 _LIB = None

@@ -259,6 +259,12 @@ def best_device(hits, n: int, num_docs: int, best, best_hits=None, stream: int |
     check(load().xs_best_device(_dptr(hits), n, num_docs, _dptr(best), _dptr(best_hits), stream))
 
 
+def gather_reads_device(seqs, offsets, index, m: int, out_seqs, out_offsets, stream: int | None = None) -> None:
+    """xs_gather_reads_device: out read j = read index[j] at out_offsets[j]."""
+    check(load().xs_gather_reads_device(_dptr(seqs), _dptr(offsets), _dptr(index), m, _dptr(out_seqs),
+                                        _dptr(out_offsets), stream))
+
+
 def _dptr(x) -> int | None:
     """Device pointer of a torch tensor, or an int pointer, or None."""
     if x is None:

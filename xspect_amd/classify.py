@@ -103,3 +103,31 @@ def classify_mlst(input_path: Path, organism: str, mlst_scheme: str, output_path
         path = out_path(idx, Path(output_path))
         result.save(path)
         print(f"Saved result as {path.name}")
+
+
+def classify_pipeline(model_genus: str, input_path: Path, output_dir: Path | None = None, threshold: float = 0.7,
+                      sparse_sampling_step: int = 1, display_names: bool = False, validation: bool = False,
+                      mlst_scheme: str | None = None):
+    """The full pipeline of ``xspect`` (``src/xspect/main.py:84-187`` all_pipeline):
+    genus filter, species classification, MLST for A. baumannii, as one fused
+    GPU pass per input file (xspect_amd.pipeline).  ``mlst_scheme`` names the
+    abaumannii scheme (the reference takes the first one it has downloaded)."""
+    from .pipeline import run_pipeline
+    from .probabilistic_filter_model import ProbabilisticFilterModel
+    from .probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+    from .probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+
+    if validation:
+        raise NotImplementedError("validation (alignment-based misclassification detection) "
+                                  "is outside the GPU probe path")
+    genus = ProbabilisticSingleFilterModel.load(genus_model_path(model_genus))
+    spath = species_model_path(model_genus)
+    species = (ProbabilisticFilterSVMModel if is_svm_model(spath) else ProbabilisticFilterModel).load(spath)
+    mlst = None
+    if mlst_scheme is not None:
+        from .probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+        p = mlst_model_path("abaumannii", mlst_scheme)
+        if p.exists():
+            mlst = ProbabilisticFilterMlstSchemeModel.load(p)
+    return run_pipeline(genus, species, Path(input_path), output_dir, threshold, sparse_sampling_step,
+                        display_names, mlst=mlst)

@@ -760,6 +760,15 @@ int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_
     return XS_OK;
 }
 
+int xs_gather_reads_device(const void* d_seqs, const uint64_t* d_offsets, const uint32_t* d_index, uint64_t m,
+                           void* d_out_seqs, const uint64_t* d_out_offsets, void* stream) {
+    if (m && (!d_seqs || !d_offsets || !d_index || !d_out_seqs || !d_out_offsets))
+        return fail(XS_ERR_ARG, "null argument");
+    HIPCHK(launch_gather_reads(static_cast<const uint8_t*>(d_seqs), d_offsets, d_index, m,
+                               static_cast<uint8_t*>(d_out_seqs), d_out_offsets, static_cast<hipStream_t>(stream)));
+    return XS_OK;
+}
+
 int xs_best_device(const uint32_t* d_hits, uint64_t n, uint64_t num_docs, uint32_t* d_best_doc,
                    uint32_t* d_best_hits, void* stream) {
     if ((!d_hits || !d_best_doc) && n) return fail(XS_ERR_ARG, "null argument");

@@ -101,21 +101,26 @@ struct HostBuf {
 
 // One thread's records.
 struct Part {
-    std::string seq, ids;
-    std::vector<uint64_t> lens, id_lens;
+    std::string seq, ids, descs;
+    std::vector<uint64_t> lens, id_lens, desc_lens;
     std::string err;
     const char* stop = nullptr;  // where parsing ended (next record start)
     void clear() {
         seq.clear();
         ids.clear();
+        descs.clear();
         lens.clear();
         id_lens.clear();
+        desc_lens.clear();
         err.clear();
         stop = nullptr;
     }
 };
 
+// Record title (header minus '>'/'@', right-stripped) and id (its first token).
 void push_id(Part& out, const char* tb, const char* te) {
+    out.descs.append(tb, (size_t)(te - tb));
+    out.desc_lens.push_back((uint64_t)(te - tb));
     while (tb < te && is_ws((unsigned char)*tb)) ++tb;
     const char* t = tb;
     while (t < te && !is_ws((unsigned char)*t)) ++t;
@@ -301,7 +306,7 @@ bool fastq_wrapped(const char* p, const char* end) {
 }
 
 struct Batch {
-    HostBuf seqs, offs, ids, id_offs;
+    HostBuf seqs, offs, ids, id_offs, descs, desc_offs;
     uint64_t n = 0, seq_bytes = 0;
 };
 
@@ -424,34 +429,42 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     if (got || r->cur >= r->size || !nparts) break;
     }
     // pack the parts
-    uint64_t n = 0, sbytes = 0, ibytes = 0;
+    uint64_t n = 0, sbytes = 0, ibytes = 0, dbytes = 0;
     for (int i = 0; i < nparts; ++i) {
         n += r->parts[i].lens.size();
         sbytes += r->parts[i].seq.size();
         ibytes += r->parts[i].ids.size();
+        dbytes += r->parts[i].descs.size();
     }
     if (int rc = bt.seqs.ensure(sbytes + 64)) return rc;
     if (int rc = bt.offs.ensure((n + 1) * 8)) return rc;
     if (int rc = bt.ids.ensure(ibytes + 1)) return rc;
     if (int rc = bt.id_offs.ensure((n + 1) * 8)) return rc;
+    if (int rc = bt.descs.ensure(dbytes + 1)) return rc;
+    if (int rc = bt.desc_offs.ensure((n + 1) * 8)) return rc;
     auto* offs = reinterpret_cast<uint64_t*>(bt.offs.p);
     auto* ioffs = reinterpret_cast<uint64_t*>(bt.id_offs.p);
-    std::vector<uint64_t> rec0(nparts + 1, 0), s0(nparts + 1, 0), i0(nparts + 1, 0);
+    auto* doffs = reinterpret_cast<uint64_t*>(bt.desc_offs.p);
+    std::vector<uint64_t> rec0(nparts + 1, 0), s0(nparts + 1, 0), i0(nparts + 1, 0), d0(nparts + 1, 0);
     for (int i = 0; i < nparts; ++i) {
         rec0[i + 1] = rec0[i] + r->parts[i].lens.size();
         s0[i + 1] = s0[i] + r->parts[i].seq.size();
         i0[i + 1] = i0[i] + r->parts[i].ids.size();
+        d0[i + 1] = d0[i] + r->parts[i].descs.size();
     }
     auto pack = [&](int i) {
         const Part& pt = r->parts[i];
         if (!pt.seq.empty()) memcpy(bt.seqs.p + s0[i], pt.seq.data(), pt.seq.size());
         if (!pt.ids.empty()) memcpy(bt.ids.p + i0[i], pt.ids.data(), pt.ids.size());
-        uint64_t so = s0[i], io = i0[i];
+        if (!pt.descs.empty()) memcpy(bt.descs.p + d0[i], pt.descs.data(), pt.descs.size());
+        uint64_t so = s0[i], io = i0[i], dd = d0[i];
         for (size_t j = 0; j < pt.lens.size(); ++j) {
             offs[rec0[i] + j] = so;
             ioffs[rec0[i] + j] = io;
+            doffs[rec0[i] + j] = dd;
             so += pt.lens[j];
             io += pt.id_lens[j];
+            dd += pt.desc_lens[j];
         }
     };
     {
@@ -462,6 +475,7 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     }
     offs[n] = sbytes;
     ioffs[n] = ibytes;
+    doffs[n] = dbytes;
     memset(bt.seqs.p + sbytes, 0, 64);  // defined bytes past the end
     bt.n = n;
     bt.seq_bytes = sbytes;
@@ -474,9 +488,51 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     out->id_offsets = ioffs;
     out->text_offset = r->cur;
     out->text_bytes = r->size;
+    out->descs = bt.descs.p;
+    out->desc_offsets = doffs;
     return XS_OK;
 }
 
 void xs_fastx_close(xs_fastx* r) { delete r; }
+
+int xs_write_fasta(const char* path, int append, const char* seqs, const uint64_t* offsets, const char* descs,
+                   const uint64_t* desc_offsets, const uint32_t* index, uint64_t n, uint32_t width) {
+    if (!path || (n && (!seqs || !offsets || !desc_offsets))) return xs::set_error(XS_ERR_ARG, "null argument");
+    if (width == 0) return xs::set_error(XS_ERR_ARG, "width must be >= 1");
+    FILE* f = fopen(path, append ? "ab" : "wb");
+    if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot open ") + path).c_str());
+    const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, n / 4096));
+    const uint64_t block = 1 << 15;
+    std::vector<std::string> out((size_t)T);
+    bool ok = true;
+    for (uint64_t b0 = 0; b0 < n && ok; b0 += block) {
+        const uint64_t b1 = std::min(n, b0 + block), per = (b1 - b0 + T - 1) / T;
+        auto work = [&](int t) {
+            std::string& o = out[t];
+            o.clear();
+            const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
+            for (uint64_t i = lo; i < hi; ++i) {
+                const uint64_t r = index ? index[i] : i;
+                o += '>';
+                o.append(descs + desc_offsets[r], (size_t)(desc_offsets[r + 1] - desc_offsets[r]));
+                o += '\n';
+                const char* s = seqs + offsets[r];
+                const uint64_t len = offsets[r + 1] - offsets[r];
+                for (uint64_t p = 0; p < len; p += width) {
+                    o.append(s + p, (size_t)std::min<uint64_t>(width, len - p));
+                    o += '\n';
+                }
+            }
+        };
+        std::vector<std::thread> th;
+        for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+        work(0);
+        for (auto& x : th) x.join();
+        for (int t = 0; t < T && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
+    }
+    if (fclose(f) != 0) ok = false;
+    if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
+    return XS_OK;
+}
 
 }  // extern "C"

@@ -98,6 +98,9 @@ constexpr uint32_t kBestAmbiguous = 0xFFFFFFFFu;
 hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_t* best,
                            uint32_t* best_hits, hipStream_t s);
 
+hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
+                               uint8_t* out, const uint64_t* out_offs, hipStream_t s);
+
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
 

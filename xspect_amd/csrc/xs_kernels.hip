@@ -1082,6 +1082,25 @@ __global__ void __launch_bounds__(256) best_doc_kernel(const uint32_t* __restric
     }
 }
 
+// ------------------------------------------------------------------ read gather
+// out read j = in read index[j], at out_offs[j] (computed by the caller): the
+// device-side compaction of reads that passed the genus filter.  One wave per
+// read, lanes copy bytes (coalesced 64-byte runs).
+__global__ void __launch_bounds__(256) gather_reads_kernel(const uint8_t* __restrict__ seqs,
+                                                           const uint64_t* __restrict__ offs,
+                                                           const uint32_t* __restrict__ index, uint64_t m,
+                                                           uint8_t* __restrict__ out,
+                                                           const uint64_t* __restrict__ out_offs) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t j = wave; j < m; j += waves) {
+        const uint32_t r = index[j];
+        const uint64_t a = offs[r], len = offs[r + 1] - a, o = out_offs[j];
+        for (uint64_t i = (uint64_t)lane; i < len; i += 64) out[o + i] = seqs[a + i];
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 static inline int grid_for(uint64_t work, int per_block, int cap) {
     uint64_t g = (work + per_block - 1) / per_block;
@@ -1353,6 +1372,13 @@ hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_
                            uint32_t* best_hits, hipStream_t s) {
     if (n == 0 || D == 0) return hipSuccess;
     best_doc_kernel<<<grid_for(n, 4, 16384), 256, 0, s>>>(hits, n, D, best, best_hits);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
+                               uint8_t* out, const uint64_t* out_offs, hipStream_t s) {
+    if (m == 0) return hipSuccess;
+    gather_reads_kernel<<<grid_for(m, 4, 16384), 256, 0, s>>>(seqs, offs, index, m, out, out_offs);
     return hipGetLastError();
 }
 

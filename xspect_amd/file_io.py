@@ -69,10 +69,14 @@ class SeqBatch:
             ioffs = np.ctypeslib.as_array(ctypes.cast(fb.id_offsets, ctypes.POINTER(ctypes.c_uint64)), (n + 1,))
             self._ids_raw = ctypes.string_at(fb.ids, int(ioffs[n])) if ioffs[n] else b""
             self._ioffs = ioffs.copy()
+            doffs = np.ctypeslib.as_array(ctypes.cast(fb.desc_offsets, ctypes.POINTER(ctypes.c_uint64)), (n + 1,))
+            self._descs_raw = ctypes.string_at(fb.descs, int(doffs[n])) if doffs[n] else b""
+            self._doffs = doffs.copy()
         else:
             offs = np.zeros(1, dtype=np.uint64)
             buf = np.zeros(1, dtype=np.uint8)
             self._ids_raw, self._ioffs = b"", np.zeros(1, dtype=np.uint64)
+            self._descs_raw, self._doffs = b"", np.zeros(1, dtype=np.uint64)
         self.packed = PackedReads(buf, offs)
 
     def ids(self) -> list[str]:
@@ -82,8 +86,24 @@ class SeqBatch:
             return [s[o[i]:o[i + 1]] for i in range(self.n)]
         return [raw[o[i]:o[i + 1]].decode("utf-8", errors="replace") for i in range(self.n)]
 
+    def descriptions(self) -> list[str]:
+        """Record titles (header line without '>'/'@', right-stripped)."""
+        raw, o = self._descs_raw, self._doffs.tolist()
+        return [raw[o[i]:o[i + 1]].decode("utf-8", errors="replace") for i in range(self.n)]
+
     def lengths(self) -> np.ndarray:
         return self.packed.lengths()
+
+    def write_fasta(self, path: Path, index: np.ndarray | None = None, append: bool = True) -> None:
+        """Append records (all, or those in `index`) to a FASTA file the way
+        Bio.SeqIO.write(record, fh, "fasta") does (file_io.py:188-191)."""
+        idx = None if index is None else np.ascontiguousarray(index, dtype=np.uint32)
+        n = self.n if idx is None else int(idx.size)
+        vp = ctypes.c_void_p
+        check(load().xs_write_fasta(str(path).encode(), 1 if append else 0, vp(self.packed.buf.ctypes.data),
+                                    vp(self.packed.offsets.ctypes.data), self._descs_raw,
+                                    vp(self._doffs.ctypes.data), vp(idx.ctypes.data) if idx is not None and n else None,
+                                    n, 60))
 
     def records(self) -> list[Record]:
         buf, o = self.packed.buf, self.packed.offsets.tolist()
