@@ -47,6 +47,31 @@ HBM_PEAK_GBS = 8000.0
 # shows 128 B fills"; profiles/r01_pmc_probe.txt shows TCC_EA0_RDREQ_128B ==
 # TCC_EA0_RDREQ (915.9 M per launch, 32B/64B requests ~0), so 128 B it is.
 ROW_BYTES = 128
+# Rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo
+# collectives through host copies (RCCL does not share a device between ranks).
+SHARE_GPU = os.environ.get("XSPECT_BENCH_SHARE_GPU") == "1"
+
+
+def all_reduce(t, op=None):
+    import torch.distributed as dist
+    op = dist.ReduceOp.SUM if op is None else op
+    if SHARE_GPU:
+        c = t.cpu()
+        dist.all_reduce(c, op=op)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=op)
+
+
+def all_gather(outs, t):
+    import torch.distributed as dist
+    if SHARE_GPU:
+        cs = [o.cpu() for o in outs]
+        dist.all_gather(cs, t.cpu())
+        for o, c in zip(outs, cs):
+            o.copy_(c)
+    else:
+        dist.all_gather(outs, t)
 
 
 def parse():
@@ -188,16 +213,15 @@ class Workload:
                        "signature_rows": int(sum(sum(g) for g in group_rows))}
 
     def step(self):
-        import torch.distributed as dist
         for b, h, t in zip(self.banks, self.d_hits, self.d_tot):
             b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step, h, self.d_nk, t,
                            stream=self.stream)
         if self.world > 1:
             if self.args.workload == "multigenus":
-                dist.all_gather(self.gathered, self.d_hits[0])  # docs sharded: hit vectors over xGMI
+                all_gather(self.gathered, self.d_hits[0])  # docs sharded: hit vectors over xGMI
             else:
                 for t in self.d_tot:
-                    dist.all_reduce(t)  # per-doc totals + k-mer total over all ranks
+                    all_reduce(t)  # per-doc totals + k-mer total over all ranks
 
     def probes_per_step(self):
         per_rank = self.kmers * sum(self.docs)
@@ -224,10 +248,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(rank, f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if SHARE_GPU:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if SHARE_GPU:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
     stream = torch.cuda.current_stream(dev)
     t_setup = time.time()
     wl = Workload(args, rank, world, dev, stream)
@@ -260,7 +289,7 @@ def main():
     probe_ms = probe_ms_total / max(1, launches)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     # sanity of the last step: whole-job k-mer totals
@@ -276,7 +305,9 @@ def main():
     tj = Path(args.traffic_json)
     if tj.exists():
         try:
-            tr = json.loads(tj.read_text()).get(args.workload) or {}
+            data = json.loads(tj.read_text())
+            # multigenus runs the species kernel on a bank of the same size
+            tr = data.get(args.workload) or (data.get("species") if args.workload == "multigenus" else None) or {}
             if tr.get("reads") == wl.n:  # measured on this workload at this size
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:
