@@ -42,6 +42,8 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0
+# BASELINE.json "metric", verbatim (the line reports one N of the 1/2/4/8 curve)
+METRIC = "k-mer\u00d7filter probes/s (150bp reads, ~100-species Bloom bank) at 1/2/4/8 GPUs"
 # Bytes one random row (or filter dword) costs: the gfx950 L2 fills a whole
 # 128-byte line per miss.  SURVEY.md §8(d) prices a row at 64 B "unless rocprof
 # shows 128 B fills"; profiles/r01_pmc_probe.txt shows TCC_EA0_RDREQ_128B ==
@@ -326,7 +328,7 @@ def main():
            "mlst": f"reads sharded x{world}, loci banks replicated, RCCL all-reduce of totals",
            "multigenus": f"docs sharded x{world} (one bank per GPU), reads replicated, RCCL all-gather of hits"}
     line = {
-        "metric": "k-mer x filter probes/s (150bp reads, ~100-species Bloom bank)",
+        "metric": METRIC,
         "value": value,
         "unit": "probes/s",
         "n_gpus": world,

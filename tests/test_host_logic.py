@@ -178,3 +178,16 @@ def test_slice_reads():
     pr = pack_sequences(["AAA", "CC", "GGGG", "T"])
     s = distributed.slice_reads(pr, 1, 3)
     assert s.offsets.tolist() == [0, 2, 6] and s.buf[:6].tobytes() == b"CCGGGG"
+
+
+def test_bench_metric_is_baseline_metric():
+    """bench.py reports BASELINE.json's metric verbatim (driver contract)."""
+    import importlib.util
+    import json
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parents[1]
+    spec = importlib.util.spec_from_file_location("bench_mod", root / "bench.py")
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.METRIC == json.loads((root / "BASELINE.json").read_text())["metric"]
