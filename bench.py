@@ -315,6 +315,8 @@ def main():
         except Exception:
             traffic = None
 
+    host = host_path(wl, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args)
@@ -355,6 +357,7 @@ def main():
             **({"note": wl.roofline_note} if wl.roofline_note else {}),
         },
         "cpu_baseline": cpu,
+        "host_path": host,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -397,6 +400,7 @@ def cpu_baseline(wl, args):
         extra = max(1, int(args.cpu_seconds / max(dt, 1e-3)) - 1)
         dt += sum(run(m2)[0] for _ in range(extra))
         passes += extra
+    ref_style = reference_style_baseline(wl, args, obanks)
     mism = 0
     probes = 0
     for (hits, nk), d_h in zip(outs, wl.d_hits):
@@ -408,7 +412,59 @@ def cpu_baseline(wl, args):
         "sample": f"{passes} pass(es) over {m2} of the benchmark reads x {len(obanks)} bank(s) "
                   f"({probes} probes) in {dt:.1f}s with the C oracle (OpenMP, {threads} threads)",
         "parity_sample_mismatches": mism,
+        "reference_style": ref_style,
     }
+
+
+def host_path(wl, args, reps=3):
+    """The same step from host buffers (SURVEY.md §8(d) time (i)): packed reads
+    in pageable host memory -> H2D -> kernels -> D2H of the n x D hit matrix
+    (xs_query), and of the totals only (xs_query_totals).  PCIe-inclusive;
+    never the headline value, which starts with the reads in HBM."""
+    from xspect_amd.packing import pack_fixed
+
+    pr = pack_fixed(wl.reads)
+    out = {}
+    for name, fn in (("hits", lambda b: b.query(pr, step=args.step)),
+                     ("totals", lambda b: b.query_totals(pr, step=args.step))):
+        for b in wl.banks:  # warm
+            fn(b)
+        t = time.perf_counter()
+        for _ in range(reps):
+            for b in wl.banks:
+                fn(b)
+        dt = (time.perf_counter() - t) / reps
+        out[name] = {"ms_per_step": dt * 1e3, "probes_per_s": wl.probes_per_step() / wl.world / dt}
+    out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H (hits: n x D uint32 matrix; "
+                   "totals: D+1 counters); the headline value starts with the reads in HBM")
+    return out
+
+
+def reference_style_baseline(wl, args, obanks, m=10_000):
+    """SURVEY.md §8(d) CPU baseline (ii): the reference's loop shape, one
+    native query per read from a Python loop plus the per-read result
+    dictionary (probabilistic_filter_model.py:291-310, :227, :393-409), on one
+    core over a 10k-read subset; extrapolated to probes/s."""
+    import numpy as np
+
+    m = min(m, wl.n)
+    names = [[str(d) for d in range(n)] for n in wl.docs]
+    t = time.perf_counter()
+    probes = 0
+    for i in range(m):
+        read = wl.reads[i]
+        buf = np.concatenate([read, np.zeros(1, dtype=np.uint8)])
+        offs = np.array([0, read.size], dtype=np.uint64)
+        for ob, nm in zip(obanks, names):
+            hits, nk = ob.query_packed(buf, offs, step=args.step, threads=1)
+            row = hits.reshape(-1)
+            order = np.argsort(-row.astype(np.int64), kind="stable")
+            _ = {nm[j]: int(row[j]) for j in order.tolist()}
+            probes += int(nk[0]) * len(nm)
+    dt = time.perf_counter() - t
+    return {"value": probes / dt, "unit": "probes/s", "cores": 1,
+            "sample": f"{m} reads, one oracle query + result dict per read from a Python loop, "
+                      f"{dt:.1f}s (the reference's per-read loop shape; its C++/Rust libraries are absent)"}
 
 
 if __name__ == "__main__":
