@@ -27,6 +27,7 @@
 #include <fstream>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "xs_internal.h"
@@ -81,6 +82,42 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging for large device -> pageable-host copies.
+struct PinnedBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return XS_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
+        if (e != hipSuccess) return fail(XS_ERR_HIP, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        cap = bytes;
+        return XS_OK;
+    }
+    ~PinnedBuf() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
+// memcpy on up to `threads` host threads.
+void par_memcpy(void* dst, const void* src, size_t n, int threads) {
+    if (n < (4u << 20) || threads <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t per = (n + threads - 1) / threads;
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) {
+        const size_t a = per * t;
+        if (a >= n) break;
+        th.emplace_back([=] { memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, std::min(per, n - a)); });
+    }
+    memcpy(dst, src, std::min(per, n));
+    for (auto& x : th) x.join();
+}
+
 }  // namespace
 
 struct xs_bank {
@@ -101,6 +138,8 @@ struct xs_bank {
     // workspace
     DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
         best;
+    PinnedBuf stage[2];             // D2H staging ring for large host outputs
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -456,6 +495,51 @@ int stage_host_reads(xs_bank* b, const char* seqs, const uint64_t* offsets, uint
     return XS_OK;
 }
 
+// Device -> pageable host copy of `bytes`, ordered after the work already on
+// the bank stream.  Large copies go through a pinned two-slot ring: the DMA of
+// chunk i overlaps the host copy of chunk i-1 (a plain pageable D2H runs at
+// about 9 GB/s on the box, a pinned one at PCIe rate).  Returns once the data
+// is in `host`.
+int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes) {
+    constexpr size_t kChunk = 32u << 20;
+    bool pinned = false;
+    if (bytes >= 2 * kChunk) {
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, host) == hipSuccess) pinned = attr.type == hipMemoryTypeHost;
+        else (void)hipGetLastError();  // pageable memory is "not a HIP pointer"
+    }
+    if (bytes < 2 * kChunk || pinned) {
+        HIPCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        return XS_OK;
+    }
+    for (int s = 0; s < 2; ++s) {
+        if (int rc = b->stage[s].ensure(kChunk)) return rc;
+        if (!b->stage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b->stage_ev[s], hipEventDisableTiming));
+    }
+    const unsigned hw = std::thread::hardware_concurrency();
+    const int threads = (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+    size_t prev_off = 0, prev_n = 0;
+    int prev_slot = -1;
+    for (size_t off = 0, i = 0; off < bytes; off += kChunk, ++i) {
+        const int slot = (int)(i & 1);
+        const size_t n = std::min(kChunk, bytes - off);
+        HIPCHK(hipMemcpyAsync(b->stage[slot].p, static_cast<const char*>(dev) + off, n, hipMemcpyDeviceToHost,
+                              b->stream));
+        HIPCHK(hipEventRecord(b->stage_ev[slot], b->stream));
+        if (prev_slot >= 0) {
+            HIPCHK(hipEventSynchronize(b->stage_ev[prev_slot]));
+            par_memcpy(static_cast<char*>(host) + prev_off, b->stage[prev_slot].p, prev_n, threads);
+        }
+        prev_off = off;
+        prev_n = n;
+        prev_slot = slot;
+    }
+    HIPCHK(hipEventSynchronize(b->stage_ev[prev_slot]));
+    par_memcpy(static_cast<char*>(host) + prev_off, b->stage[prev_slot].p, prev_n, threads);
+    return XS_OK;
+}
+
 xs_bank* new_bank(int device, int kind) {
     xs_bank* b = new xs_bank();
     b->device = device;
@@ -721,7 +805,8 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
         d_nk = b->nk.as<uint64_t>();
     }
     if (int rc = run_query(b, in, step, d_hits, d_nk, nullptr, b->stream)) return rc;
-    if (hits_out) HIPCHK(hipMemcpyAsync(hits_out, d_hits, n * cols * 4, hipMemcpyDeviceToHost, b->stream));
+    if (hits_out)
+        if (int rc = d2h_pageable(b, hits_out, d_hits, n * cols * 4)) return rc;
     if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
@@ -885,6 +970,8 @@ void xs_bank_close(xs_bank* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (auto& ev : b->stage_ev)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->events) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
