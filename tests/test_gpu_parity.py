@@ -199,6 +199,61 @@ def test_device_api_with_torch_stream(xs, oracle_mod):
     gb.close()
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_device_api_unaligned_tight_buffers(xs, oracle_mod, shift):
+    """Reads handed over at an unaligned device address, the last read ending
+    at the last byte of the buffer, offsets not starting at 0, ragged lengths,
+    mixed case and N (window loads stop at the buffer end)."""
+    torch = pytest.importorskip("torch")
+    rng = np.random.default_rng(shift)
+    for D, k, h, sig, bloom in [(100, 21, 7, [30_011], False), (40, 31, 1, [5_003], False), (1, 21, 7, None, True)]:
+        if bloom:
+            genome = _reads(rng, 3, k, alphabet="ACGTacgtN", min_len=2000, max_len=3000)
+            nbytes, K = oracle_mod.BloomFilter.params(9000, 0.01)
+            ob = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+            ob.build(genome)
+            gb = xs.Bank.create_bloom(k, nbytes, K)
+            gb.upload(ob.bits)
+            reads = [g[i:i + 150] for g in genome for i in range(0, 1800, 97)]
+        else:
+            ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D + shift)
+            reads = [s[i:i + int(rng.integers(k - 1, 300))] for s in seqs[:60] for i in (0, 37)]
+        reads += _reads(rng, 50, k, alphabet="ACGTacgtNRY", min_len=k - 2, max_len=200)
+        lead = 5  # offsets start at 5 inside the handed-over buffer
+        body = b"".join(reads)
+        raw = np.frombuffer(b"\x00" * shift + b"X" * lead + body, dtype=np.uint8)
+        offs = np.zeros(len(reads) + 1, dtype=np.uint64)
+        np.cumsum([len(r) for r in reads], out=offs[1:])
+        offs += lead
+        dev = torch.device("cuda", 0)
+        d_all = torch.from_numpy(raw.copy()).to(dev)
+        d_seqs = d_all[shift:]  # unaligned base, ends at the last read byte
+        assert d_seqs.data_ptr() % 4 == shift % 4 and d_seqs.numel() == lead + len(body)
+        d_offs = torch.from_numpy(offs.astype(np.int64)).to(dev)
+        cols = 1 if bloom else D
+        d_hits = torch.empty((len(reads), cols), dtype=torch.int32, device=dev)
+        d_nk = torch.empty(len(reads), dtype=torch.int64, device=dev)
+        gb.query_device(d_seqs, d_seqs.numel(), d_offs, len(reads), 1, d_hits, d_nk, None,
+                        stream=torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        want_h, want_n = ob.query(reads)
+        assert np.array_equal(d_nk.cpu().numpy().view(np.uint64), want_n)
+        assert np.array_equal(d_hits.cpu().numpy().view(np.uint32).reshape(-1), want_h.reshape(-1))
+        gb.close()
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4])
+def test_tiny_k(xs, oracle_mod, k):
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 9, k, 3, [257], seed=k)
+    rng = np.random.default_rng(k)
+    reads = _reads(rng, 200, k, alphabet="ACGTacgtN", min_len=0, max_len=40)
+    for step in (1, 2, 5):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n) and np.array_equal(got_h, want_h)
+    gb.close()
+
+
 def test_mlst_sum_matches_numpy(xs):
     rng = np.random.default_rng(0)
     gb = xs.Bank.create_cobs(21, 1, [101], 50)
