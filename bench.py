@@ -87,6 +87,8 @@ def parse():
     ap.add_argument("--docs", type=int, default=100)
     ap.add_argument("--genome-len", type=int, default=4_000_000)
     ap.add_argument("--step", type=int, default=1, help="sparse sampling step")
+    ap.add_argument("--k", type=int, default=None, help="species/multigenus: k-mer length (default 21)")
+    ap.add_argument("--hashes", type=int, default=7, help="species/multigenus: COBS num_hashes (default 7)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_traffic.json"))
@@ -110,7 +112,7 @@ class Workload:
         s = stream.cuda_stream
         self.stream = s
         w = args.workload
-        self.k = 31 if w == "mlst" else 21
+        self.k = 31 if w == "mlst" else (args.k or 21)
         self.banks = []
         self.config = {}
         self.row_bytes = ROW_BYTES
@@ -129,15 +131,17 @@ class Workload:
                 self.rows_per_kmer = nh
                 self.kernel = f"probe_bloom_kernel<21,{nh}>"
             else:
-                sig = cobs_signature_size(args.genome_len - self.k + 1, 7, 0.01)
-                bank = Bank.create_cobs(self.k, 7, [sig], args.docs,
+                h = args.hashes
+                sig = cobs_signature_size(args.genome_len - self.k + 1, h, 0.01)
+                bank = Bank.create_cobs(self.k, h, [sig], args.docs,
                                         [f"species_{gseed}_{i:03d}" for i in range(args.docs)],
                                         device=dev.index)
                 g_docs = torch.arange(args.docs, dtype=torch.int32, device=dev)
                 bank.build_device(g_dev, genomes.size, g_offs, args.docs, g_docs, stream=s)
-                self.config.update(signature_rows=sig, num_hashes=7, fpr=0.01)
-                self.rows_per_kmer = 7
-                self.kernel = "probe_cobs_fast<21,7>"
+                self.config.update(signature_rows=sig, num_hashes=h, fpr=0.01)
+                self.rows_per_kmer = h
+                self.kernel = ("probe_cobs_fast<21,7>" if (self.k, h) == (21, 7) and args.docs <= 128
+                               else f"probe_cobs (k={self.k}, h={h}, D={args.docs})")
             torch.cuda.synchronize(dev)
             del g_dev
             self.banks = [bank]

@@ -1,0 +1,9 @@
+# species workload at other (k, h) and D: the general / slot kernel paths
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+for kh in "21 7 100" "25 5 100" "21 3 100" "31 7 100" "21 7 300" "21 7 1000"; do
+  set -- $kh
+  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 5 --warmup 2 --k $1 --hashes $2 --docs $3 --genome-len 1000000 > gpurun_out/kh_$1_$2_$3.json 2> gpurun_out/kh.err || { tail -20 gpurun_out/kh.err; exit 8; }
+  python3 -c "import json;d=json.load(open('gpurun_out/kh_$1_$2_$3.json'));r=d['roofline'];print('k=$1 h=$2 D=$3: probe %.2f ms  %.0f GB/s frac %.3f  %.3e probes/s' % (r['probe_ms_avg'], r['achieved'], r['frac'], d['value']))"
+done

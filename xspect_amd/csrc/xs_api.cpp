@@ -15,8 +15,9 @@
 //                 page_size bytes (group g = docs [8*page_size*g, 8*page_size*(g+1))).
 //   rbloom        u64 little-endian K, then the filter bytes (bit i = byte i>>3,
 //                 bit i&7).
-// On the device every row is padded to a 16-byte pitch so that one row of a
-// group is one aligned dwordx4 per 128 docs and never straddles a 64-byte line.
+// On the device every row is padded to a 16, 32 or 64-byte pitch, or to a
+// multiple of 128 bytes: one row of a group is whole aligned dwordx4 chunks
+// (128 docs each) and never straddles a 128-byte line.
 #include "../../include/xspect_hip.h"
 
 #include <hip/hip_runtime.h>
@@ -158,7 +159,7 @@ struct xs_bank {
         v.groups = groups.as<GroupDesc>();
         v.G = (uint32_t)G;
         v.pitch = (uint32_t)pitch;
-        v.nchunks = (uint32_t)(pitch / 16);
+        v.nchunks = (uint32_t)((page + 15) / 16);  // chunks that hold doc bits
         v.h = h;
         v.page = page;
         v.D = D;
@@ -196,7 +197,11 @@ int validate_geometry(xs_bank* b) {
                     (unsigned long long)b->D);
     for (auto s : b->sig)
         if (s == 0) return fail(XS_ERR_FORMAT, "zero signature size");
-    b->pitch = (b->page + 15) / 16 * 16;
+    // Device row pitch: 16, 32, 64 or a multiple of 128 bytes, so that no row
+    // straddles a 128-byte line (a 48-byte pitch made 2 rows in 8 cost two
+    // line fills).  The kernels load only the (page + 15) / 16 data chunks.
+    const uint64_t p16 = (b->page + 15) / 16 * 16;
+    b->pitch = p16 <= 64 ? (p16 <= 16 ? 16 : p16 <= 32 ? 32 : 64) : (p16 + 127) / 128 * 128;
     int wpb;
     size_t lds;
     if (probe_blocks(b->D, &wpb, &lds) != 0)

@@ -765,17 +765,21 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
                         for (int j = 0; j < NH; ++j)
                             if ((uint32_t)j < h) ro[j] = gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch;
                     }
+                    // row-major issue order: the chunks of one row leave back to back,
+                    // so the vector L1 sees one row line in consecutive requests
+                    const bool on = (uint32_t)g < G && act;
 #pragma unroll
-                    for (int cc = 0; cc < CM; ++cc) {
-                        uint4 m = make_uint4(0u, 0u, 0u, 0u);
-                        if ((uint32_t)g < G && (uint32_t)cc < cpg && act) {
-                            m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    for (int cc = 0; cc < CM; ++cc)
+                        mk[g * CM + cc] = (on && (uint32_t)cc < cpg) ? make_uint4(~0u, ~0u, ~0u, ~0u)
+                                                                     : make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
-                            for (int j = 0; j < NH; ++j)
-                                if ((uint32_t)j < h)
-                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
-                        }
-                        mk[g * CM + cc] = m;
+                    for (int j = 0; j < NH; ++j) {
+                        if ((uint32_t)j >= h) continue;
+#pragma unroll
+                        for (int cc = 0; cc < CM; ++cc)
+                            if (on && (uint32_t)cc < cpg)
+                                mk[g * CM + cc] = and4(mk[g * CM + cc],
+                                                       *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
                     }
                 }
 #pragma unroll
