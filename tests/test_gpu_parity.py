@@ -63,6 +63,9 @@ CLASSIC_CASES = [
     (1000, 21, 7, [3_001]),
     (13, 32, 4, [2_048]),
     (40, 17, 9, [1_231]),
+    (200, 21, 7, [12_007]),   # wide kernel, 2 chunk lanes
+    (500, 31, 1, [9_001]),    # wide kernel, 4 chunk lanes
+    (700, 25, 5, [4_001]),    # wide kernel, 8 chunk lanes, general (k, h)
     (2048, 31, 1, [9_001]),   # 16 chunks: widest slot kernel
     (2100, 21, 7, [4_001]),   # 17 chunks: general kernel
 ]

@@ -388,7 +388,8 @@ __device__ __forceinline__ void xpose_init(int lane, Xpose& X) {
 
 __device__ __forceinline__ uint32_t bsel(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 
-__device__ __forceinline__ uint32_t column_popc32(uint32_t x, const Xpose& X) {
+// The 32x32 transpose itself: bit r of lane c's result is row r's bit c.
+__device__ __forceinline__ uint32_t xpose32(uint32_t x, const Xpose& X) {
     uint32_t y;
     y = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);                 // lane ^ 16
     x = bsel(X.msk[0], x, __builtin_amdgcn_alignbit(y, y, 16));
@@ -400,7 +401,11 @@ __device__ __forceinline__ uint32_t column_popc32(uint32_t x, const Xpose& X) {
     x = bsel(X.msk[3], x, __builtin_amdgcn_alignbit(y, y, X.rot[2]));
     y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1032 = lane ^ 1
     x = bsel(X.msk[4], x, __builtin_amdgcn_alignbit(y, y, X.rot[3]));
-    return (uint32_t)__popc(x);
+    return x;
+}
+
+__device__ __forceinline__ uint32_t column_popc32(uint32_t x, const Xpose& X) {
+    return (uint32_t)__popc(xpose32(x, X));
 }
 
 // Sum of lane l and lane l ^ 32 (the two halves' counts of the same doc).
@@ -679,6 +684,148 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
             for (int w = 0; w < wpb; ++w) s += smem[(size_t)w * 2 * dpad + dpad + d];
             out[d] = s;
         }
+        if (threadIdx.x == 0) {
+            uint64_t s = 0;
+            for (int w = 0; w < wpb; ++w) s += s_kmers[w];
+            out[D] = s;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ COBS probe (wide classic rows)
+// Classic banks of 129..1024 docs: a row is C 16-byte chunks (C = 2, 4 or 8,
+// the next power of two of its data chunks; the pitch is padded so a row is
+// one 128-byte line at most).  Hashing stays one lane per k-mer, but the
+// gathers run C lanes per k-mer: in sub-tile s, lane l loads chunk l % C of
+// k-mer s * (64 / C) + l / C.  One load instruction then reads 64 / C whole
+// rows, so the vector L1 sees each row line once instead of once per chunk.
+// Counting: after the 32x32 transpose of a 32-lane half, bit r of lane t is
+// lane r's bit t, and lanes r = c (mod C) hold chunk c: one masked popcount
+// per chunk.
+template <int C>
+struct ChunkLanes {  // bits r of a 32-row column with r % C == 0
+    static constexpr uint32_t m0 = C == 2 ? 0x55555555u : C == 4 ? 0x11111111u : 0x01010101u;
+};
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int KT, int HT, int C>
+__global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv, CobsView bv,
+                                                                    uint32_t* __restrict__ hits,
+                                                                    uint64_t* __restrict__ partials,
+                                                                    uint32_t dpad) {
+    constexpr int K = 64 / C;  // k-mers per sub-tile
+    constexpr uint32_t M0 = ChunkLanes<C>::m0;
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_tot[];  // [dpad] per block
+    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    for (uint32_t d = threadIdx.x; d < dpad; d += blockDim.x) s_tot[d] = 0;
+    __syncthreads();
+    Xpose X;
+    xpose_init(lane, X);
+
+    constexpr int NH = HT ? HT : (int)kMaxHashes;
+    const uint32_t k = KT ? KT : rv.k;
+    const uint32_t h = HT ? HT : bv.h;
+    const uint32_t step = rv.step;
+    const uint64_t D = bv.D;
+    const uint32_t cpg = bv.nchunks;  // data chunks, <= C (host-checked)
+    const GroupDesc gd = bv.groups[0];
+    const int my_c = lane % C, my_slot = lane / C;
+    const bool my_chunk_on = (uint32_t)my_c < cpg;
+    const uint64_t U = rv.queue[0];
+    uint64_t kmer_total = 0;
+
+    for (;;) {
+        const uint64_t base = grab_units(rv.queue, lane);
+        if (base >= U) break;
+        const uint64_t uend = min(base + kGrab, U);
+        for (uint64_t u = base; u < uend; ++u) {
+            const uint32_t r = rv.unit_read[u];
+            const uint64_t seg = u - rv.unit_ofs[r];
+            const uint64_t o0 = rv.offs[r];
+            const uint64_t len = rv.offs[r + 1] - o0;
+            const uint64_t nk = num_kmers(len, k, step);
+            const uint64_t t0 = seg * kSegKmers;
+            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+            kmer_total += cnt;
+            uint32_t acc[2 * C];  // chunk cc, words q: 16-bit counters, reg 2*cc + (q >> 1)
+#pragma unroll
+            for (int i = 0; i < 2 * C; ++i) acc[i] = 0;
+
+            for (uint32_t tb = 0; tb < cnt; tb += 64) {
+                const bool act = tb + lane < cnt;
+                uint64_t ro[NH];
+#pragma unroll
+                for (int j = 0; j < NH; ++j) ro[j] = 0;
+                if (act) {
+                    Kmer c;
+                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    Xxh64Pre pre;
+                    xxh64_pre<KT>(c, k, pre);
+#pragma unroll
+                    for (int j = 0; j < NH; ++j)
+                        if ((uint32_t)j < h)
+                            ro[j] = gd.base + fastmod(xxh64_seed<KT>(c, pre, k, (uint64_t)j), gd.sig, gd.magic) * bv.pitch;
+                }
+                const uint32_t tile = min(64u, cnt - tb);
+#pragma unroll
+                for (int s = 0; s < C; ++s) {
+                    if ((uint32_t)(s * K) >= tile) continue;  // uniform
+                    const int src = s * K + my_slot;
+                    const bool on = (uint32_t)src < tile && my_chunk_on;
+                    uint64_t o[NH];
+#pragma unroll
+                    for (int j = 0; j < NH; ++j) o[j] = (uint32_t)j < h ? shfl64(ro[j], src) : 0;
+                    uint4 m = on ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                    for (int j = 0; j < NH; ++j)
+                        if ((uint32_t)j < h && on)
+                            m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + o[j] + my_c * 16));
+                    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (__ballot(w[q] != 0u) == 0ull) continue;
+                        const uint32_t x = xpose32(w[q], X);
+#pragma unroll
+                        for (int cc = 0; cc < C; ++cc)
+                            acc[2 * cc + (q >> 1)] += (uint32_t)__popc(x & (M0 << cc)) << (16 * (q & 1));
+                    }
+                }
+            }
+            // lane t < 32 holds doc 128 cc + 32 q + t after folding the halves
+            const bool whole = nk <= kSegKmers;
+#pragma unroll
+            for (int cc = 0; cc < C; ++cc) {
+                if ((uint32_t)cc >= cpg) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t d0 = (uint64_t)cc * 128 + q * 32;
+                    if (d0 >= D) continue;
+                    const uint32_t v = fold_halves((acc[2 * cc + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
+                    const uint64_t d = d0 + (uint64_t)lane;
+                    if (lane < 32 && d < D) {
+                        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[d]), (unsigned long long)v);
+                        if (hits) {
+                            if (whole) hits[(uint64_t)r * D + d] = v;
+                            else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
+                        }
+                    }
+                }
+            }
+        }
+    }
+    if (lane == 0) s_kmers[wid] = kmer_total;
+    __syncthreads();
+    if (partials) {
+        const int wpb = blockDim.x >> 6;
+        uint64_t* out = partials + (uint64_t)blockIdx.x * (D + 1);
+        for (uint64_t d = threadIdx.x; d < D; d += blockDim.x) out[d] = s_tot[d];
         if (threadIdx.x == 0) {
             uint64_t s = 0;
             for (int w = 0; w < wpb; ++w) s += s_kmers[w];
@@ -1204,6 +1351,21 @@ static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t
     return hipGetLastError();
 }
 
+// Wide kernel chunk lanes for a classic bank of 2..8 data chunks (0: none).
+static int wide_for(const CobsView& bv) {
+    if (bv.G != 1 || bv.nchunks < 2 || bv.nchunks > 8) return 0;
+    return bv.nchunks == 2 ? 2 : bv.nchunks <= 4 ? 4 : 8;
+}
+
+using WideFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*, uint32_t);
+
+template <int KT, int HT>
+static WideFn wide_fn(int c) {
+    return c == 2 ? probe_cobs_wide<KT, HT, 2> : c == 4 ? probe_cobs_wide<KT, HT, 4> : probe_cobs_wide<KT, HT, 8>;
+}
+
+static WideFn pick_wide(uint32_t k, uint32_t h, int c);
+
 // Slot kernel shape (GM groups x CM chunks) for a bank, or {0, 0} when its
 // rows span more than 16 chunks (general kernel).  D <= 16 * 128 follows, so
 // the LDS totals need <= 16 KB.
@@ -1257,6 +1419,14 @@ static SlotsFn pick_slots(uint32_t k, uint32_t h, SlotShape s) {
     }
 }
 
+static WideFn pick_wide(uint32_t k, uint32_t h, int c) {
+    switch (kh_variant(k, h)) {
+        case 0: return wide_fn<21, 7>(c);
+        case 1: return wide_fn<31, 1>(c);
+        default: return wide_fn<0, 0>(c);
+    }
+}
+
 static int shape_index(SlotShape s) {  // 0..12, for the grid cache
     static const int gms[13] = {1, 1, 1, 1, 4, 8, 16, 4, 8, 2, 3, 4, 0};
     static const int cms[13] = {4, 8, 12, 16, 1, 1, 1, 2, 2, 4, 4, 4, 0};
@@ -1270,11 +1440,15 @@ static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
-    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][13] = {};
+    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][13] = {}, wide[3][3] = {};
     if (cobs_fast(bv, k)) {
         if (k == 21)
             return fast21 ? fast21 : (fast21 = resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0));
         return fast31 ? fast31 : (fast31 = resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0));
+    }
+    if (const int c = wide_for(bv)) {
+        int& g = wide[kh_variant(k, bv.h)][c == 2 ? 0 : c == 4 ? 1 : 2];
+        return g ? g : (g = resident_grid(pick_wide(k, bv.h, c), kProbeThreads, 8192));
     }
     const SlotShape sh = slots_for(bv);
     if (sh.gm) {
@@ -1302,6 +1476,12 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
         fb.image_bytes = (uint32_t)min(bv.sig0 * 16ull, 0xFFFFFFFFull);
         if (rv.k == 21) return launch_fast_t<21, 7>(rv, fb, hits, partials, blocks, s);
         return launch_fast_t<31, 1>(rv, fb, hits, partials, blocks, s);
+    }
+    if (const int c = wide_for(bv)) {
+        const size_t lds = slots_lds(bv);
+        pick_wide(rv.k, bv.h, c)<<<blocks, kProbeThreads, lds, s>>>(rv, bv, hits, partials,
+                                                                  (uint32_t)(lds / sizeof(uint64_t)));
+        return hipGetLastError();
     }
     const SlotShape sh = slots_for(bv);
     if (sh.gm) {
