@@ -7,7 +7,7 @@ Default workload = BASELINE.json configs[1] / SURVEY.md §8(d) config 2: 1M
 synthetic 150 bp reads per GPU against a D=100 species COBS classic bank
 (k=21, h=7, fpr=0.01; 38.4M rows, 0.5 GB file / 0.61 GB in HBM, larger than
 the 256 MiB Infinity Cache).  One step = one query of the whole read batch,
-resident in HBM (strands -> units -> scan -> probe -> totals).  With N>1
+resident in HBM (units -> scan -> scatter -> probe -> totals).  With N>1
 ranks the D+1 per-doc totals (the input of the SVM vector) are all-reduced
 over RCCL: reads sharded (seed 42+rank), bank replicated, weak scaling.
 
@@ -22,10 +22,13 @@ metric = k-mer x filter probes/s = sum(ceil((L-k+1)/step)) x docs / second,
 whole job.  roofline prices the probe kernel alone (HIP events on its launch
 stream around every launch of the timed region) at its algorithmic bytes:
 one 128-byte L2 line fill per random row (COBS: h rows per k-mer and doc
-group; rbloom: K dwords per k-mer) + the streamed strand windows, hit matrix
-and per-read metadata; peak = 8.0 TB/s.  cpu_baseline: the C oracle
-(oracle/liboracle.so, OpenMP) on a bounded sample of the same reads and bank
-(rank 0, N=1 only); its hits are also compared with the GPU's.
+group; rbloom: K dwords per k-mer; MLST: the 64-byte rows themselves, its
+banks being Infinity-Cache resident) + the read bytes, hit matrix and
+per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per launch from
+profiles/r01_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
+OpenMP) on a bounded sample of the same reads and bank (rank 0, N=1 only);
+its hits are also compared with the GPU's; plus the reference's per-read loop
+shape on one core.  host_path: the same step from host buffers (PCIe).
 """
 from __future__ import annotations
 

@@ -59,7 +59,7 @@ int fail(int code, const char* fmt, ...) {
 
 const char kClassicMagic[] = "CLASSIC_INDEX";
 const char kCompactMagic[] = "COMPACT_INDEX";
-constexpr uint64_t kPad = 64;  // device over-read guard for strand windows
+constexpr uint64_t kPad = 64;  // spare bytes after staged host reads
 
 struct DevBuf {
     void* p = nullptr;
@@ -411,7 +411,7 @@ struct Inputs {
     uint64_t n;
 };
 
-// Strands + unit decomposition for n device-resident reads.
+// Unit decomposition (k-mer counts, units, unit -> read map) for n device-resident reads.
 int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, uint32_t* hits_zero,
                   uint64_t zero_cols, hipStream_t s, ReadView* rv) {
     if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;

@@ -21,7 +21,8 @@ constexpr uint32_t kMaxChunks = 8;
 // LDS budget per probe block for per-wave doc counters.
 constexpr uint32_t kLdsBudget = 64 * 1024;
 
-enum StrandMode : int { kStrandCobs = 0, kStrandBio = 1 };
+// How a k-mer's bytes are canonicalised: COBS (species, MLST) or rbloom/Biopython (genus).
+enum KmerMode : int { kKmerCobs = 0, kKmerBio = 1 };
 
 // One COBS doc group on the device.
 struct GroupDesc {

@@ -425,7 +425,7 @@ __device__ __forceinline__ void kmer_at(const ReadView& rv, uint64_t o0, uint64_
     const int kk = KT ? KT : (int)k;
     uint32_t f[8], r[8];
     load_window<KT>(rv.seq, rv.seq_bytes, o0 + p, k, f);
-    if constexpr (MODE == kStrandCobs) {
+    if constexpr (MODE == kKmerCobs) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) f[i] = cobs_norm4(f[i]) & tail_mask(i, kk);
         rc_perm<KT>(f, k, r);
@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
                 uint4 m = make_uint4(0u, 0u, 0u, 0u);
                 if (tb + lane < cnt) {
                     Kmer c;
-                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
                     uint32_t off[HT];
@@ -614,7 +614,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
                 uint64_t hv[HT ? HT : kMaxHashes];
                 if (act) {
                     Kmer c;
-                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
 #pragma unroll
@@ -765,7 +765,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
                 for (int j = 0; j < NH; ++j) ro[j] = 0;
                 if (act) {
                     Kmer c;
-                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
 #pragma unroll
@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
                 for (int j = 0; j < NH; ++j) hv[j] = 0;
                 if (act) {
                     Kmer c;
-                    kmer_at<KT, kStrandCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     Xxh64Pre pre;
                     xxh64_pre<KT>(c, k, pre);
 #pragma unroll
@@ -1043,7 +1043,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
                 bool in = false;
                 if (tb + lane < cnt) {
                     Kmer c;
-                    kmer_at<KT, kStrandBio>(rv, o0, len, (t0 + tb + lane) * step, k, c);
+                    kmer_at<KT, kKmerBio>(rv, o0, len, (t0 + tb + lane) * step, k, c);
                     in = bloom_member<KT, KB>(c, k, bv);
                 }
                 c_unit += (uint32_t)__popcll(__ballot(in));
@@ -1098,7 +1098,7 @@ __global__ void __launch_bounds__(kProbeThreads) build_cobs_kernel(ReadView rv,
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
                 if (tb + lane >= cnt) continue;
                 Kmer c;
-                kmer_at<KT, kStrandCobs>(rv, o0, len, t0 + tb + lane, k, c);
+                kmer_at<KT, kKmerCobs>(rv, o0, len, t0 + tb + lane, k, c);
                 Xxh64Pre pre;
                 xxh64_pre<KT>(c, k, pre);
                 for (uint32_t j = 0; j < h; ++j) {
@@ -1132,7 +1132,7 @@ __global__ void __launch_bounds__(kProbeThreads) build_bloom_kernel(ReadView rv,
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
                 if (tb + lane >= cnt) continue;
                 Kmer c;
-                kmer_at<KT, kStrandBio>(rv, o0, len, t0 + tb + lane, k, c);
+                kmer_at<KT, kKmerBio>(rv, o0, len, t0 + tb + lane, k, c);
                 uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
                 for (uint32_t j = 0; j < bv.K; ++j) {
                     const uint64_t pm = sl * kLcgMl;
