@@ -90,6 +90,8 @@ def parse():
     ap.add_argument("--docs", type=int, default=100)
     ap.add_argument("--genome-len", type=int, default=4_000_000)
     ap.add_argument("--step", type=int, default=1, help="sparse sampling step")
+    ap.add_argument("--genus-filter-frac", type=float, default=1.0,
+                    help="genus: build the filter from this fraction of the genomes (reads come from all)")
     ap.add_argument("--k", type=int, default=None, help="species/multigenus: k-mer length (default 21)")
     ap.add_argument("--hashes", type=int, default=7, help="species/multigenus: COBS num_hashes (default 7)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
@@ -126,13 +128,15 @@ class Workload:
             g_dev = torch.from_numpy(genomes.reshape(-1)).to(dev)
             g_offs = torch.arange(args.docs + 1, dtype=torch.int64, device=dev) * args.genome_len
             if w == "genus":
-                n_items = genomes.size - self.k + 1  # Bloom(total_length - k + 1, fpr), :82-88
+                nf = max(1, int(round(args.docs * args.genus_filter_frac)))
+                n_items = genomes[:nf].size - self.k + 1  # Bloom(total_length - k + 1, fpr), :82-88
                 nbytes, nh = bloom_parameters(n_items, 0.01)
                 bank = Bank.create_bloom(self.k, nbytes, nh, device=dev.index)
-                bank.build_device(g_dev, genomes.size, g_offs, args.docs, None, stream=s)
+                bank.build_device(g_dev, genomes[:nf].size, g_offs[:nf + 1], nf, None, stream=s)
+                self.config.update(genomes_in_filter=nf)
                 self.config.update(bloom_bytes=nbytes, bloom_hashes=nh)
                 self.rows_per_kmer = nh
-                self.kernel = f"probe_bloom_kernel<21,{nh}>"
+                self.kernel = f"probe_bloom_kernel<21,{nh},2> (2 bits first, the rest if both set)"
             else:
                 h = args.hashes
                 sig = cobs_signature_size(args.genome_len - self.k + 1, h, 0.01)
@@ -278,6 +282,7 @@ def main():
     for b in wl.banks:
         b.set_profiling(True)
         b.probe_stats()  # reset
+        b.probe_rows()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -289,7 +294,9 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launches, probe_ms_total, probe_ms_max = 0, 0.0, 0.0
+    rows_read = 0
     for b in wl.banks:
+        rows_read += b.probe_rows()
         b.set_profiling(False)
         n_l, tot_ms, mx = b.probe_stats()
         launches += n_l
@@ -308,6 +315,8 @@ def main():
         assert int(tot[-1]) == want, f"k-mer total {int(tot[-1])} != {want}"
 
     value = wl.probes_per_step() * args.steps / elapsed
+    if rows_read:  # rbloom: the data-dependent count of filter words loaded
+        wl.rows_per_kmer = rows_read / max(1, launches) / wl.kmers
     algo_bytes = wl.algo_bytes_per_launch()
     achieved = algo_bytes / (probe_ms * 1e-3) / 1e9
     traffic = None
@@ -360,7 +369,7 @@ def main():
             "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": wl.kernel,
             "probe_ms_avg": probe_ms, "probe_ms_max": probe_ms_max, "probe_launches": launches,
-            "algo_bytes_per_launch": algo_bytes, "row_bytes": wl.row_bytes,
+            "algo_bytes_per_launch": algo_bytes, "row_bytes": wl.row_bytes, "rows_per_kmer": wl.rows_per_kmer,
             **({"note": wl.roofline_note} if wl.roofline_note else {}),
         },
         "cpu_baseline": cpu,

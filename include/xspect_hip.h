@@ -174,6 +174,13 @@ int xs_bank_last_probe_ms(xs_bank* bank, float* ms);
  * profiling was enabled or the last call of this function (then resets). */
 int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float* max_ms);
 
+/* rbloom banks: filter words the probe kernels loaded since profiling was
+ * enabled or the last call (then resets).  The probe tests 2 bits first and
+ * loads the other K-2 only for k-mers that pass them, as rbloom stops at the
+ * first zero bit, so the count depends on the data.  0 for COBS banks, whose
+ * kernels read exactly h rows per k-mer and doc group. */
+int xs_bank_probe_rows(xs_bank* bank, uint64_t* rows);
+
 void xs_bank_close(xs_bank* bank);
 
 /* ---- Result output (src/xspect/models/result.py:151-202, json.dumps(indent=4)).

@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 P=gpurun_out/pmct
 mkdir -p $P
-for w in species genus mlst; do
+for w in ${WORKLOADS:-species genus mlst}; do
   B="bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline"
   timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $P/$w/f -o run -- python $B > $P/$w.f.json 2> $P/$w.f.err || { tail -20 $P/$w.f.err; exit 30; }
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $P/$w/w -o run -- python $B > $P/$w.w.json 2> $P/$w.w.err || { tail -20 $P/$w.w.err; exit 31; }

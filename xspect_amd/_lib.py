@@ -106,6 +106,7 @@ SIGNATURES = {
     "xs_bank_last_probe_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_float)]),
+    "xs_bank_probe_rows": (_int, [_vp, ctypes.POINTER(_u64)]),
     "xs_bank_close": (None, [_vp]),
     "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _vp, ctypes.c_char_p, _vp,
                                         ctypes.c_char_p, _vp, _vp, _int]),

@@ -235,6 +235,12 @@ class Bank:
         check(load().xs_bank_probe_stats(self.handle, ctypes.byref(n), ctypes.byref(tot), ctypes.byref(mx)))
         return int(n.value), float(tot.value), float(mx.value)
 
+    def probe_rows(self) -> int:
+        """rbloom: filter words loaded by the probes since the last call (profiling on)."""
+        n = ctypes.c_uint64(0)
+        check(load().xs_bank_probe_rows(self.handle, ctypes.byref(n)))
+        return int(n.value)
+
     # ------------------------------------------------------------ lifetime
     def close(self) -> None:
         if self._h is not None:

@@ -139,6 +139,7 @@ struct xs_bank {
     // workspace
     DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
         best;
+    DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
     PinnedBuf stage[2];             // D2H staging ring for large host outputs
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     bool profiling = false;
@@ -172,6 +173,7 @@ struct xs_bank {
         v.mbits = nbytes * 8;
         v.magic = barrett_magic(v.mbits);
         v.K = h;
+        v.rows_read = profiling ? rows_read.as<uint64_t>() : nullptr;
         return v;
     }
 };
@@ -936,7 +938,25 @@ int xs_mlst_sum(xs_bank* b, const uint32_t* hits, const uint32_t* seq_of_chunk, 
 int xs_bank_set_profiling(xs_bank* b, int on) {
     if (!b) return fail(XS_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(b->mu);
+    if (on && !b->profiling) {
+        HIPCHK(hipSetDevice(b->device));
+        if (int rc = b->rows_read.ensure(sizeof(uint64_t))) return rc;
+        HIPCHK(hipMemsetAsync(b->rows_read.p, 0, sizeof(uint64_t), b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+    }
     b->profiling = on != 0;
+    return XS_OK;
+}
+
+int xs_bank_probe_rows(xs_bank* b, uint64_t* rows) {
+    if (!b || !rows) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    *rows = 0;
+    if (b->kind != XS_BANK_RBLOOM || !b->rows_read.p) return XS_OK;
+    HIPCHK(hipSetDevice(b->device));
+    HIPCHK(hipDeviceSynchronize());  // probes may have run on a caller's stream
+    HIPCHK(hipMemcpy(rows, b->rows_read.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(b->rows_read.p, 0, sizeof(uint64_t)));
     return XS_OK;
 }
 

@@ -48,6 +48,7 @@ struct BloomView {
     uint64_t mbits;        // number of bits (nbytes*8)
     uint64_t magic;        // floor((2^64-1)/mbits)
     uint32_t K;
+    uint64_t* rows_read;   // when profiling: += filter words the probe loaded
 };
 
 // Reads / records laid out for one probe or build call.

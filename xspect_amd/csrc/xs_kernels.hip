@@ -987,10 +987,14 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
 }
 
 // ------------------------------------------------------------------ rbloom probe
+// Filter bits tested before the rest: 2 measured fastest for member-heavy
+// and foreign-heavy reads alike (tools/gpu_bloom_ab.sh).
+constexpr int kBloomSplitDefault = 2;
 // All K bit indices first, then all K dword loads in flight at once (the
 // reference stops at the first zero bit; the answer is the same).
-template <int KT, int KB>
-__device__ __forceinline__ bool bloom_member(const Kmer& c, uint32_t k, const BloomView& bv) {
+// Returns bit 0: member; bit 1: the second load phase ran.
+template <int KT, int KB, int SPLIT>
+__device__ __forceinline__ uint32_t bloom_member(const Kmer& c, uint32_t k, const BloomView& bv) {
     constexpr int NK = KB ? KB : (int)kMaxHashes;
     const uint32_t K = KB ? KB : bv.K;
     uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
@@ -1006,14 +1010,24 @@ __device__ __forceinline__ bool bloom_member(const Kmer& c, uint32_t k, const Bl
             idx[j] = fastmod(sh, bv.mbits, bv.magic);
         }
     }
+    // The first SPLIT bits decide most non-members (rbloom stops at the
+    // first zero bit); the other loads go out only for lanes still in.
+    // SPLIT = 0: all K loads at once.
     uint32_t all = 1;
 #pragma unroll
     for (int j = 0; j < NK; ++j)
-        if ((uint32_t)j < K) all &= bv.bits[idx[j] >> 5] >> (idx[j] & 31);
-    return all & 1u;
+        if ((uint32_t)j < K && (SPLIT == 0 || j < SPLIT)) all &= bv.bits[idx[j] >> 5] >> (idx[j] & 31);
+    uint32_t phase2 = 0;
+    if (SPLIT != 0 && (all & 1u) && (uint32_t)SPLIT < K) {
+        phase2 = 2u;
+#pragma unroll
+        for (int j = SPLIT; j < NK; ++j)
+            if ((uint32_t)j < K) all &= bv.bits[idx[j] >> 5] >> (idx[j] & 31);
+    }
+    return (all & 1u) | phase2;
 }
 
-template <int KT, int KB>
+template <int KT, int KB, int SPLIT>
 __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv, BloomView bv,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials) {
@@ -1024,7 +1038,7 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
     const uint32_t k = KT ? KT : rv.k;
     const uint32_t step = rv.step;
     const uint64_t U = rv.queue[0];
-    uint64_t hit_total = 0, kmer_total = 0;
+    uint64_t hit_total = 0, kmer_total = 0, rows_total = 0;
 
     for (;;) {
         const uint64_t base = grab_units(rv.queue, lane);
@@ -1040,13 +1054,21 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
             const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
             uint32_t c_unit = 0;
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
-                bool in = false;
+                bool in = false, again = false;
                 if (tb + lane < cnt) {
                     Kmer c;
                     kmer_at<KT, kKmerBio>(rv, o0, len, (t0 + tb + lane) * step, k, c);
-                    in = bloom_member<KT, KB>(c, k, bv);
+                    const uint32_t res = bloom_member<KT, KB, SPLIT>(c, k, bv);
+                    in = res & 1u;
+                    again = (res & 2u) != 0;
                 }
                 c_unit += (uint32_t)__popcll(__ballot(in));
+                if (bv.rows_read) {
+                    const uint32_t K = KB ? KB : bv.K;
+                    const uint32_t first = SPLIT == 0 || (uint32_t)SPLIT >= K ? K : (uint32_t)SPLIT;
+                    rows_total += (uint64_t)__popcll(__ballot(tb + lane < cnt)) * first +
+                                  (uint64_t)__popcll(__ballot(again)) * (K - first);
+                }
             }
             kmer_total += cnt;
             hit_total += c_unit;
@@ -1056,6 +1078,8 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
             }
         }
     }
+    if (bv.rows_read && lane == 0 && rows_total)
+        atomicAdd(reinterpret_cast<unsigned long long*>(bv.rows_read), (unsigned long long)rows_total);
     if (partials) {
         if (lane == 0) { s_hits[wid] = hit_total; s_kmers[wid] = kmer_total; }
         __syncthreads();
@@ -1499,16 +1523,40 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
     return launch_cobs_t<0, 0>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
 }
 
+// Bits tested before the rest (XSPECT_AMD_BLOOM_SPLIT; 0 = all at once).
+static int bloom_split() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("XSPECT_AMD_BLOOM_SPLIT");
+        v = e ? atoi(e) : kBloomSplitDefault;
+        if (v != 0 && v != 1 && v != 2 && v != 3) v = kBloomSplitDefault;
+    }
+    return v;
+}
+
 int probe_grid_bloom() {
     static int cache = 0;
-    if (!cache) cache = resident_grid(probe_bloom_kernel<21, 7>, kProbeThreads, 0);
+    if (!cache) cache = resident_grid(probe_bloom_kernel<21, 7, 0>, kProbeThreads, 0);
     return cache;
+}
+
+template <int SPLIT>
+static void launch_bloom_t(const ReadView& rv, const BloomView& bv, uint32_t* hits, uint64_t* partials,
+                           int blocks, hipStream_t s) {
+    if (rv.k == 21 && bv.K == 7)
+        probe_bloom_kernel<21, 7, SPLIT><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    else
+        probe_bloom_kernel<0, 0, SPLIT><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
 }
 
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
                               uint64_t* partials, int blocks, hipStream_t s) {
-    if (rv.k == 21 && bv.K == 7) probe_bloom_kernel<21, 7><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
-    else probe_bloom_kernel<0, 0><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    switch (bloom_split()) {
+        case 1: launch_bloom_t<1>(rv, bv, hits, partials, blocks, s); break;
+        case 2: launch_bloom_t<2>(rv, bv, hits, partials, blocks, s); break;
+        case 3: launch_bloom_t<3>(rv, bv, hits, partials, blocks, s); break;
+        default: launch_bloom_t<0>(rv, bv, hits, partials, blocks, s); break;
+    }
     return hipGetLastError();
 }
 
