@@ -308,3 +308,26 @@ def test_query_best_matches_hit_matrix(xs, oracle_mod):
     best, bh, nk, tot = b.query_best([], want_totals=True)
     assert best.size == 0 and tot.tolist() == [0, 0]
     b.close()
+
+
+def test_concurrent_handles_from_threads(xs, oracle_mod):
+    """The threading contract of include/xspect_hip.h: distinct handles run
+    concurrently (ctypes releases the GIL), calls on one handle are serialised
+    by its mutex; every result stays bit-exact."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    pairs = [_pair(xs, oracle_mod, D, 21, 7, [sig], seed=D) for D, sig in ((50, 9_001), (100, 12_007), (7, 3_001))]
+    rng = np.random.default_rng(12)
+    batches = [_reads(rng, 400, 21, max_len=250) for _ in range(6)]
+    want = {(i, j): pairs[i][0].query(b)[0] for i in range(len(pairs)) for j, b in enumerate(batches)}
+
+    def job(args):
+        i, j = args
+        return (i, j), pairs[i][1].query(batches[j])[0]
+
+    work = [(i, j) for i in range(len(pairs)) for j in range(len(batches))] * 2  # shared handles too
+    with ThreadPoolExecutor(6) as pool:
+        for key, got in pool.map(job, work):
+            assert np.array_equal(got, want[key]), key
+    for _, gb, _, _ in pairs:
+        gb.close()

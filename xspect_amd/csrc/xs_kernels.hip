@@ -16,6 +16,7 @@
 //   rbloom `kmer in bf`                    probabilistic_single_filter_model.py:122-124
 #include <hipcub/hipcub.hpp>
 
+#include <atomic>
 #include <cstdlib>
 
 #include "xs_internal.h"
@@ -1345,13 +1346,24 @@ static bool cobs_fast(const CobsView& bv, uint32_t k) {
 }
 
 static int load_policy() {
-    static int pol = -1;
-    if (pol < 0) {
+    static const int pol = [] {  // thread-safe one-time init
         const char* e = getenv("XSPECT_AMD_LOADPOL");
-        pol = e ? atoi(e) : 0;
-        if (pol < 0 || pol > 4) pol = 0;
-    }
+        const int v = e ? atoi(e) : 0;
+        return (v < 0 || v > 4) ? 0 : v;
+    }();
     return pol;
+}
+
+// One grid size per kernel variant, computed on first use.  Banks may be
+// queried from several host threads at once, hence the atomics.
+template <class F>
+static int cached_grid(std::atomic<int>& slot, F compute) {
+    int v = slot.load(std::memory_order_relaxed);
+    if (!v) {
+        v = compute();
+        slot.store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 template <int KT, int HT>
@@ -1464,28 +1476,26 @@ static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
-    static int fast21 = 0, fast31 = 0, generic[3] = {0, 0, 0}, slots[3][13] = {}, wide[3][3] = {};
+    static std::atomic<int> fast21{0}, fast31{0}, generic[3], slots[3][13], wide[3][3];
     if (cobs_fast(bv, k)) {
-        if (k == 21)
-            return fast21 ? fast21 : (fast21 = resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0));
-        return fast31 ? fast31 : (fast31 = resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0));
+        if (k == 21) return cached_grid(fast21, [] { return resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0); });
+        return cached_grid(fast31, [] { return resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0); });
     }
     if (const int c = wide_for(bv)) {
-        int& g = wide[kh_variant(k, bv.h)][c == 2 ? 0 : c == 4 ? 1 : 2];
-        return g ? g : (g = resident_grid(pick_wide(k, bv.h, c), kProbeThreads, 8192));
+        return cached_grid(wide[kh_variant(k, bv.h)][c == 2 ? 0 : c == 4 ? 1 : 2],
+                           [&] { return resident_grid(pick_wide(k, bv.h, c), kProbeThreads, 8192); });
     }
     const SlotShape sh = slots_for(bv);
     if (sh.gm) {
         // LDS is 16 KB at most: residency is set by registers, not by D
-        int& g = slots[kh_variant(k, bv.h)][shape_index(sh)];
-        return g ? g : (g = resident_grid(pick_slots(k, bv.h, sh), kProbeThreads, 16384));
+        return cached_grid(slots[kh_variant(k, bv.h)][shape_index(sh)],
+                           [&] { return resident_grid(pick_slots(k, bv.h, sh), kProbeThreads, 16384); });
     }
     int wpb;
     size_t lds;
     if (probe_blocks(bv.D, &wpb, &lds) != 0) return 0;
-    const int slot = wpb == 4 ? 0 : wpb == 2 ? 1 : 2;
-    if (!generic[slot]) generic[slot] = resident_grid(probe_cobs_kernel<0, 0>, wpb * kWave, lds);
-    return generic[slot];
+    return cached_grid(generic[wpb == 4 ? 0 : wpb == 2 ? 1 : 2],
+                       [&] { return resident_grid(probe_cobs_kernel<0, 0>, wpb * kWave, lds); });
 }
 
 hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* hits,
@@ -1525,19 +1535,25 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
 
 // Bits tested before the rest (XSPECT_AMD_BLOOM_SPLIT; 0 = all at once).
 static int bloom_split() {
-    static int v = -1;
-    if (v < 0) {
+    static const int v = [] {  // thread-safe one-time init
         const char* e = getenv("XSPECT_AMD_BLOOM_SPLIT");
-        v = e ? atoi(e) : kBloomSplitDefault;
-        if (v != 0 && v != 1 && v != 2 && v != 3) v = kBloomSplitDefault;
-    }
+        const int s = e ? atoi(e) : kBloomSplitDefault;
+        return (s == 0 || s == 1 || s == 2 || s == 3) ? s : kBloomSplitDefault;
+    }();
     return v;
 }
 
 int probe_grid_bloom() {
-    static int cache = 0;
-    if (!cache) cache = resident_grid(probe_bloom_kernel<21, 7, 0>, kProbeThreads, 0);
-    return cache;
+    static std::atomic<int> cache[4];
+    const int sp = bloom_split();
+    return cached_grid(cache[sp], [sp] {
+        switch (sp) {
+            case 1: return resident_grid(probe_bloom_kernel<21, 7, 1>, kProbeThreads, 0);
+            case 2: return resident_grid(probe_bloom_kernel<21, 7, 2>, kProbeThreads, 0);
+            case 3: return resident_grid(probe_bloom_kernel<21, 7, 3>, kProbeThreads, 0);
+            default: return resident_grid(probe_bloom_kernel<21, 7, 0>, kProbeThreads, 0);
+        }
+    });
 }
 
 template <int SPLIT>
