@@ -60,8 +60,12 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
         mine = part_a if rank % 2 == 0 else part_b
         dh, _ = distributed.docs_sharded_hits(
             pr, 1, lambda sl, st: mine.query_packed(sl.buf, sl.offsets, step=st, threads=1))
+        labels = [f"sp{d:02d}" for d in range(10)][::-1]  # label order differs from doc order
+        pred = distributed.reads_sharded_svm_predict(
+            pr, 1, labels, lambda sl, st: local_totals(sl, st),
+            lambda x: "|".join(f"{v:.2f}" for v in x[0]))  # the vector itself, as the "label"
         np.savez(Path(out_dir) / f"r{rank}.npz", tot=tot, nk=nk, lo=lo, hi=hi, hits=hits,
-                 g_tot=g_tot, g_nk=g_nk, dh=dh)
+                 g_tot=g_tot, g_nk=g_nk, dh=dh, pred=np.array(pred))
     finally:
         dist.destroy_process_group()
 
@@ -91,3 +95,12 @@ def test_gloo_reads_and_docs_sharded(tmp_path, world):
     want = np.concatenate([ha if r % 2 == 0 else hb for r in range(world)], axis=1)
     for o in outs:
         assert np.array_equal(o["dh"], want)
+    # SVM vector from the all-reduced totals, formed on rank 0 and broadcast,
+    # equals the single-process ModelResult total scores in label order
+    from xspect_amd.result import ModelResult
+    labels = [f"sp{d:02d}" for d in range(10)][::-1]
+    hits = {f"r{i}": {labels[d]: int(want_h1[i, d]) for d in range(10)} for i in range(len(reads))}
+    res = ModelResult("m", hits, {f"r{i}": int(n) for i, n in enumerate(want_n1)})
+    vec = [v for _, v in sorted(res.get_scores()["total"].items())]
+    for o in outs:
+        assert str(o["pred"]) == "|".join(f"{v:.2f}" for v in vec)

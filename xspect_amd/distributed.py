@@ -103,3 +103,25 @@ def docs_sharded_hits(reads: PackedReads, step: int,
     dist.all_gather(parts, t)
     cols = [p.cpu().numpy()[:, :int(d.item())] for p, d in zip(parts, dims)]
     return np.concatenate(cols, axis=1).view(np.uint32), np.asarray(nk)
+
+
+def svm_vector(labels: list[str], totals, total_kmers: int) -> list[float]:
+    """The SVM feature row from whole-job totals: round(T_d / N, 2) in label
+    order (probabilistic_filter_svm_model.py:212-213 over result.py:57-72)."""
+    scores = {lab: round(int(t) / total_kmers, 2) for lab, t in zip(labels, totals)}
+    return [scores[lab] for lab in sorted(scores)]
+
+
+def reads_sharded_svm_predict(reads: PackedReads, step: int, labels: list[str],
+                              local_totals: Callable[[PackedReads, int], tuple[np.ndarray, int]],
+                              classify: Callable[[list[list[float]]], object], device=None) -> str:
+    """Config 3 end to end: every rank probes its slice, the D+1 totals are
+    all-reduced, rank 0 forms the SVM vector and classifies it, and the label
+    is broadcast to every rank."""
+    tot, nk = reads_sharded_totals(reads, step, local_totals, device)
+    dist = _dist()
+    out = [None]
+    if dist.get_rank() == 0:
+        out[0] = str(classify([svm_vector(labels, tot, nk)]))
+    dist.broadcast_object_list(out, src=0)
+    return out[0]
