@@ -96,8 +96,6 @@ def parse():
     ap.add_argument("--hashes", type=int, default=7, help="species/multigenus: COBS num_hashes (default 7)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--mlst-group", type=int, default=1,
-                    help="mlst: loci probed per launch (xs_query_multi_device); 1 = one launch per locus")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_traffic.json"))
     return ap.parse_args()
 
@@ -160,17 +158,13 @@ class Workload:
         else:  # mlst
             reads, loci_info = self._mlst(args, dev, s)
             self.config.update(loci=len(self.banks), **loci_info)
-            self.kernel = ("probe_cobs_slots<31,1,3,4> (compact, 3 groups x 4 chunks)" if args.mlst_group <= 1 else
-                           f"probe_cobs_multi<31,3,4> ({min(args.mlst_group, len(self.banks))} loci per launch)")
-            self.config.update(loci_per_launch=min(max(1, args.mlst_group), len(self.banks)))
+            self.kernel = "probe_cobs_slots<31,1,3,4> (compact, 3 groups x 4 chunks)"
         self.reads = reads
         self.n = reads.shape[0]
         self.seq_bytes = reads.size
         self.d_seqs = torch.from_numpy(reads.reshape(-1)).to(dev)
         self.d_offs = torch.arange(self.n + 1, dtype=torch.int64, device=dev) * args.read_len
         self.docs = [b.num_docs for b in self.banks]
-        g = max(1, args.mlst_group) if w == "mlst" else 1
-        self.launch_groups = [list(range(i, min(i + g, len(self.banks)))) for i in range(0, len(self.banks), g)]
         self.d_hits = [torch.empty((self.n, d), dtype=torch.int32, device=dev) for d in self.docs]
         self.d_nk = torch.empty(self.n, dtype=torch.int64, device=dev)
         self.d_tot = [torch.zeros(d + 1, dtype=torch.int64, device=dev) for d in self.docs]
@@ -222,7 +216,6 @@ class Workload:
             st = int(rng.integers(0, a.size - args.read_len + 1))
             reads[i] = a[st:st + args.read_len]
         self.rows_per_kmer = sum(len(g) for g in group_rows)  # one 64-B row per group per locus
-        self.bank_rows = [len(g) for g in group_rows]
         # a locus bank (~97 MB) stays in the 256 MB Infinity Cache: count the
         # row itself (page bytes), not an HBM line fill
         self.row_bytes = page
@@ -233,16 +226,9 @@ class Workload:
                        "signature_rows": int(sum(sum(g) for g in group_rows))}
 
     def step(self):
-        from xspect_amd.bank import query_multi_device
-        for grp in self.launch_groups:
-            if len(grp) == 1:
-                b = grp[0]
-                self.banks[b].query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step,
-                                           self.d_hits[b], self.d_nk, self.d_tot[b], stream=self.stream)
-            else:  # the loci of the group in one launch (k-mers assembled and hashed once)
-                query_multi_device([self.banks[b] for b in grp], self.d_seqs, self.seq_bytes, self.d_offs, self.n,
-                                   self.args.step, [self.d_hits[b] for b in grp], self.d_nk,
-                                   [self.d_tot[b] for b in grp], self.stream)
+        for b, h, t in zip(self.banks, self.d_hits, self.d_tot):
+            b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step, h, self.d_nk, t,
+                           stream=self.stream)
         if self.world > 1:
             if self.args.workload == "multigenus":
                 all_gather(self.gathered, self.d_hits[0])  # docs sharded: hit vectors over xGMI
@@ -255,15 +241,14 @@ class Workload:
         return per_rank * self.world
 
     def algo_bytes_per_launch(self):
-        """Bytes one probe launch must move (averaged over the launches of a step)."""
-        per_launch = []
-        for grp in self.launch_groups:
-            rows = sum(self.bank_rows[b] for b in grp) if self.args.workload == "mlst" else self.rows_per_kmer
-            docs = sum(self.docs[b] for b in grp)
+        """Bytes one probe launch must move (per bank; averaged over banks)."""
+        per_bank = []
+        for d in self.docs:
+            rows = self.rows_per_kmer if self.args.workload != "mlst" else self.rows_per_kmer / len(self.docs)
             # rows + the read bytes (one window pass) + hit rows + per-read metadata
-            per_launch.append(self.kmers * rows * self.row_bytes + self.seq_bytes + self.n * docs * 4
-                              + self.n * (8 + 4 + 8 + 8))
-        return sum(per_launch) / len(per_launch)
+            per_bank.append(self.kmers * rows * self.row_bytes + self.seq_bytes + self.n * d * 4
+                            + self.n * (8 + 4 + 8 + 8))
+        return sum(per_bank) / len(per_bank)
 
 
 def main():
@@ -340,8 +325,7 @@ def main():
         try:
             data = json.loads(tj.read_text())
             # multigenus runs the species kernel on a bank of the same size
-            key = args.workload if args.workload != "mlst" or args.mlst_group <= 1 else f"mlst_g{args.mlst_group}"
-            tr = data.get(key) or (data.get("species") if args.workload == "multigenus" else None) or {}
+            tr = data.get(args.workload) or (data.get("species") if args.workload == "multigenus" else None) or {}
             if tr.get("reads") == wl.n:  # measured on this workload at this size
                 traffic = tr.get("hbm_bytes_per_launch")
         except Exception:

@@ -139,18 +139,6 @@ int xs_query_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes,
                     const uint64_t* d_offsets, uint64_t n, uint32_t step, uint32_t* d_hits,
                     uint64_t* d_num_kmers, uint64_t* d_totals, void* stream);
 
-/* Several COBS banks over the same reads in one probe launch (the loci of
- * an MLST scheme, probabilistic_filter_mlst_model.py:237-256): each k-mer is
- * assembled and hashed once for all banks.  Banks share the device and k;
- * one launch needs h = 1 and at most 4 doc groups of <= 512 docs per bank
- * (16 banks); other sets run bank after bank on the same stream.  d_hits[b]
- * (n x D_b uint32) and d_totals[b] (D_b + 1) may be NULL (the arrays
- * themselves too); d_num_kmers (n) may be NULL.  Timed as one probe of
- * banks[0] when its profiling is on. */
-int xs_query_multi_device(xs_bank* const* banks, int nbanks, const void* d_seqs, uint64_t seq_bytes,
-                          const uint64_t* d_offsets, uint64_t n, uint32_t step, uint32_t* const* d_hits,
-                          uint64_t* d_num_kmers, uint64_t* const* d_totals, void* stream);
-
 /* Per-read best doc without materialising the hit matrix on the host:
  * best_doc[r] = the doc with the most hits of read r, or XS_BEST_AMBIGUOUS when
  * two or more docs share the maximum (the per-read call of the reference's

@@ -331,70 +331,3 @@ def test_concurrent_handles_from_threads(xs, oracle_mod):
             assert np.array_equal(got, want[key]), key
     for _, gb, _, _ in pairs:
         gb.close()
-
-
-@pytest.mark.parametrize("k,specs", [
-    # (D, h, page or None) per bank
-    (31, [(1430, 1, 64), (600, 1, 64), (900, 1, 64), (200, 1, 32), (1500, 1, 64), (100, 1, None), (50, 1, 2)]),
-    (21, [(300, 1, 64), (37, 1, None), (1024, 1, 64)]),
-    (21, [(100, 1, None), (60, 7, None), (2600, 1, 64)]),  # h = 7 and G = 6: bank after bank
-])
-def test_multi_bank_probe_matches_oracle(xs, oracle_mod, k, specs):
-    """xs_query_multi_device (the loci of an MLST scheme in one launch) gives
-    each bank exactly its own single-bank result: hits, k-mer counts, totals."""
-    torch = pytest.importorskip("torch")
-    rng = np.random.default_rng(k + len(specs))
-    pairs = []
-    for i, (D, h, page) in enumerate(specs):
-        G = 1 if page is None else -(-D // (8 * page))
-        sig = [int(x) for x in rng.integers(500, 6000, G)]
-        pairs.append(_pair(xs, oracle_mod, D, k, h, sig, page=page, seed=D + i, per_doc=1))
-    reads = _reads(rng, 300, k) + _reads(rng, 20, k, "ACGTNacgt")
-    for _, _, seqs, _ in pairs:
-        reads += [s[:int(rng.integers(k, 400))] for s in seqs[:30]]
-    reads += [b"", b"C" * k, pairs[0][2][0] * 3]  # empty, one k-mer, multi-unit read
-    buf = np.frombuffer(b"".join(reads), dtype=np.uint8)
-    offs = np.zeros(len(reads) + 1, dtype=np.int64)
-    np.cumsum([len(r) for r in reads], out=offs[1:])
-    dev = torch.device("cuda", 0)
-    d_seqs = torch.from_numpy(buf.copy()).to(dev)
-    d_offs = torch.from_numpy(offs).to(dev)
-    stream = torch.cuda.current_stream().cuda_stream
-    banks = [p[1] for p in pairs]
-    for step in (1, 3):
-        hits = [torch.full((len(reads), b.num_docs), 7, dtype=torch.int32, device=dev) for b in banks]
-        tots = [torch.empty(b.num_docs + 1, dtype=torch.int64, device=dev) for b in banks]
-        d_nk = torch.empty(len(reads), dtype=torch.int64, device=dev)
-        xs.query_multi_device(banks, d_seqs, buf.size, d_offs, len(reads), step, hits, d_nk, tots, stream)
-        torch.cuda.synchronize()
-        for (ob, _, _, _), dh, dt in zip(pairs, hits, tots):
-            want_h, want_n = ob.query(reads, step=step)
-            got = dh.cpu().numpy().view(np.uint32)
-            assert np.array_equal(got, want_h), _explain(got, want_h, reads)
-            assert np.array_equal(d_nk.cpu().numpy().view(np.uint64), want_n)
-            t = dt.cpu().numpy().view(np.uint64)
-            assert np.array_equal(t[:-1], want_h.sum(axis=0, dtype=np.uint64)) and int(t[-1]) == int(want_n.sum())
-    # totals only (no hit matrices), and no reads
-    tots = [torch.empty(b.num_docs + 1, dtype=torch.int64, device=dev) for b in banks]
-    xs.query_multi_device(banks, d_seqs, buf.size, d_offs, len(reads), 1, None, None, tots, stream)
-    torch.cuda.synchronize()
-    for (ob, _, _, _), dt in zip(pairs, tots):
-        want_h, want_n = ob.query(reads)
-        t = dt.cpu().numpy().view(np.uint64)
-        assert np.array_equal(t[:-1], want_h.sum(axis=0, dtype=np.uint64)) and int(t[-1]) == int(want_n.sum())
-    xs.query_multi_device(banks, d_seqs, buf.size, d_offs, 0, 1, None, None, tots, stream)
-    torch.cuda.synchronize()
-    assert all(int(t.abs().sum()) == 0 for t in tots)
-    for _, gb, _, _ in pairs:
-        gb.close()
-
-
-def test_multi_bank_rejects_bad_sets(xs):
-    a = xs.Bank.create_cobs(21, 1, [101], 5)
-    b = xs.Bank.create_cobs(31, 1, [101], 5)
-    c = xs.Bank.create_bloom(21, 4096, 7)
-    for bad in ([a, b], [a, c], [a, a]):
-        with pytest.raises(RuntimeError, match="share the device|COBS banks|appears twice"):
-            xs.query_multi_device(bad, None, 0, None, 0)
-    for x in (a, b, c):
-        x.close()

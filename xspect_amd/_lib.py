@@ -98,7 +98,6 @@ SIGNATURES = {
     "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
-    "xs_query_multi_device": (_int, [_vp, _int, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "xs_query_best": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "xs_gather_reads_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "xs_best_device": (_int, [_vp, _u64, _u64, _vp, _vp, _vp]),

@@ -265,20 +265,6 @@ def best_device(hits, n: int, num_docs: int, best, best_hits=None, stream: int |
     check(load().xs_best_device(_dptr(hits), n, num_docs, _dptr(best), _dptr(best_hits), stream))
 
 
-def query_multi_device(banks, seqs, seq_bytes: int, offsets, n: int, step: int = 1, hits=None,
-                       num_kmers=None, totals=None, stream: int | None = None) -> None:
-    """xs_query_multi_device: several COBS banks over the same device reads in
-    one launch.  `hits` / `totals`: per-bank lists of device tensors (or None)."""
-    nb = len(banks)
-    arr = (ctypes.c_void_p * nb)(*[b.handle for b in banks])
-    h = (ctypes.c_void_p * nb)(*[_dptr(x) for x in hits]) if hits is not None else None
-    t = (ctypes.c_void_p * nb)(*[_dptr(x) for x in totals]) if totals is not None else None
-    check(load().xs_query_multi_device(ctypes.cast(arr, ctypes.c_void_p), nb, _dptr(seqs), seq_bytes, _dptr(offsets),
-                                       n, step, ctypes.cast(h, ctypes.c_void_p) if h is not None else None,
-                                       _dptr(num_kmers), ctypes.cast(t, ctypes.c_void_p) if t is not None else None,
-                                       stream))
-
-
 def gather_reads_device(seqs, offsets, index, m: int, out_seqs, out_offsets, stream: int | None = None) -> None:
     """xs_gather_reads_device: out read j = read index[j] at out_offsets[j]."""
     check(load().xs_gather_reads_device(_dptr(seqs), _dptr(offsets), _dptr(index), m, _dptr(out_seqs),

@@ -22,7 +22,6 @@
 
 #include <hip/hip_runtime.h>
 
-#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -850,83 +849,6 @@ int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_
         HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
     if (totals_out) HIPCHK(hipMemcpyAsync(totals_out, d_tot, (cols + 1) * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
-    return XS_OK;
-}
-
-int xs_query_multi_device(xs_bank* const* banks, int nbanks, const void* d_seqs, uint64_t seq_bytes,
-                          const uint64_t* d_offsets, uint64_t n, uint32_t step, uint32_t* const* d_hits,
-                          uint64_t* d_num_kmers, uint64_t* const* d_totals, void* stream) {
-    if (!banks || nbanks < 1) return fail(XS_ERR_ARG, "no banks");
-    for (int b = 0; b < nbanks; ++b) {
-        if (!banks[b]) return fail(XS_ERR_ARG, "null bank");
-        if (banks[b]->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "multi-bank queries take COBS banks");
-        if (banks[b]->device != banks[0]->device || banks[b]->k != banks[0]->k)
-            return fail(XS_ERR_ARG, "banks of one multi-bank query share the device and k");
-        for (int c = 0; c < b; ++c)
-            if (banks[c] == banks[b]) return fail(XS_ERR_ARG, "a bank appears twice");
-    }
-    if (!d_offsets || (!d_seqs && n)) return fail(XS_ERR_ARG, "null argument");
-    std::vector<CobsView> views((size_t)nbanks);
-    for (int b = 0; b < nbanks; ++b) views[b] = banks[b]->cobs_view();
-    if (nbanks > kMultiMaxBanks || !multi_supported(views.data(), (uint32_t)nbanks, banks[0]->k)) {
-        // not one launch: the banks one after another on the same stream
-        for (int b = 0; b < nbanks; ++b)
-            if (int rc = xs_query_device(banks[b], d_seqs, seq_bytes, d_offsets, n, step, d_hits ? d_hits[b] : nullptr,
-                                         b == 0 ? d_num_kmers : nullptr, d_totals ? d_totals[b] : nullptr, stream))
-                return rc;
-        return XS_OK;
-    }
-    // lock every bank (address order: no deadlock with concurrent multi-bank calls)
-    std::vector<xs_bank*> order(banks, banks + nbanks);
-    std::sort(order.begin(), order.end());
-    std::vector<std::unique_lock<std::mutex>> locks;
-    for (xs_bank* b : order) locks.emplace_back(b->mu);
-    xs_bank* w = banks[0];  // its workspace serves the launch
-    HIPCHK(hipSetDevice(w->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);
-    if (n == 0) {
-        for (int b = 0; b < nbanks; ++b)
-            if (d_totals && d_totals[b]) HIPCHK(hipMemsetAsync(d_totals[b], 0, (banks[b]->D + 1) * 8, s));
-        return XS_OK;
-    }
-    if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
-    if (n >= (1ull << 31)) return fail(XS_ERR_ARG, "at most 2^31-1 reads per call");
-    Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n};
-    ReadView rv;
-    uint32_t* hits0 = d_hits ? d_hits[0] : nullptr;
-    if (int rc = prepare_units(w, in, step, d_num_kmers, hits0, banks[0]->D, s, &rv)) return rc;
-    for (int b = 1; b < nbanks; ++b)
-        if (d_hits && d_hits[b])
-            HIPCHK(launch_zero_split_rows(w->nseg.as<uint64_t>(), n, d_hits[b], banks[b]->D, s));
-    MultiArgs ma{};
-    ma.nb = (uint32_t)nbanks;
-    const int blocks = std::max(1, probe_grid_multi(views.data(), (uint32_t)nbanks, w->k));
-    uint64_t part = 0;
-    for (int b = 0; b < nbanks; ++b) {
-        ma.v[b] = views[b];
-        ma.hits[b] = d_hits ? d_hits[b] : nullptr;
-        ma.part_off[b] = part;
-        part += (uint64_t)blocks * (banks[b]->D + 1);
-    }
-    if (int rc = w->partials.ensure(part * 8)) return rc;
-    uint64_t* partials = w->partials.as<uint64_t>();
-    if (w->profiling) {
-        if (w->events_used == w->events.size()) {
-            hipEvent_t a, c;
-            HIPCHK(hipEventCreate(&a));
-            HIPCHK(hipEventCreate(&c));
-            w->events.emplace_back(a, c);
-        }
-        HIPCHK(hipEventRecord(w->events[w->events_used].first, s));
-    }
-    HIPCHK(launch_probe_multi(rv, ma, partials, blocks, s));
-    if (w->profiling) {
-        HIPCHK(hipEventRecord(w->events[w->events_used].second, s));
-        ++w->events_used;
-    }
-    for (int b = 0; b < nbanks; ++b)
-        if (d_totals && d_totals[b])
-            HIPCHK(launch_reduce_partials(partials + ma.part_off[b], blocks, banks[b]->D + 1, d_totals[b], s));
     return XS_OK;
 }
 

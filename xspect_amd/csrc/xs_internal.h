@@ -103,21 +103,6 @@ hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_
 hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
                                uint8_t* out, const uint64_t* out_offs, hipStream_t s);
 
-// Several COBS banks (same k, h = 1) in one probe launch (MLST loci); passed
-// by value as kernel arguments.
-constexpr int kMultiMaxBanks = 16;
-struct MultiArgs {
-    CobsView v[kMultiMaxBanks];
-    uint32_t* hits[kMultiMaxBanks];      // n x D_b hit matrices (may be NULL)
-    uint64_t part_off[kMultiMaxBanks];   // bank b's partials start (blocks x (D_b + 1))
-    uint32_t nb;
-    uint32_t dstride;                    // LDS counters per bank (set by the launcher)
-};
-bool multi_supported(const CobsView* views, uint32_t nb, uint32_t k);
-int probe_grid_multi(const CobsView* views, uint32_t nb, uint32_t k);
-hipError_t launch_probe_multi(const ReadView& rv, MultiArgs ma, uint64_t* partials, int blocks, hipStream_t s);
-hipError_t launch_zero_split_rows(const uint64_t* nseg, uint64_t n, uint32_t* hits, uint64_t D, hipStream_t s);
-
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
 

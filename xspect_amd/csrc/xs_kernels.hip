@@ -16,7 +16,6 @@
 //   rbloom `kmer in bf`                    probabilistic_single_filter_model.py:122-124
 #include <hipcub/hipcub.hpp>
 
-#include <algorithm>
 #include <atomic>
 #include <cstdlib>
 
@@ -353,15 +352,6 @@ __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
             queue[1] = 0;
         }
     }
-}
-
-// Zero the hit rows of reads the probe does not store whole (no k-mers, or
-// split over several units): for the extra banks of a multi-bank probe.
-__global__ void zero_split_rows_kernel(const uint64_t* __restrict__ nseg, uint64_t n, uint32_t* __restrict__ hits,
-                                       uint64_t D) {
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n; r += (uint64_t)gridDim.x * blockDim.x)
-        if (nseg[r] != 1)
-            for (uint64_t d = 0; d < D; ++d) hits[r * D + d] = 0;
 }
 
 // Hand out kGrab units per atomic to balance ragged reads across waves.
@@ -841,144 +831,6 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
             uint64_t s = 0;
             for (int w = 0; w < wpb; ++w) s += s_kmers[w];
             out[D] = s;
-        }
-    }
-}
-
-// ------------------------------------------------------------------ COBS probe (several banks)
-// One launch for the loci of an MLST scheme (or any set of COBS banks with
-// the same k and h = 1): each unit's k-mers are assembled and hashed once,
-// kept in registers (one u64 per lane per tile), then probed against every
-// bank in turn with the slot-kernel gather and counting.  The per-bank
-// totals live in LDS as u32 (a block never counts 2^32 k-mers).
-template <int KT, int GM, int CM>
-__global__ void __launch_bounds__(kProbeThreads, 4) probe_cobs_multi(ReadView rv, MultiArgs ma,
-                                                                     uint64_t* __restrict__ partials) {
-    const uint32_t nb = ma.nb, dstride = ma.dstride;
-    constexpr int NS = GM * CM;
-    constexpr int TM = (int)(kSegKmers / 64);  // tiles per unit
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_tot32[];  // [nb][dstride]
-    __shared__ uint64_t s_kmers[kProbeThreads / kWave];
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    for (uint32_t d = threadIdx.x; d < nb * dstride; d += blockDim.x) s_tot32[d] = 0;
-    __syncthreads();
-    Xpose X;
-    xpose_init(lane, X);
-    const uint32_t k = KT ? KT : rv.k;
-    const uint32_t step = rv.step;
-    const uint64_t U = rv.queue[0];
-    uint64_t kmer_total = 0;
-
-    for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
-        if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
-        for (uint64_t u = base; u < uend; ++u) {
-            const uint32_t r = rv.unit_read[u];
-            const uint64_t seg = u - rv.unit_ofs[r];
-            const uint64_t o0 = rv.offs[r];
-            const uint64_t len = rv.offs[r + 1] - o0;
-            const uint64_t nk = num_kmers(len, k, step);
-            const uint64_t t0 = seg * kSegKmers;
-            const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
-            kmer_total += cnt;
-            const bool whole = nk <= kSegKmers;
-            // XXH64(canonical k-mer, seed 0) of every k-mer of the unit, once
-            uint64_t hv[TM];
-#pragma unroll
-            for (int tt = 0; tt < TM; ++tt) {
-                hv[tt] = 0;
-                const uint32_t idx = (uint32_t)tt * 64 + (uint32_t)lane;
-                if (idx < cnt) {
-                    Kmer c;
-                    kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + idx) * step, k, c);
-                    Xxh64Pre pre;
-                    xxh64_pre<KT>(c, k, pre);
-                    hv[tt] = xxh64_seed<KT>(c, pre, k, 0ull);
-                }
-            }
-            for (uint32_t b = 0; b < nb; ++b) {
-                const CobsView bv = ma.v[b];
-                const uint32_t G = bv.G, cpg = bv.nchunks;
-                const uint64_t D = bv.D, gdocs = 8 * bv.page;
-                uint32_t acc[2 * NS];
-#pragma unroll
-                for (int i = 0; i < 2 * NS; ++i) acc[i] = 0;
-#pragma unroll
-                for (int tt = 0; tt < TM; ++tt) {
-                    if ((uint32_t)tt * 64 >= cnt) continue;  // uniform
-                    const bool act = (uint32_t)tt * 64 + (uint32_t)lane < cnt;
-                    uint4 mk[NS];
-#pragma unroll
-                    for (int g = 0; g < GM; ++g) {
-                        const bool on = (uint32_t)g < G && act;
-                        uint64_t ro = 0;
-                        if ((uint32_t)g < G) {
-                            const GroupDesc gd = bv.groups[g];
-                            ro = gd.base + fastmod(hv[tt], gd.sig, gd.magic) * bv.pitch;
-                        }
-#pragma unroll
-                        for (int cc = 0; cc < CM; ++cc)
-                            mk[g * CM + cc] = (on && (uint32_t)cc < cpg)
-                                                  ? *reinterpret_cast<const uint4*>(bv.rows + ro + cc * 16)
-                                                  : make_uint4(0u, 0u, 0u, 0u);
-                    }
-#pragma unroll
-                    for (int g = 0; g < GM; ++g) {
-#pragma unroll
-                        for (int cc = 0; cc < CM; ++cc) {
-                            if ((uint32_t)g < G && (uint32_t)cc < cpg) {
-                                const int i = g * CM + cc;
-                                const uint32_t w[4] = {mk[i].x, mk[i].y, mk[i].z, mk[i].w};
-#pragma unroll
-                                for (int q = 0; q < 4; ++q)
-                                    if (__ballot(w[q] != 0u) != 0ull)
-                                        acc[2 * i + (q >> 1)] += column_popc32(w[q], X) << (16 * (q & 1));
-                            }
-                        }
-                    }
-                }
-                uint32_t* hits = ma.hits[b];
-                uint32_t* tot = s_tot32 + (size_t)b * dstride;
-#pragma unroll
-                for (int g = 0; g < GM; ++g) {
-                    if ((uint32_t)g >= G) continue;
-                    const uint64_t glim = min(D, (uint64_t)g * gdocs + gdocs);
-#pragma unroll
-                    for (int cc = 0; cc < CM; ++cc) {
-                        if ((uint32_t)cc >= cpg) continue;
-                        const int i = g * CM + cc;
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const uint64_t d0 = (uint64_t)g * gdocs + cc * 128 + q * 32;
-                            if (d0 >= glim) continue;
-                            const uint32_t v = fold_halves((acc[2 * i + (q >> 1)] >> (16 * (q & 1))) & 0xFFFFu);
-                            const uint64_t d = d0 + (uint64_t)lane;
-                            if (lane < 32 && d < glim) {
-                                if (v) atomicAdd(&tot[d], v);
-                                if (hits) {
-                                    if (whole) hits[(uint64_t)r * D + d] = v;
-                                    else if (v) atomicAdd(&hits[(uint64_t)r * D + d], v);
-                                }
-                            }
-                        }
-                    }
-                }
-            }
-        }
-    }
-    if (lane == 0) s_kmers[wid] = kmer_total;
-    __syncthreads();
-    if (partials) {
-        const int wpb = blockDim.x >> 6;
-        uint64_t ksum = 0;
-        for (int w = 0; w < wpb; ++w) ksum += s_kmers[w];
-        for (uint32_t b = 0; b < nb; ++b) {
-            const uint64_t D = ma.v[b].D;
-            uint64_t* out = partials + ma.part_off[b] + (uint64_t)blockIdx.x * (D + 1);
-            for (uint64_t d = threadIdx.x; d < D; d += blockDim.x) out[d] = s_tot32[(size_t)b * dstride + d];
-            if (threadIdx.x == 0) out[D] = ksum;
         }
     }
 }
@@ -1775,64 +1627,6 @@ hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const 
                                uint8_t* out, const uint64_t* out_offs, hipStream_t s) {
     if (m == 0) return hipSuccess;
     gather_reads_kernel<<<grid_for(m, 4, 16384), 256, 0, s>>>(seqs, offs, index, m, out, out_offs);
-    return hipGetLastError();
-}
-
-// Multi-bank probe: the kernel shape for a set of banks (one shape covering
-// every bank's groups x chunks), or {0, 0} when the set does not qualify.
-static SlotShape multi_shape(const CobsView* v, uint32_t nb, uint32_t k) {
-    (void)k;
-    if (nb == 0 || nb > (uint32_t)kMultiMaxBanks) return {0, 0};
-    uint64_t G = 0, c = 0, dpad = 0;
-    for (uint32_t b = 0; b < nb; ++b) {
-        if (v[b].h != 1) return {0, 0};
-        G = std::max<uint64_t>(G, v[b].G);
-        c = std::max<uint64_t>(c, v[b].nchunks);
-        dpad = std::max<uint64_t>(dpad, (v[b].D + 127) / 128 * 128);
-    }
-    if (nb * dpad * 4 > kLdsBudget) return {0, 0};
-    if (c <= 4 && G <= 4) return {(int)(G <= 1 ? 1 : G <= 2 ? 2 : G <= 3 ? 3 : 4), 4};
-    return {0, 0};
-}
-
-using MultiFn = void (*)(ReadView, MultiArgs, uint64_t*);
-
-template <int KT>
-static MultiFn multi_fn(int gm) {
-    return gm == 1 ? probe_cobs_multi<KT, 1, 4> : gm == 2 ? probe_cobs_multi<KT, 2, 4>
-                   : gm == 3 ? probe_cobs_multi<KT, 3, 4> : probe_cobs_multi<KT, 4, 4>;
-}
-
-static size_t multi_lds(const CobsView* v, uint32_t nb, uint32_t* dstride) {
-    uint64_t dpad = 0;
-    for (uint32_t b = 0; b < nb; ++b) dpad = std::max<uint64_t>(dpad, (v[b].D + 127) / 128 * 128);
-    *dstride = (uint32_t)dpad;
-    return (size_t)nb * dpad * 4;
-}
-
-bool multi_supported(const CobsView* views, uint32_t nb, uint32_t k) { return multi_shape(views, nb, k).gm != 0; }
-
-int probe_grid_multi(const CobsView* views, uint32_t nb, uint32_t k) {
-    const SlotShape sh = multi_shape(views, nb, k);
-    if (!sh.gm) return 0;
-    uint32_t dstride;
-    const size_t lds = multi_lds(views, nb, &dstride);
-    const MultiFn fn = k == 31 ? multi_fn<31>(sh.gm) : multi_fn<0>(sh.gm);
-    return resident_grid(fn, kProbeThreads, lds);  // LDS depends on the bank set: not cached
-}
-
-hipError_t launch_probe_multi(const ReadView& rv, MultiArgs ma, uint64_t* partials, int blocks, hipStream_t s) {
-    const SlotShape sh = multi_shape(ma.v, ma.nb, rv.k);
-    if (!sh.gm) return hipErrorInvalidValue;
-    const size_t lds = multi_lds(ma.v, ma.nb, &ma.dstride);
-    const MultiFn fn = rv.k == 31 ? multi_fn<31>(sh.gm) : multi_fn<0>(sh.gm);
-    fn<<<blocks, kProbeThreads, lds, s>>>(rv, ma, partials);
-    return hipGetLastError();
-}
-
-hipError_t launch_zero_split_rows(const uint64_t* nseg, uint64_t n, uint32_t* hits, uint64_t D, hipStream_t s) {
-    if (n == 0 || !hits) return hipSuccess;
-    zero_split_rows_kernel<<<grid_for(n, 256, 4096), 256, 0, s>>>(nseg, n, hits, D);
     return hipGetLastError();
 }
 
