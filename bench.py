@@ -110,8 +110,8 @@ class Workload:
 
     def __init__(self, args, rank, world, dev, stream):
         import torch
-        from xspect_amd.bank import Bank, bloom_parameters, cobs_signature_size
-        from xspect_amd.synth import make_genomes, make_reads
+        from xspect2_amd.bank import Bank, bloom_parameters, cobs_signature_size
+        from xspect2_amd.synth import make_genomes, make_reads
 
         self.args, self.rank, self.world, self.dev = args, rank, world, dev
         s = stream.cuda_stream
@@ -175,7 +175,7 @@ class Workload:
 
     def _mlst(self, args, dev, s):
         import torch
-        from xspect_amd.bank import Bank, cobs_signature_size
+        from xspect2_amd.bank import Bank, cobs_signature_size
         rng = np.random.default_rng(4242)
         acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
         loci, n_alleles, page = 7, 1430, 64
@@ -387,7 +387,7 @@ def cpu_baseline(wl, args):
     """Oracle C restatement on a bounded sample of the same reads (rank 0, N=1)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # checker + CPU baseline only
-    from xspect_amd.packing import pack_fixed
+    from xspect2_amd.packing import pack_fixed
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     obanks = []
@@ -437,7 +437,7 @@ def host_path(wl, args, reps=3):
     in pageable host memory -> H2D -> kernels -> D2H of the n x D hit matrix
     (xs_query), and of the totals only (xs_query_totals).  PCIe-inclusive;
     never the headline value, which starts with the reads in HBM."""
-    from xspect_amd.packing import pack_fixed
+    from xspect2_amd.packing import pack_fixed
 
     pr = pack_fixed(wl.reads)
     out = {}

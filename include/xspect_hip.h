@@ -197,7 +197,7 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
  * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path
  * probabilistic_filter_model.py:316-330).  Records come out packed the way
- * xs_query takes them.  Semantics: see xspect_amd/csrc/xs_fastx.cpp. */
+ * xs_query takes them.  Semantics: see xspect2_amd/csrc/xs_fastx.cpp. */
 #define XS_FASTX_FASTA 1
 #define XS_FASTX_FASTQ 2
 #define XS_FASTX_PINNED 1 /* flag: batch sequence/offset buffers in pinned host memory */

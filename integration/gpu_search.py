@@ -2,7 +2,7 @@
 
 This is the file a maintainer drops into the reference as
 src/xspect/models/gpu_search.py.  It depends on
-ctypes + numpy only: no torch, no xspect_amd.  GpuSearch stands in for
+ctypes + numpy only: no torch, no xspect2_amd.  GpuSearch stands in for
 cobs_index.Search (probabilistic_filter_model.py:389, :227) and for
 rbloom.Bloom.load (probabilistic_single_filter_model.py:155-158).
 Tested by tests/test_integration_stub.py.

@@ -1,7 +1,7 @@
 """Pure-Python restatement of Biopython's FASTA / FASTQ record parsing.
 
 TEST INFRASTRUCTURE ONLY: the checker for the native reader
-(xspect_amd/csrc/xs_fastx.cpp, xs_fastx_* in include/xspect_hip.h).  Only
+(xspect2_amd/csrc/xs_fastx.cpp, xs_fastx_* in include/xspect_hip.h).  Only
 tests/ may import it.
 
 The reference parses input files with ``Bio.SeqIO.parse(path, "fasta"|"fastq")``

@@ -1,7 +1,7 @@
 """CPU ORACLE for the k-mer x filter probe path (test infrastructure only).
 
 Only ``tests/``, ``__graft_entry__.smoke()`` and the ``cpu_baseline`` leg of
-``bench.py`` may import this module.  The product path (``xspect_amd``)
+``bench.py`` may import this module.  The product path (``xspect2_amd``)
 never imports it and never falls back to it.
 
 Two independent restatements live here and are checked against each other

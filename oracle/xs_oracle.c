@@ -3,7 +3,7 @@
  *
  * This file is the plain-C restatement of the k-mer extract + probabilistic
  * filter lookup that XspecT delegates to its native dependencies.  It is the
- * CHECKER for the HIP product path in xspect_amd/csrc; nothing in the product
+ * CHECKER for the HIP product path in xspect2_amd/csrc; nothing in the product
  * links, loads or calls it.  Only tests/, __graft_entry__.smoke() and the
  * cpu_baseline leg of bench.py may use it.
  *

@@ -24,7 +24,7 @@ def test_header_parses_and_lists_entry_points():
 
 
 def test_library_exports_every_declared_symbol():
-    from xspect_amd import _lib
+    from xspect2_amd import _lib
     lib = _lib.load()
     out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.SO_PATH)], capture_output=True,
                          text=True, check=True).stdout
@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_version_and_errors_without_gpu():
-    from xspect_amd import _lib
+    from xspect2_amd import _lib
     lib = _lib.load()
     assert lib.xs_version() >= 100
     # argument errors are reported before any device work
@@ -51,11 +51,11 @@ def test_version_and_errors_without_gpu():
 
 def test_product_does_not_import_oracle():
     """The product package never touches oracle/ (checker only)."""
-    for py in (ROOT / "xspect_amd").rglob("*.py"):
+    for py in (ROOT / "xspect2_amd").rglob("*.py"):
         src = py.read_text()
         assert "import oracle" not in src and "from oracle" not in src, py
         assert "liboracle" not in src, py
-    for c in (ROOT / "xspect_amd" / "csrc").iterdir():
+    for c in (ROOT / "xspect2_amd" / "csrc").iterdir():
         src = c.read_text()
         assert not re.search(r'#include\s+[<"][^>"]*oracle', src), c
         assert "xo_" not in re.sub(r"//.*", "", src), c

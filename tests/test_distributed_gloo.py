@@ -1,4 +1,4 @@
-"""Multi-process collectives of xspect_amd.distributed with gloo on CPU.
+"""Multi-process collectives of xspect2_amd.distributed with gloo on CPU.
 
 The per-rank compute is the CPU oracle here (test infrastructure); on MI355X
 the same functions run with the HIP banks and RCCL (bench.py, config 3).
@@ -42,8 +42,8 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
     import torch.distributed as dist
-    from xspect_amd import distributed
-    from xspect_amd.packing import pack_sequences
+    from xspect2_amd import distributed
+    from xspect2_amd.packing import pack_sequences
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -97,7 +97,7 @@ def test_gloo_reads_and_docs_sharded(tmp_path, world):
         assert np.array_equal(o["dh"], want)
     # SVM vector from the all-reduced totals, formed on rank 0 and broadcast,
     # equals the single-process ModelResult total scores in label order
-    from xspect_amd.result import ModelResult
+    from xspect2_amd.result import ModelResult
     labels = [f"sp{d:02d}" for d in range(10)][::-1]
     hits = {f"r{i}": {labels[d]: int(want_h1[i, d]) for d in range(10)} for i in range(len(reads))}
     res = ModelResult("m", hits, {f"r{i}": int(n) for i, n in enumerate(want_n1)})

@@ -19,7 +19,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "oracle"))
 import fastx as ofx  # noqa: E402  (test-only checker)
 
-from xspect_amd.file_io import FastxReader, get_record_iterator, read_batches  # noqa: E402
+from xspect2_amd.file_io import FastxReader, get_record_iterator, read_batches  # noqa: E402
 
 
 def _pick(rng, alphabet: bytes, n: int) -> bytes:

@@ -13,8 +13,8 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from xspect_amd.file_io import Record, get_record_iterator, write_fasta
-from xspect_amd.synth import make_genomes
+from xspect2_amd.file_io import Record, get_record_iterator, write_fasta
+from xspect2_amd.synth import make_genomes
 
 pytestmark = pytest.mark.gpu
 
@@ -67,7 +67,7 @@ def _expected_hits(ob, names, seqs, step=1, exclude=None):
 
 
 def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mod, monkeypatch):
-    from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
 
     base = tmp_path / "xspect_data"
     model = ProbabilisticFilterModel(K, "Test Filter", "John Doe", "j@x", "Species", base)
@@ -103,7 +103,7 @@ def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mo
     assert res2.hits["read_0"][key] == w3[0]["GCF_000006945"]
 
     # FASTQ path streamed in many native batches == the same records in memory
-    import xspect_amd.file_io as fio
+    import xspect2_amd.file_io as fio
     fq = tmp_path / "reads.fq"
     fq.write_text("".join(f"@{r.id} d\n{r.seq}\n+\n{'I' * len(r.seq)}\n" for r in recs))
     monkeypatch.setattr(fio, "DEFAULT_BATCH_TEXT", 1500)
@@ -123,7 +123,7 @@ def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mo
 
 
 def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
-    from xspect_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+    from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
 
     svm_dir = tmp_path / "svm"
     for i in range(4):
@@ -160,7 +160,7 @@ def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
 
 
 def test_genus_bloom_model(tmp_path, genomes, oracle_mod):
-    from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+    from xspect2_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
 
     fa = tmp_path / "concatenated_assembly.fna"
     write_fasta([Record("a", genomes[0].tobytes().decode()), Record("b", genomes[1].tobytes().decode())], fa)
@@ -203,7 +203,7 @@ def _scheme(tmp_path, rng, loci=3, alleles=40):
 
 
 def test_mlst_model(tmp_path, oracle_mod):
-    from xspect_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+    from xspect2_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
 
     rng = np.random.default_rng(5)
     root = _scheme(tmp_path, rng)

@@ -16,8 +16,8 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(scope="module")
 def xs():
-    from xspect_amd import bank as bank_mod
-    from xspect_amd import _lib
+    from xspect2_amd import bank as bank_mod
+    from xspect2_amd import _lib
     assert _lib.device_count() >= 1, "no HIP device visible"
     return bank_mod
 

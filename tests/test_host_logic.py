@@ -7,15 +7,15 @@ from pathlib import Path
 import numpy as np
 import pytest
 
-from xspect_amd import distributed
-from xspect_amd.bank import bloom_parameters, cobs_signature_size
-from xspect_amd.file_io import Record, get_record_iterator, prepare_input_output_paths, write_fasta
-from xspect_amd.packing import pack_fixed, pack_sequences
-from xspect_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
-from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel, _batches, cobs_result_order
-from xspect_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
-from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
-from xspect_amd.util import slugify
+from xspect2_amd import distributed
+from xspect2_amd.bank import bloom_parameters, cobs_signature_size
+from xspect2_amd.file_io import Record, get_record_iterator, prepare_input_output_paths, write_fasta
+from xspect2_amd.packing import pack_fixed, pack_sequences
+from xspect2_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel, _batches, cobs_result_order
+from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+from xspect2_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+from xspect2_amd.util import slugify
 
 
 def _model(tmp_path, **kw):
@@ -114,7 +114,7 @@ def test_packing_and_batches():
     assert pr.offsets.tolist() == [0, 4, 4, 6] and pr.buf[:6].tobytes() == b"ACGTGG"
     pf = pack_fixed(np.frombuffer(b"AAAACCCC", dtype=np.uint8).reshape(2, 4))
     assert pf.offsets.tolist() == [0, 4, 8] and pf.n == 2
-    import xspect_amd.probabilistic_filter_model as pfm
+    import xspect2_amd.probabilistic_filter_model as pfm
     old = pfm.MAX_BATCH_BYTES
     pfm.MAX_BATCH_BYTES = 10
     try:

@@ -16,13 +16,13 @@ import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
-LIB = ROOT / "xspect_amd" / "libxspect_hip.so"
+LIB = ROOT / "xspect2_amd" / "libxspect_hip.so"
 
 
 def _load_stub():
     if not LIB.exists():
         pytest.skip("libxspect_hip.so not built")
-    from xspect_amd import _lib
+    from xspect2_amd import _lib
     _lib.load()  # same process-wide HIP runtime as the product path
     os.environ["XSPECT_HIP_LIB"] = str(LIB)
     spec = importlib.util.spec_from_file_location("gpu_search", ROOT / "integration" / "gpu_search.py")
@@ -51,7 +51,7 @@ def test_integration_doc_matches_stub():
 @pytest.mark.gpu
 def test_stub_search_matches_oracle(oracle_mod, tmp_path):
     mod = _load_stub()
-    from xspect_amd import bank as xs
+    from xspect2_amd import bank as xs
 
     rng = np.random.default_rng(11)
     D, k, h, sig = 12, 21, 7, [6007]

@@ -10,7 +10,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from xspect_amd.result import MatrixResult, ModelResult
+from xspect2_amd.result import MatrixResult, ModelResult
 
 
 def _dict_result(slug, ids, labels, hits, nk, step=1, prediction=None, source=None, mask=None):
@@ -75,7 +75,7 @@ def test_escaping_duplicates_and_display_labels(tmp_path):
 
 def test_scores_round_like_python():
     """Every (h, n) score string equals repr(round(h / n, 2)) for n up to 300."""
-    from xspect_amd.result import MatrixResult as MR
+    from xspect2_amd.result import MatrixResult as MR
     import json
     for n in list(range(1, 301)) + [1000, 4096, 99991]:
         hs = range(n + 1) if n <= 300 else range(0, n + 1, max(1, n // 997))

@@ -1,4 +1,4 @@
-"""Fused genus -> species pipeline (xspect_amd.pipeline).
+"""Fused genus -> species pipeline (xspect2_amd.pipeline).
 
 CPU: the keep decision equals the reference's round(h / n, 2) >= threshold
 (result.py get_filter_mask) on every (h, n).  GPU: one fused pass writes the
@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 import pytest
 
-from xspect_amd.pipeline import check_threshold, keep_mask
+from xspect2_amd.pipeline import check_threshold, keep_mask
 
 
 def test_keep_mask_matches_python_round():
@@ -31,11 +31,11 @@ def test_keep_mask_matches_python_round():
 @pytest.mark.parametrize("fmt,threshold,dup", [("fq", 0.7, False), ("fasta", 0.0, False), ("fq", 1.0, False),
                                                ("fq", -1, False), ("fq", 0.7, True)])
 def test_fused_pipeline_equals_three_pass(tmp_path, fmt, threshold, dup):
-    from xspect_amd.file_io import Record, write_fasta
-    from xspect_amd.pipeline import reference_pipeline, run_pipeline
-    from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
-    from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
-    from xspect_amd.synth import make_genomes
+    from xspect2_amd.file_io import Record, write_fasta
+    from xspect2_amd.pipeline import reference_pipeline, run_pipeline
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect2_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+    from xspect2_amd.synth import make_genomes
 
     k = 21
     genomes = make_genomes(4, 30_000, seed=5)
@@ -70,7 +70,7 @@ def test_fused_pipeline_equals_three_pass(tmp_path, fmt, threshold, dup):
             else:
                 fh.write(f">{desc}\n{seq}\n")
 
-    import xspect_amd.file_io as fio
+    import xspect2_amd.file_io as fio
     fio_default = fio.DEFAULT_BATCH_TEXT
     fio.DEFAULT_BATCH_TEXT = 20_000  # many batches
     try:

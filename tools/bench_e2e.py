@@ -39,9 +39,9 @@ def main():
     args = ap.parse_args()
 
     import torch
-    from xspect_amd.bank import Bank, cobs_signature_size
-    from xspect_amd.file_io import FastxReader, read_batches
-    from xspect_amd.synth import make_genomes, make_reads
+    from xspect2_amd.bank import Bank, cobs_signature_size
+    from xspect2_amd.file_io import FastxReader, read_batches
+    from xspect2_amd.synth import make_genomes, make_reads
 
     k = 21
     dev = torch.device("cuda", 0)
@@ -108,7 +108,7 @@ def main():
     res["e2e_best_reads_per_s_pinned"] = n / dt
 
     # result JSON: columnar writer (whole file) vs per-read dicts (sample, scaled)
-    from xspect_amd.result import MatrixResult
+    from xspect2_amd.result import MatrixResult
     ids, hs, nks = [], [], []
     for b in read_batches(fq, mb):
         h, nk = bank.query(b.packed)
@@ -140,10 +140,10 @@ def main():
         f.unlink()
 
     # fused genus -> species pipeline vs the reference's three passes, on 200k reads
-    from xspect_amd.bank import bloom_parameters
-    from xspect_amd.pipeline import reference_pipeline, run_pipeline
-    from xspect_amd.probabilistic_filter_model import ProbabilisticFilterModel
-    from xspect_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
+    from xspect2_amd.bank import bloom_parameters
+    from xspect2_amd.pipeline import reference_pipeline, run_pipeline
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect2_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
     half = args.docs // 2  # the genus filter holds half of the species: about half of the reads pass
     gsz = genomes[:half].size
     nb, nh = bloom_parameters(gsz - k + 1, 0.01)
@@ -197,7 +197,7 @@ def main():
     with FastxReader(fq) as rd:
         b = rd.next_batch(mb)
         h1, _ = bank.query(b.packed)
-    from xspect_amd.packing import pack_fixed
+    from xspect2_amd.packing import pack_fixed
     h2, _ = bank.query(pack_fixed(reads[: b.n]))
     res["first_batch_hits_equal"] = bool(np.array_equal(h1, h2))
     print(json.dumps(res))

@@ -1,4 +1,4 @@
-"""xspect_amd — MI355X-native k-mer x filter probe path for XspecT.
+"""xspect2_amd — MI355X-native k-mer x filter probe path for XspecT.
 
 Host side in Python (the reference's model surface), hot path in hand-written
 gfx950 HIP behind the C ABI of ``include/xspect_hip.h`` (libxspect_hip.so).

@@ -1,7 +1,7 @@
 """ctypes binding of libxspect_hip.so (include/xspect_hip.h).
 
-The library is built in-tree (``xspect_amd/libxspect_hip.so``) by
-``xspect_amd.build.build_library()``.  There is no CPU fallback: if the shared
+The library is built in-tree (``xspect2_amd/libxspect_hip.so``) by
+``xspect2_amd.build.build_library()``.  There is no CPU fallback: if the shared
 object is missing or cannot be loaded, importing this module raises.
 """
 from __future__ import annotations
@@ -130,7 +130,7 @@ def load() -> ctypes.CDLL:
             " (the probe path has no CPU fallback)")
     # torch (if present) must own the HIP runtime first: libamdhip64.so.7 is
     # then shared by soname instead of loading a second copy from /opt/rocm.
-    if os.environ.get("XSPECT_AMD_NO_TORCH_PRELOAD") is None:
+    if os.environ.get("XSPECT2_AMD_NO_TORCH_PRELOAD") is None:
         try:
             import torch  # noqa: F401
         except Exception:  # pragma: no cover - torch is optional for the ABI

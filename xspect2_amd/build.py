@@ -12,7 +12,7 @@ CSRC = PKG / "csrc"
 SO_PATH = PKG / "libxspect_hip.so"
 SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_json.cpp", CSRC / "xs_kernels.hip"]
 HEADERS = [CSRC / "xs_internal.h", ROOT / "include" / "xspect_hip.h"]
-ARCH = os.environ.get("XSPECT_AMD_ARCH", "gfx950")
+ARCH = os.environ.get("XSPECT2_AMD_ARCH", "gfx950")
 
 
 def hipcc() -> str:

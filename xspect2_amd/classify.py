@@ -110,7 +110,7 @@ def classify_pipeline(model_genus: str, input_path: Path, output_dir: Path | Non
                       mlst_scheme: str | None = None):
     """The full pipeline of ``xspect`` (``src/xspect/main.py:84-187`` all_pipeline):
     genus filter, species classification, MLST for A. baumannii, as one fused
-    GPU pass per input file (xspect_amd.pipeline).  ``mlst_scheme`` names the
+    GPU pass per input file (xspect2_amd.pipeline).  ``mlst_scheme`` names the
     abaumannii scheme (the reference takes the first one it has downloaded)."""
     from .pipeline import run_pipeline
     from .probabilistic_filter_model import ProbabilisticFilterModel

@@ -465,7 +465,7 @@ struct FastBank {
     uint32_t image_bytes;
 };
 
-// Row gather policies (XSPECT_AMD_LOADPOL): 0 global_load_dwordx4; buffer_load
+// Row gather policies (XSPECT2_AMD_LOADPOL): 0 global_load_dwordx4; buffer_load
 // with cache-policy aux 1: none, 2: nt, 3: sc1, 4: sc0 sc1 (L1 bypass forms).
 template <int POL>
 __device__ __forceinline__ uint4 load_row(const FastBank& fb, uint32_t off) {
@@ -1347,7 +1347,7 @@ static bool cobs_fast(const CobsView& bv, uint32_t k) {
 
 static int load_policy() {
     static const int pol = [] {  // thread-safe one-time init
-        const char* e = getenv("XSPECT_AMD_LOADPOL");
+        const char* e = getenv("XSPECT2_AMD_LOADPOL");
         const int v = e ? atoi(e) : 0;
         return (v < 0 || v > 4) ? 0 : v;
     }();
@@ -1533,10 +1533,10 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
     return launch_cobs_t<0, 0>(rv, bv, hits, partials, blocks, wpb, lds, dpad, s);
 }
 
-// Bits tested before the rest (XSPECT_AMD_BLOOM_SPLIT; 0 = all at once).
+// Bits tested before the rest (XSPECT2_AMD_BLOOM_SPLIT; 0 = all at once).
 static int bloom_split() {
     static const int v = [] {  // thread-safe one-time init
-        const char* e = getenv("XSPECT_AMD_BLOOM_SPLIT");
+        const char* e = getenv("XSPECT2_AMD_BLOOM_SPLIT");
         const int s = e ? atoi(e) : kBloomSplitDefault;
         return (s == 0 || s == 1 || s == 2 || s == 3) ? s : kBloomSplitDefault;
     }();

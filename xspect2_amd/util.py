@@ -25,8 +25,8 @@ def slugify(text: str) -> str:
 
 
 def default_device() -> int:
-    """GPU ordinal for banks: XSPECT_AMD_DEVICE, else LOCAL_RANK, else 0."""
-    for var in ("XSPECT_AMD_DEVICE", "LOCAL_RANK"):
+    """GPU ordinal for banks: XSPECT2_AMD_DEVICE, else LOCAL_RANK, else 0."""
+    for var in ("XSPECT2_AMD_DEVICE", "LOCAL_RANK"):
         v = os.environ.get(var)
         if v is not None and v.strip():
             return int(v)
