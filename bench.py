@@ -96,6 +96,8 @@ def parse():
     ap.add_argument("--hashes", type=int, default=7, help="species/multigenus: COBS num_hashes (default 7)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--totals-only", action="store_true",
+                    help="diagnostic: probe without writing the per-read hit matrix (totals only)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_traffic.json"))
     return ap.parse_args()
 
@@ -147,6 +149,8 @@ class Workload:
                 bank.build_device(g_dev, genomes.size, g_offs, args.docs, g_docs, stream=s)
                 self.config.update(signature_rows=sig, num_hashes=h, fpr=0.01)
                 self.rows_per_kmer = h
+                # a row costs the 128-B lines its padded device pitch spans (two at D > 1024)
+                self.row_bytes = max(ROW_BYTES, -(-bank.info.device_row_pitch // ROW_BYTES) * ROW_BYTES)
                 self.kernel = ("probe_cobs_fast<21,7>" if (self.k, h) == (21, 7) and args.docs <= 128
                                else f"probe_cobs (k={self.k}, h={h}, D={args.docs})")
             torch.cuda.synchronize(dev)
@@ -227,8 +231,8 @@ class Workload:
 
     def step(self):
         for b, h, t in zip(self.banks, self.d_hits, self.d_tot):
-            b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step, h, self.d_nk, t,
-                           stream=self.stream)
+            b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step,
+                           None if self.args.totals_only else h, self.d_nk, t, stream=self.stream)
         if self.world > 1:
             if self.args.workload == "multigenus":
                 all_gather(self.gathered, self.d_hits[0])  # docs sharded: hit vectors over xGMI

@@ -66,7 +66,9 @@ CLASSIC_CASES = [
     (200, 21, 7, [12_007]),   # wide kernel, 2 chunk lanes
     (500, 31, 1, [9_001]),    # wide kernel, 4 chunk lanes
     (700, 25, 5, [4_001]),    # wide kernel, 8 chunk lanes, general (k, h)
-    (2048, 31, 1, [9_001]),   # 16 chunks: widest slot kernel
+    (2048, 31, 1, [9_001]),   # wide kernel, 16 chunk lanes (rows of two lines)
+    (2000, 21, 7, [6_007]),   # wide kernel, 16 chunk lanes, species (k, h)
+    (1100, 16, 3, [3_011]),   # wide kernel, 9 data chunks of 16 lanes, general (k, h)
     (2100, 21, 7, [4_001]),   # 17 chunks: general kernel
 ]
 

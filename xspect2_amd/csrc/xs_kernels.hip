@@ -629,23 +629,22 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
                     uint64_t ro[HT ? HT : kMaxHashes];
 #pragma unroll
                     for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
-                        if (j < h) ro[j] = act ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
+                        if (j < h) ro[j] = gd.base + fastmod(act ? hv[j] : 0, gd.sig, gd.magic) * bv.pitch;
                     // kMaxChunks chunk loads of the group's h rows in flight, then count
                     const uint32_t nch_all = (uint32_t)min((uint64_t)bv.nchunks, (dlim - doc0 + 127) / 128);
                     for (uint32_t cb = 0; cb < nch_all; cb += kMaxChunks) {
                     const uint32_t nch = min(kMaxChunks, nch_all - cb);
+                    // unconditional loads (chunk 0 past the batch, row 0 without a
+                    // k-mer), masked afterwards, so they all stay in flight
                     uint4 mk[kMaxChunks];
 #pragma unroll
                     for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
-                        mk[cc] = make_uint4(0u, 0u, 0u, 0u);
-                        if (cc < nch && act) {
-                            uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
+                        const uint32_t co = cc < nch ? (cb + cc) * 16 : 0;
+                        uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
-                            for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
-                                if (j < h)
-                                    m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + (cb + cc) * 16));
-                            mk[cc] = m;
-                        }
+                        for (uint32_t j = 0; j < (HT ? HT : kMaxHashes); ++j)
+                            if (j < h) m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + ro[j] + co));
+                        mk[cc] = (cc < nch && act) ? m : make_uint4(0u, 0u, 0u, 0u);
                     }
 #pragma unroll
                     for (uint32_t cc = 0; cc < kMaxChunks; ++cc) {
@@ -694,9 +693,9 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 }
 
 // ------------------------------------------------------------------ COBS probe (wide classic rows)
-// Classic banks of 129..1024 docs: a row is C 16-byte chunks (C = 2, 4 or 8,
-// the next power of two of its data chunks; the pitch is padded so a row is
-// one 128-byte line at most).  Hashing stays one lane per k-mer, but the
+// Classic banks of 129..2048 docs: a row is C 16-byte chunks (C = 2, 4, 8 or
+// 16, the next power of two of its data chunks; the pitch is padded so a row
+// is one 128-byte line, or two aligned lines at C = 16).  Hashing stays one lane per k-mer, but the
 // gathers run C lanes per k-mer: in sub-tile s, lane l loads chunk l % C of
 // k-mer s * (64 / C) + l / C.  One load instruction then reads 64 / C whole
 // rows, so the vector L1 sees each row line once instead of once per chunk.
@@ -705,22 +704,17 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
 // per chunk.
 template <int C>
 struct ChunkLanes {  // bits r of a 32-row column with r % C == 0
-    static constexpr uint32_t m0 = C == 2 ? 0x55555555u : C == 4 ? 0x11111111u : 0x01010101u;
+    static constexpr uint32_t m0 = C == 2 ? 0x55555555u : C == 4 ? 0x11111111u : C == 8 ? 0x01010101u : 0x00010001u;
 };
 
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64);
-    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-    return ((uint64_t)hi << 32) | lo;
-}
-
-template <int KT, int HT, int C>
+template <int KT, int HT, int C, int P>
 __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv, CobsView bv,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials,
                                                                     uint32_t dpad) {
     constexpr int K = 64 / C;  // k-mers per sub-tile
     constexpr uint32_t M0 = ChunkLanes<C>::m0;
+    static_assert(C % P == 0, "sub-tiles in flight must divide the sub-tile count");
     extern __shared__ __attribute__((aligned(16))) uint64_t s_tot[];  // [dpad] per block
     __shared__ uint64_t s_kmers[kProbeThreads / kWave];
     const int lane = threadIdx.x & 63;
@@ -736,9 +730,12 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
     const uint32_t step = rv.step;
     const uint64_t D = bv.D;
     const uint32_t cpg = bv.nchunks;  // data chunks, <= C (host-checked)
-    const GroupDesc gd = bv.groups[0];
+    const GroupDesc gd = bv.groups[0];  // sig < 2^32 (host-checked): 32-bit row indices
+    const uint8_t* rows = bv.rows + gd.base;
+    const uint32_t pitch = bv.pitch;
     const int my_c = lane % C, my_slot = lane / C;
     const bool my_chunk_on = (uint32_t)my_c < cpg;
+    const uint32_t my_c_ofs = my_chunk_on ? (uint32_t)my_c * 16 : 0;
     const uint64_t U = rv.queue[0];
     uint64_t kmer_total = 0;
 
@@ -761,9 +758,9 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
 
             for (uint32_t tb = 0; tb < cnt; tb += 64) {
                 const bool act = tb + lane < cnt;
-                uint64_t ro[NH];
+                uint32_t ri[NH];  // row index of hash j
 #pragma unroll
-                for (int j = 0; j < NH; ++j) ro[j] = 0;
+                for (int j = 0; j < NH; ++j) ri[j] = 0;
                 if (act) {
                     Kmer c;
                     kmer_at<KT, kKmerCobs>(rv, o0, len, (t0 + tb + lane) * step, k, c);
@@ -772,30 +769,46 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
 #pragma unroll
                     for (int j = 0; j < NH; ++j)
                         if ((uint32_t)j < h)
-                            ro[j] = gd.base + fastmod(xxh64_seed<KT>(c, pre, k, (uint64_t)j), gd.sig, gd.magic) * bv.pitch;
+                            ri[j] = (uint32_t)fastmod(xxh64_seed<KT>(c, pre, k, (uint64_t)j), gd.sig, gd.magic);
                 }
                 const uint32_t tile = min(64u, cnt - tb);
 #pragma unroll
-                for (int s = 0; s < C; ++s) {
-                    if ((uint32_t)(s * K) >= tile) continue;  // uniform
-                    const int src = s * K + my_slot;
-                    const bool on = (uint32_t)src < tile && my_chunk_on;
-                    uint64_t o[NH];
+                for (int s0 = 0; s0 < C; s0 += P) {
+                    if ((uint32_t)(s0 * K) >= tile) continue;  // uniform
+                    // P sub-tiles' row chunks in flight before any counting.  The
+                    // loads are unconditional (a lane without a k-mer has row 0,
+                    // a lane past the data chunks reads chunk 0) and masked
+                    // afterwards: a load under a divergent branch would be
+                    // waited for before the branch joins, one row at a time.
+                    uint4 mm[P];
 #pragma unroll
-                    for (int j = 0; j < NH; ++j) o[j] = (uint32_t)j < h ? shfl64(ro[j], src) : 0;
-                    uint4 m = on ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0u, 0u, 0u, 0u);
+                    for (int p = 0; p < P; ++p) {
+                        const int src = (s0 + p) * K + my_slot;
+                        const bool on = (uint32_t)src < tile && my_chunk_on;
+                        uint4 v[NH];
 #pragma unroll
-                    for (int j = 0; j < NH; ++j)
-                        if ((uint32_t)j < h && on)
-                            m = and4(m, *reinterpret_cast<const uint4*>(bv.rows + o[j] + my_c * 16));
-                    const uint32_t w[4] = {m.x, m.y, m.z, m.w};
+                        for (int j = 0; j < NH; ++j) {
+                            if ((uint32_t)j >= h) continue;
+                            const uint32_t rj = (uint32_t)__shfl((int)ri[j], src, 64);
+                            v[j] = *reinterpret_cast<const uint4*>(rows + (uint64_t)rj * pitch + my_c_ofs);
+                        }
+                        uint4 m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (__ballot(w[q] != 0u) == 0ull) continue;
-                        const uint32_t x = xpose32(w[q], X);
+                        for (int j = 0; j < NH; ++j)
+                            if ((uint32_t)j < h) m = and4(m, v[j]);
+                        mm[p] = on ? m : make_uint4(0u, 0u, 0u, 0u);
+                    }
 #pragma unroll
-                        for (int cc = 0; cc < C; ++cc)
-                            acc[2 * cc + (q >> 1)] += (uint32_t)__popc(x & (M0 << cc)) << (16 * (q & 1));
+                    for (int p = 0; p < P; ++p) {
+                        const uint32_t w[4] = {mm[p].x, mm[p].y, mm[p].z, mm[p].w};
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            if (__ballot(w[q] != 0u) == 0ull) continue;
+                            const uint32_t x = xpose32(w[q], X);
+#pragma unroll
+                            for (int cc = 0; cc < C; ++cc)
+                                acc[2 * cc + (q >> 1)] += (uint32_t)__popc(x & (M0 << cc)) << (16 * (q & 1));
+                        }
                     }
                 }
             }
@@ -837,8 +850,8 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv,
 
 // ------------------------------------------------------------------ COBS probe (slots)
 // Banks whose rows span at most GM groups x CM 16-byte chunks (classic
-// D <= 16*128 as GM = 1; compact schemes such as an MLST locus: 3 groups x 4
-// chunks).  The layout is compile-time, so every slot's group and chunk is a
+// rows the fast and wide kernels do not take, as GM = 1; compact schemes such
+// as an MLST locus: 3 groups x 4 chunks).  The layout is compile-time, so every slot's group and chunk is a
 // constant; runtime guards only switch slots off.  Every chunk of every
 // group's h rows is in flight before any counting; per-doc counts of the unit
 // live in registers, two 16-bit counters per VGPR (a unit has <= 256 k-mers,
@@ -852,9 +865,13 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
     constexpr int NS = GM * CM;
     extern __shared__ __attribute__((aligned(16))) uint64_t s_tot[];  // [dpad] per block
     __shared__ uint64_t s_kmers[kProbeThreads / kWave];
+    // group descriptors staged once in LDS (slots past G alias group 0): their
+    // reads wait on lgkmcnt, never behind the row loads' vmcnt
+    __shared__ GroupDesc s_gd[GM];
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     for (uint32_t d = threadIdx.x; d < dpad; d += blockDim.x) s_tot[d] = 0;
+    if (threadIdx.x < GM) s_gd[threadIdx.x] = bv.groups[threadIdx.x < bv.G ? threadIdx.x : 0];
     __syncthreads();
     Xpose X;
     xpose_init(lane, X);
@@ -867,6 +884,9 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
     const uint32_t G = bv.G;               // <= GM (host-checked)
     const uint32_t cpg = bv.nchunks;       // <= CM (host-checked)
     const uint64_t gdocs = 8 * bv.page;    // docs per group
+    uint32_t cofs[CM];                     // byte offset of chunk cc (0 past the data chunks)
+#pragma unroll
+    for (int cc = 0; cc < CM; ++cc) cofs[cc] = (uint32_t)cc < cpg ? cc * 16 : 0;
     const uint64_t U = rv.queue[0];
     uint64_t kmer_total = 0;
 
@@ -901,34 +921,34 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_slots(ReadView rv
                     for (int j = 0; j < NH; ++j)
                         if ((uint32_t)j < h) hv[j] = xxh64_seed<KT>(c, pre, k, (uint64_t)j);
                 }
+                // Every row load is unconditional: a lane without a k-mer has
+                // hash 0 (a valid row), a chunk past the data reads chunk 0, a
+                // group past G reads group 0; results are masked afterwards.  A
+                // load under a divergent branch would be waited for at the join.
                 uint4 mk[NS];
 #pragma unroll
                 for (int g = 0; g < GM; ++g) {
+                    const GroupDesc gd = s_gd[g];
                     uint64_t ro[NH];
 #pragma unroll
-                    for (int j = 0; j < NH; ++j) ro[j] = 0;
-                    if ((uint32_t)g < G) {
-                        const GroupDesc gd = bv.groups[g];
-#pragma unroll
-                        for (int j = 0; j < NH; ++j)
-                            if ((uint32_t)j < h) ro[j] = gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch;
-                    }
+                    for (int j = 0; j < NH; ++j)
+                        ro[j] = (uint32_t)j < h ? gd.base + fastmod(hv[j], gd.sig, gd.magic) * bv.pitch : 0;
                     // row-major issue order: the chunks of one row leave back to back,
                     // so the vector L1 sees one row line in consecutive requests
-                    const bool on = (uint32_t)g < G && act;
 #pragma unroll
-                    for (int cc = 0; cc < CM; ++cc)
-                        mk[g * CM + cc] = (on && (uint32_t)cc < cpg) ? make_uint4(~0u, ~0u, ~0u, ~0u)
-                                                                     : make_uint4(0u, 0u, 0u, 0u);
+                    for (int cc = 0; cc < CM; ++cc) mk[g * CM + cc] = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                     for (int j = 0; j < NH; ++j) {
                         if ((uint32_t)j >= h) continue;
 #pragma unroll
                         for (int cc = 0; cc < CM; ++cc)
-                            if (on && (uint32_t)cc < cpg)
-                                mk[g * CM + cc] = and4(mk[g * CM + cc],
-                                                       *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cc * 16));
+                            mk[g * CM + cc] = and4(mk[g * CM + cc],
+                                                   *reinterpret_cast<const uint4*>(bv.rows + ro[j] + cofs[cc]));
                     }
+                    const bool on = (uint32_t)g < G && act;
+#pragma unroll
+                    for (int cc = 0; cc < CM; ++cc)
+                        if (!(on && (uint32_t)cc < cpg)) mk[g * CM + cc] = make_uint4(0u, 0u, 0u, 0u);
                 }
 #pragma unroll
                 for (int g = 0; g < GM; ++g) {
@@ -1387,34 +1407,39 @@ static hipError_t launch_cobs_t(const ReadView& rv, const CobsView& bv, uint32_t
     return hipGetLastError();
 }
 
-// Wide kernel chunk lanes for a classic bank of 2..8 data chunks (0: none).
+// Wide kernel chunk lanes for a classic bank of 2..16 data chunks (0: none).
 static int wide_for(const CobsView& bv) {
-    if (bv.G != 1 || bv.nchunks < 2 || bv.nchunks > 8) return 0;
-    return bv.nchunks == 2 ? 2 : bv.nchunks <= 4 ? 4 : 8;
+    if (bv.G != 1 || bv.nchunks < 2 || bv.nchunks > 16 || bv.sig0 >= (1ull << 32)) return 0;
+    return bv.nchunks == 2 ? 2 : bv.nchunks <= 4 ? 4 : bv.nchunks <= 8 ? 8 : 16;
 }
 
 using WideFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*, uint32_t);
 
+// Two sub-tiles' row loads are issued before counting: measured against one
+// and four at D = 200 / 600 / 1000 / 2000 (profiles/r01_wide16.txt).
+constexpr int kWideInFlight = 2;
+
 template <int KT, int HT>
 static WideFn wide_fn(int c) {
-    return c == 2 ? probe_cobs_wide<KT, HT, 2> : c == 4 ? probe_cobs_wide<KT, HT, 4> : probe_cobs_wide<KT, HT, 8>;
+    constexpr int P = kWideInFlight;
+    return c == 2 ? probe_cobs_wide<KT, HT, 2, P> : c == 4 ? probe_cobs_wide<KT, HT, 4, P>
+         : c == 8 ? probe_cobs_wide<KT, HT, 8, P> : probe_cobs_wide<KT, HT, 16, P>;
 }
 
 static WideFn pick_wide(uint32_t k, uint32_t h, int c);
 
-// Slot kernel shape (GM groups x CM chunks) for a bank, or {0, 0} when its
-// rows span more than 16 chunks (general kernel).  D <= 16 * 128 follows, so
-// the LDS totals need <= 16 KB.
+// Slot kernel shape (GM groups x CM chunks) for a bank, or {0, 0} for the
+// general kernel: classic rows of more than 8 chunks that the wide kernel does
+// not take, compact rows of more than 16 slots.  D <= 16 * 128 follows, so the
+// LDS totals need <= 16 KB.
 struct SlotShape {
     int gm, cm;
 };
 static SlotShape slots_for(const CobsView& bv) {
     const uint64_t G = bv.G, c = bv.nchunks;
-    if (G == 1) {
+    if (G == 1) {  // classic rows of 2..16 chunks take the wide kernel first
         if (c <= 4) return {1, 4};
         if (c <= 8) return {1, 8};
-        if (c <= 12) return {1, 12};
-        if (c <= 16) return {1, 16};
         return {0, 0};
     }
     if (c == 1) return G <= 4 ? SlotShape{4, 1} : G <= 8 ? SlotShape{8, 1} : G <= 16 ? SlotShape{16, 1} : SlotShape{0, 0};
@@ -1427,12 +1452,7 @@ using SlotsFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*, uint32_t);
 
 template <int KT, int HT>
 static SlotsFn slots_fn_classic(SlotShape s) {
-    switch (s.cm) {
-        case 4: return probe_cobs_slots<KT, HT, 1, 4>;
-        case 8: return probe_cobs_slots<KT, HT, 1, 8>;
-        case 12: return probe_cobs_slots<KT, HT, 1, 12>;
-        default: return probe_cobs_slots<KT, HT, 1, 16>;
-    }
+    return s.cm == 4 ? probe_cobs_slots<KT, HT, 1, 4> : probe_cobs_slots<KT, HT, 1, 8>;
 }
 
 template <int KT, int HT>
@@ -1464,8 +1484,8 @@ static WideFn pick_wide(uint32_t k, uint32_t h, int c) {
 }
 
 static int shape_index(SlotShape s) {  // 0..12, for the grid cache
-    static const int gms[13] = {1, 1, 1, 1, 4, 8, 16, 4, 8, 2, 3, 4, 0};
-    static const int cms[13] = {4, 8, 12, 16, 1, 1, 1, 2, 2, 4, 4, 4, 0};
+    static const int gms[13] = {1, 1, 0, 0, 4, 8, 16, 4, 8, 2, 3, 4, 0};
+    static const int cms[13] = {4, 8, 0, 0, 1, 1, 1, 2, 2, 4, 4, 4, 0};
     for (int i = 0; i < 12; ++i)
         if (gms[i] == s.gm && cms[i] == s.cm) return i;
     return 12;
@@ -1476,14 +1496,14 @@ static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
-    static std::atomic<int> fast21{0}, fast31{0}, generic[3], slots[3][13], wide[3][3];
+    static std::atomic<int> fast21{0}, fast31{0}, generic[3], slots[3][13], wide[3][4];
     if (cobs_fast(bv, k)) {
         if (k == 21) return cached_grid(fast21, [] { return resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0); });
         return cached_grid(fast31, [] { return resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0); });
     }
     if (const int c = wide_for(bv)) {
-        return cached_grid(wide[kh_variant(k, bv.h)][c == 2 ? 0 : c == 4 ? 1 : 2],
-                           [&] { return resident_grid(pick_wide(k, bv.h, c), kProbeThreads, 8192); });
+        return cached_grid(wide[kh_variant(k, bv.h)][c == 2 ? 0 : c == 4 ? 1 : c == 8 ? 2 : 3],
+                           [&] { return resident_grid(pick_wide(k, bv.h, c), kProbeThreads, 16 * c * 64); });
     }
     const SlotShape sh = slots_for(bv);
     if (sh.gm) {
