@@ -124,7 +124,13 @@ def load() -> ctypes.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    if not SO_PATH.exists():
+    path = SO_PATH
+    variant = os.environ.get("XSPECT2_AMD_LIB_VARIANT")  # A/B runs: libxspect_hip.<variant>.so in-tree
+    if variant:
+        path = SO_PATH.with_name(f"libxspect_hip.{variant}.so")
+        if not path.exists():
+            raise ImportError(f"{path} is missing")
+    if not path.exists():
         raise ImportError(
             f"{SO_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the probe path has no CPU fallback)")
@@ -135,7 +141,7 @@ def load() -> ctypes.CDLL:
             import torch  # noqa: F401
         except Exception:  # pragma: no cover - torch is optional for the ABI
             pass
-    lib = ctypes.CDLL(str(SO_PATH))
+    lib = ctypes.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
