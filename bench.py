@@ -151,8 +151,14 @@ class Workload:
                 self.rows_per_kmer = h
                 # a row costs the 128-B lines its padded device pitch spans (two at D > 1024)
                 self.row_bytes = max(ROW_BYTES, -(-bank.info.device_row_pitch // ROW_BYTES) * ROW_BYTES)
-                self.kernel = ("probe_cobs_fast<21,7>" if (self.k, h) == (21, 7) and args.docs <= 128
-                               else f"probe_cobs (k={self.k}, h={h}, D={args.docs})")
+                nch = -(-args.docs // 128)  # 16-byte chunks of a row
+                if (self.k, h) in ((21, 7), (31, 1)) and args.docs <= 128:
+                    self.kernel = f"probe_cobs_fast<{self.k},{h}>"
+                elif 2 <= nch <= 16:
+                    lanes = 2 if nch == 2 else 4 if nch <= 4 else 8 if nch <= 8 else 16
+                    self.kernel = f"probe_cobs_wide<k={self.k},h={h},C={lanes}> (D={args.docs})"
+                else:
+                    self.kernel = f"probe_cobs (k={self.k}, h={h}, D={args.docs})"
             torch.cuda.synchronize(dev)
             del g_dev
             self.banks = [bank]
@@ -162,7 +168,7 @@ class Workload:
         else:  # mlst
             reads, loci_info = self._mlst(args, dev, s)
             self.config.update(loci=len(self.banks), **loci_info)
-            self.kernel = "probe_cobs_slots<31,1,3,4> (compact, 3 groups x 4 chunks)"
+            self.kernel = "probe_cobs_wide<31,1,C=4,P=2,G=3> (compact, 3 groups x 4 chunk lanes)"
         self.reads = reads
         self.n = reads.shape[0]
         self.seq_bytes = reads.size

@@ -95,7 +95,8 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
 
 @pytest.mark.parametrize("D,k,h,page,G", [(600, 31, 1, 64, 2), (20, 21, 7, 1, 3), (1500, 21, 2, 64, 3),
                                           (70, 25, 3, 3, 3), (2600, 31, 1, 64, 6), (1430, 31, 1, 64, 3),
-                                          (600, 31, 1, 32, 3), (100, 21, 3, 2, 7), (2000, 31, 1, 64, 4)])
+                                          (600, 31, 1, 32, 3), (100, 21, 3, 2, 7), (2000, 31, 1, 64, 4),
+                                          (700, 31, 1, 40, 3), (500, 21, 7, 48, 2)])
 def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
     assert (G - 1) * 8 * page < D <= G * 8 * page
     rng = np.random.default_rng(D)

@@ -165,6 +165,8 @@ struct xs_bank {
         v.page = page;
         v.D = D;
         v.sig0 = sig.empty() ? 0 : sig[0];
+        v.sig_max = 0;
+        for (auto x : sig) v.sig_max = x > v.sig_max ? x : v.sig_max;
         return v;
     }
     BloomView bloom_view() const {

@@ -41,6 +41,7 @@ struct CobsView {
     uint64_t page;            // file bytes per row (docs per group = 8*page)
     uint64_t D;
     uint64_t sig0;            // host copy of groups[0].sig (fast-path selection)
+    uint64_t sig_max;         // host copy of the largest group sig (32-bit row index paths)
 };
 
 struct BloomView {
