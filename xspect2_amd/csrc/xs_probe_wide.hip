@@ -21,8 +21,14 @@ struct ChunkLanes {  // bits r of a 32-row column with r % C == 0
     static constexpr uint32_t m0 = C == 2 ? 0x55555555u : C == 4 ? 0x11111111u : C == 8 ? 0x01010101u : 0x00010001u;
 };
 
+// Min blocks per CU = waves per SIMD the register budget is sized for.  4/5/6
+// force spills and run slower on every workload (profiles/r01_wide_occupancy.txt);
+// overridable for A/B builds (tools/build_variant.sh).
+#ifndef XS_WIDE_MIN_BLOCKS
+#define XS_WIDE_MIN_BLOCKS 2
+#endif
 template <int KT, int HT, int C, int P, int GM>
-__global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_wide(ReadView rv, CobsView bv,
+__global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_wide(ReadView rv, CobsView bv,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials,
                                                                     uint32_t dpad) {
