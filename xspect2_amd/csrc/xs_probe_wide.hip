@@ -139,6 +139,10 @@ __global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_
                             const uint32_t w[4] = {mm[p][g].x, mm[p][g].y, mm[p][g].z, mm[p][g].w};
 #pragma unroll
                             for (int q = 0; q < 4; ++q) {
+#ifdef XS_WIDE_NOCOUNT  // measurement-only build: loads consumed, counting skipped (wrong hits)
+                                acc[g][q] ^= w[q];
+                                continue;
+#endif
                                 if (__ballot(w[q] != 0u) == 0ull) continue;
                                 const uint32_t x = xpose32(w[q], X);
 #pragma unroll
