@@ -94,6 +94,8 @@ def parse():
                     help="genus: build the filter from this fraction of the genomes (reads come from all)")
     ap.add_argument("--k", type=int, default=None, help="species/multigenus: k-mer length (default 21)")
     ap.add_argument("--hashes", type=int, default=7, help="species/multigenus: COBS num_hashes (default 7)")
+    ap.add_argument("--mlst-foreign", type=float, default=0.0,
+                    help="mlst: fraction of reads from outside every locus (WGS-like input: ~1.0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--totals-only", action="store_true",
@@ -225,6 +227,9 @@ class Workload:
             a = all_alleles[li[i]][ai[i]]
             st = int(rng.integers(0, a.size - args.read_len + 1))
             reads[i] = a[st:st + args.read_len]
+        if args.mlst_foreign > 0:  # reads from elsewhere in the genome: random sequence
+            nf = int(round(args.mlst_foreign * n))
+            reads[:nf] = acgt[rng.integers(0, 4, (nf, args.read_len))]
         self.rows_per_kmer = sum(len(g) for g in group_rows)  # one 64-B row per group per locus
         # a locus bank (~97 MB) stays in the 256 MB Infinity Cache: count the
         # row itself (page bytes), not an HBM line fill
@@ -232,6 +237,7 @@ class Workload:
         self.roofline_note = ("locus banks (~97 MB each) are Infinity-Cache resident: rows arrive as 128-B "
                               "line fills from the MALL, not HBM; achieved counts the 64-B rows themselves")
         return reads, {"alleles_per_locus": n_alleles, "page_size": page, "k": self.k,
+                       "foreign_read_frac": args.mlst_foreign,
                        "num_hashes": 1, "fpr": 0.001,
                        "signature_rows": int(sum(sum(g) for g in group_rows))}
 
