@@ -334,3 +334,43 @@ def test_concurrent_handles_from_threads(xs, oracle_mod):
             assert np.array_equal(got, want[key]), key
     for _, gb, _, _ in pairs:
         gb.close()
+
+
+def test_host_batches_staged_in_chunks(xs, oracle_mod):
+    """Host batches larger than one staging chunk (8 MiB first, then 32 MiB)
+    are copied and probed chunk by chunk, and their hit rows come back through
+    the D2H ring per chunk: hits, k-mer counts, totals and per-read best doc
+    must equal the oracle's across every chunk seam, including a read longer
+    than a whole staging slot and empty reads at the seams."""
+    from xspect2_amd.packing import PackedReads
+
+    ob, gb, _, _ = _pair(xs, oracle_mod, 100, 21, 7, [40_000], seed=5)
+    rng = np.random.default_rng(77)
+    n = 260_000  # 150-180 bp: ~43 MB, 3 chunks; the second chunk's hit rows (> 64 MB) take the ring
+    lens = rng.integers(150, 181, n).astype(np.uint64)
+    lens[rng.integers(0, n, 50)] = 0
+    offs = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs[1:])
+    buf = np.frombuffer(b"ACGTN", dtype=np.uint8)[rng.integers(0, 5, int(offs[-1]) + 1)]
+    pr = PackedReads(buf, offs)
+    want_h, want_n = ob.query_packed(buf, offs)
+    got_h, got_n = gb.query(pr)
+    assert np.array_equal(got_n, want_n) and np.array_equal(got_h, want_h)
+    tot, nk = gb.query_totals(pr)
+    assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+    best, bh, bnk, btot = gb.query_best(pr, want_totals=True)
+    assert np.array_equal(bh, want_h.max(axis=1)) and np.array_equal(bnk, want_n)
+    assert np.array_equal(btot[:100], tot) and int(btot[100]) == nk
+    gb.close()
+
+    # one read longer than a staging slot, between short ones, on a small bank
+    ob, gb, _, _ = _pair(xs, oracle_mod, 8, 21, 7, [5_000], seed=6)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    seqs = [acgt[rng.integers(0, 4, 200)].tobytes() for _ in range(3)]
+    seqs += [acgt[rng.integers(0, 4, 34_000_000)].tobytes()] + seqs
+    want_h, want_n = ob.query(seqs)
+    got_h, got_n = gb.query(seqs)
+    assert np.array_equal(got_n, want_n) and np.array_equal(got_h, want_h)
+    tot, nk = gb.query_totals(seqs)
+    assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+    gb.close()

@@ -22,6 +22,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -142,6 +143,10 @@ struct xs_bank {
     DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
     PinnedBuf stage[2];             // D2H staging ring for large host outputs
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    PinnedBuf hstage[2];            // H2D staging ring for host read batches
+    hipEvent_t hstage_ev[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr, d2h_stream = nullptr;
+    std::vector<hipEvent_t> chunk_ev;  // probe of batch chunk i done
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -505,11 +510,11 @@ int stage_host_reads(xs_bank* b, const char* seqs, const uint64_t* offsets, uint
 }
 
 // Device -> pageable host copy of `bytes`, ordered after the work already on
-// the bank stream.  Large copies go through a pinned two-slot ring: the DMA of
+// stream `st`.  Large copies go through a pinned two-slot ring: the DMA of
 // chunk i overlaps the host copy of chunk i-1 (a plain pageable D2H runs at
 // about 9 GB/s on the box, a pinned one at PCIe rate).  Returns once the data
 // is in `host`.
-int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes) {
+int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes, hipStream_t st) {
     constexpr size_t kChunk = 32u << 20;
     bool pinned = false;
     if (bytes >= 2 * kChunk) {
@@ -518,8 +523,8 @@ int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes) {
         else (void)hipGetLastError();  // pageable memory is "not a HIP pointer"
     }
     if (bytes < 2 * kChunk || pinned) {
-        HIPCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, b->stream));
-        HIPCHK(hipStreamSynchronize(b->stream));
+        HIPCHK(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
         return XS_OK;
     }
     for (int s = 0; s < 2; ++s) {
@@ -534,8 +539,8 @@ int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes) {
         const int slot = (int)(i & 1);
         const size_t n = std::min(kChunk, bytes - off);
         HIPCHK(hipMemcpyAsync(b->stage[slot].p, static_cast<const char*>(dev) + off, n, hipMemcpyDeviceToHost,
-                              b->stream));
-        HIPCHK(hipEventRecord(b->stage_ev[slot], b->stream));
+                              st));
+        HIPCHK(hipEventRecord(b->stage_ev[slot], st));
         if (prev_slot >= 0) {
             HIPCHK(hipEventSynchronize(b->stage_ev[prev_slot]));
             par_memcpy(static_cast<char*>(host) + prev_off, b->stage[prev_slot].p, prev_n, threads);
@@ -546,6 +551,114 @@ int d2h_pageable(xs_bank* b, void* host, const void* dev, size_t bytes) {
     }
     HIPCHK(hipEventSynchronize(b->stage_ev[prev_slot]));
     par_memcpy(static_cast<char*>(host) + prev_off, b->stage[prev_slot].p, prev_n, threads);
+    return XS_OK;
+}
+
+// ---- host batches: staging overlapped with the probe --------------------------
+// A host batch is cut at read boundaries into chunks of about kHostChunk
+// sequence bytes (the first smaller, so the probe starts early).  Chunk i is
+// copied into a pinned slot by host threads and sent on the copy stream while
+// the bank stream probes chunk i-1.  With host hits wanted, chunk i-1's hit
+// rows go back through the D2H ring on a third stream while chunk i is probed.
+// Device buffers span the whole batch, so chunks never overwrite each other's
+// reads or hits, and the workspace is sized for the whole batch up front (no
+// reallocation, hence no implicit device sync, between chunks).
+constexpr size_t kHostChunk = 32u << 20;
+constexpr size_t kHostFirst = 8u << 20;
+
+int host_threads() {
+    const unsigned hw = std::thread::hardware_concurrency();
+    return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
+}
+
+// hits_host: n x cols rows back on the host (needs d_hits); tot_host: cols + 1
+// entries (per-doc sums, then the k-mer total).
+int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+               uint32_t* d_hits, uint32_t* hits_host, uint64_t* d_nk, uint64_t* tot_host) {
+    const uint64_t base = offsets[0];
+    for (uint64_t r = 0; r < n; ++r)
+        if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    const uint64_t bytes = offsets[n] - base;
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    const uint64_t pcols = cols + 1;
+    std::vector<uint64_t> cut{0};
+    for (size_t limit = kHostFirst; cut.back() < n; limit = kHostChunk) {
+        const uint64_t r0 = cut.back();
+        uint64_t e = (uint64_t)(std::upper_bound(offsets + r0 + 1, offsets + n + 1, offsets[r0] + limit) - offsets) - 1;
+        cut.push_back(e > r0 ? e : r0 + 1);  // a read over the limit is a chunk of its own
+    }
+    const size_t nc = cut.size() - 1;
+    if (int rc = b->seqs.ensure(bytes + kPad)) return rc;
+    if (int rc = b->offs.ensure((n + 1) * 8)) return rc;
+    if (int rc = b->nseg.ensure((n + 1) * 8)) return rc;
+    if (int rc = b->unit_ofs.ensure((n + 1) * 8)) return rc;
+    if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
+    if (int rc = b->unit_read.ensure((n + bytes / kSegKmers + 1) * 4)) return rc;
+    if (int rc = b->scan_tmp.ensure(scan_temp_bytes(n))) return rc;
+    if (int rc = b->partials.ensure((size_t)probe_grid(b) * pcols * 8)) return rc;
+    if (tot_host)
+        if (int rc = b->totals.ensure(nc * pcols * 8)) return rc;
+    for (int s = 0; s < 2; ++s) {
+        if (int rc = b->hstage[s].ensure(kHostChunk)) return rc;
+        if (!b->hstage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b->hstage_ev[s], hipEventDisableTiming));
+    }
+    if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
+    if (hits_host && !b->d2h_stream) HIPCHK(hipStreamCreateWithFlags(&b->d2h_stream, hipStreamNonBlocking));
+    while (hits_host && b->chunk_ev.size() < nc) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        b->chunk_ev.push_back(e);
+    }
+    uint8_t* d_seqs = b->seqs.as<uint8_t>();
+    uint64_t* d_offs = b->offs.as<uint64_t>();
+    std::vector<uint64_t> rebased(n + 1);
+    for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
+    HIPCHK(hipMemcpyAsync(d_offs, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
+    const int threads = host_threads();
+    auto drain = [&](size_t j) -> int {  // chunk j's hit rows to the host
+        const uint64_t r0 = cut[j], m = cut[j + 1] - cut[j];
+        HIPCHK(hipStreamWaitEvent(b->d2h_stream, b->chunk_ev[j], 0));
+        return d2h_pageable(b, hits_host + r0 * cols, d_hits + r0 * cols, m * cols * 4, b->d2h_stream);
+    };
+    bool used[2] = {false, false};
+    for (size_t i = 0; i < nc; ++i) {
+        const uint64_t r0 = cut[i], r1 = cut[i + 1];
+        const uint64_t o0 = offsets[r0] - base, o1 = offsets[r1] - base, nb = o1 - o0;
+        const int slot = (int)(i & 1);
+        if (used[slot]) HIPCHK(hipEventSynchronize(b->hstage_ev[slot]));  // the slot's last H2D is done
+        if (nb && nb <= kHostChunk) {
+            par_memcpy(b->hstage[slot].p, seqs + base + o0, nb, threads);
+            HIPCHK(hipMemcpyAsync(d_seqs + o0, b->hstage[slot].p, nb, hipMemcpyHostToDevice, b->copy_stream));
+        } else if (nb) {  // one read larger than a slot
+            HIPCHK(hipMemcpyAsync(d_seqs + o0, seqs + base + o0, nb, hipMemcpyHostToDevice, b->copy_stream));
+        }
+        HIPCHK(hipEventRecord(b->hstage_ev[slot], b->copy_stream));
+        used[slot] = true;
+        HIPCHK(hipStreamWaitEvent(b->stream, b->hstage_ev[slot], 0));
+        const Inputs in{d_seqs, o1, d_offs + r0, r1 - r0};
+        if (int rc = run_query(b, in, step, d_hits ? d_hits + r0 * cols : nullptr, d_nk ? d_nk + r0 : nullptr,
+                               tot_host ? b->totals.as<uint64_t>() + i * pcols : nullptr, b->stream))
+            return rc;
+        if (hits_host) {
+            HIPCHK(hipEventRecord(b->chunk_ev[i], b->stream));
+            if (i > 0)
+                if (int rc = drain(i - 1)) return rc;
+        }
+    }
+    if (hits_host)
+        if (int rc = drain(nc - 1)) return rc;
+    if (tot_host) {
+        std::vector<uint64_t> t(nc * pcols);
+        HIPCHK(hipMemcpyAsync(t.data(), b->totals.p, t.size() * 8, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        for (uint64_t c = 0; c < pcols; ++c) {
+            uint64_t v = 0;
+            for (size_t i = 0; i < nc; ++i) v += t[i * pcols + c];
+            tot_host[c] = v;
+        }
+    }
+    HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
+    if (hits_host) HIPCHK(hipStreamSynchronize(b->d2h_stream));
     return XS_OK;
 }
 
@@ -800,8 +913,6 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
     std::lock_guard<std::mutex> lk(b->mu);
     HIPCHK(hipSetDevice(b->device));
     if (n == 0) return XS_OK;
-    Inputs in;
-    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     uint32_t* d_hits = nullptr;
     uint64_t* d_nk = nullptr;
@@ -813,9 +924,7 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
         if (int rc = b->nk.ensure(n * 8)) return rc;
         d_nk = b->nk.as<uint64_t>();
     }
-    if (int rc = run_query(b, in, step, d_hits, d_nk, nullptr, b->stream)) return rc;
-    if (hits_out)
-        if (int rc = d2h_pageable(b, hits_out, d_hits, n * cols * 4)) return rc;
+    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, hits_out, d_nk, nullptr)) return rc;
     if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
@@ -831,26 +940,23 @@ int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_
         if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
         return XS_OK;
     }
-    Inputs in;
-    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
     if (int rc = b->hits.ensure(n * cols * 4)) return rc;
     if (int rc = b->nk.ensure(n * 8)) return rc;
     if (int rc = b->best.ensure(n * 8)) return rc;
-    if (totals_out) {
-        if (int rc = b->totals.ensure((cols + 1) * 8)) return rc;
-    }
     uint32_t* d_hits = b->hits.as<uint32_t>();
     uint32_t* d_best = b->best.as<uint32_t>();
     uint32_t* d_bhits = d_best + n;
-    uint64_t* d_tot = totals_out ? b->totals.as<uint64_t>() : nullptr;
-    if (int rc = run_query(b, in, step, d_hits, b->nk.as<uint64_t>(), d_tot, b->stream)) return rc;
+    std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
+    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, b->nk.as<uint64_t>(),
+                            totals_out ? tot.data() : nullptr))
+        return rc;
     HIPCHK(launch_best_doc(d_hits, n, cols, d_best, d_bhits, b->stream));
     HIPCHK(hipMemcpyAsync(best_doc, d_best, n * 4, hipMemcpyDeviceToHost, b->stream));
     if (best_hits) HIPCHK(hipMemcpyAsync(best_hits, d_bhits, n * 4, hipMemcpyDeviceToHost, b->stream));
     if (num_kmers_out)
         HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
-    if (totals_out) HIPCHK(hipMemcpyAsync(totals_out, d_tot, (cols + 1) * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
+    if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
     return XS_OK;
 }
 
@@ -882,13 +988,8 @@ int xs_query_totals(xs_bank* b, const char* seqs, const uint64_t* offsets, uint6
         if (total_kmers_out) *total_kmers_out = 0;
         return XS_OK;
     }
-    Inputs in;
-    if (int rc = stage_host_reads(b, seqs, offsets, n, &in)) return rc;
-    if (int rc = b->totals.ensure((cols + 1) * 8)) return rc;
-    if (int rc = run_query(b, in, step, nullptr, nullptr, b->totals.as<uint64_t>(), b->stream)) return rc;
     std::vector<uint64_t> t(cols + 1);
-    HIPCHK(hipMemcpyAsync(t.data(), b->totals.p, (cols + 1) * 8, hipMemcpyDeviceToHost, b->stream));
-    HIPCHK(hipStreamSynchronize(b->stream));
+    if (int rc = query_host(b, seqs, offsets, n, step, nullptr, nullptr, nullptr, t.data())) return rc;
     memcpy(totals_out, t.data(), cols * 8);
     if (total_kmers_out) *total_kmers_out = t[cols];
     return XS_OK;
@@ -997,13 +1098,19 @@ void xs_bank_close(xs_bank* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
+    for (hipStream_t st : {b->copy_stream, b->d2h_stream})
+        if (st) (void)hipStreamSynchronize(st);
     for (auto& ev : b->stage_ev)
         if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : b->hstage_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    for (auto& ev : b->chunk_ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->events) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
-    if (b->stream) (void)hipStreamDestroy(b->stream);
+    for (hipStream_t st : {b->stream, b->copy_stream, b->d2h_stream})
+        if (st) (void)hipStreamDestroy(st);
     delete b;  // DevBuf destructors free device memory
 }
 
