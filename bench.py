@@ -258,6 +258,12 @@ class Workload:
 
     def algo_bytes_per_launch(self):
         """Bytes one probe launch must move (per bank; averaged over banks)."""
+        if getattr(self, "partitioned", False):
+            # partitioned rbloom pipeline, per filter bit tested: 4-B offset + 2-B
+            # k-mer id written and the offset read back, a miss byte zeroed,
+            # (sometimes) set and read; plus the filter once and the reads
+            entries = self.kmers * self.rows_per_kmer
+            return entries * 13 + self.banks[0].info.device_bytes + self.seq_bytes + self.n * (8 + 4 + 8 + 8)
         per_bank = []
         for d in self.docs:
             rows = self.rows_per_kmer if self.args.workload != "mlst" else self.rows_per_kmer / len(self.docs)
@@ -331,7 +337,16 @@ def main():
         assert int(tot[-1]) == want, f"k-mer total {int(tot[-1])} != {want}"
 
     value = wl.probes_per_step() * args.steps / elapsed
-    if rows_read:  # rbloom: the data-dependent count of filter words loaded
+    from xspect2_amd._lib import XS_PATH_PARTITIONED
+    wl.partitioned = args.workload == "genus" and wl.banks[0].probe_path() == XS_PATH_PARTITIONED
+    if wl.partitioned:
+        wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 1 MiB filter partition) -> "
+                     "bloom_lookup (per-XCD L2-resident partition) -> resolve -> count")
+        wl.row_bytes = None
+        wl.roofline_note = ("streamed bytes of the partitioned pipeline (13 B per filter bit tested + filter + "
+                            "reads); the bounds are VALU (hashing in bloom_bucket) and the L2 gather rate "
+                            "(bloom_lookup), not HBM: see DESIGN.md")
+    elif rows_read:  # rbloom: the data-dependent count of filter words loaded
         wl.rows_per_kmer = rows_read / max(1, launches) / wl.kmers
     algo_bytes = wl.algo_bytes_per_launch()
     achieved = algo_bytes / (probe_ms * 1e-3) / 1e9
@@ -347,6 +362,8 @@ def main():
         except Exception:
             traffic = None
 
+    if wl.partitioned:
+        traffic = None  # r01_traffic.json was measured on the gather path
     host = host_path(wl, args)
 
     cpu = None

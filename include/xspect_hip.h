@@ -177,9 +177,21 @@ int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float*
 /* rbloom banks: filter words the probe kernels loaded since profiling was
  * enabled or the last call (then resets).  The probe tests 2 bits first and
  * loads the other K-2 only for k-mers that pass them, as rbloom stops at the
- * first zero bit, so the count depends on the data.  0 for COBS banks, whose
- * kernels read exactly h rows per k-mer and doc group. */
+ * first zero bit, so the count depends on the data; the partitioned path
+ * (xs_bank_probe_path) tests all K.  0 for COBS banks, whose kernels read
+ * exactly h rows per k-mer and doc group. */
 int xs_bank_probe_rows(xs_bank* bank, uint64_t* rows);
+
+/* Probe path of the last query on this handle: XS_PATH_GATHER (one random
+ * filter/row gather per hash, every bank kind) or XS_PATH_PARTITIONED (rbloom
+ * filters of >= 16 MiB: k-mer bit indices binned by 1 MiB filter partition,
+ * each partition tested from one XCD's L2).  The partitioned path is taken
+ * while the handle's previous query found at least 35 % of its k-mers in the
+ * filter (member-rich input, where it is faster); XSPECT2_AMD_BLOOM_PART=0
+ * disables it.  Both give identical results. */
+#define XS_PATH_GATHER 0
+#define XS_PATH_PARTITIONED 1
+int xs_bank_probe_path(const xs_bank* bank, int* path);
 
 void xs_bank_close(xs_bank* bank);
 

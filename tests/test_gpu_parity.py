@@ -142,8 +142,11 @@ def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
     gb2.close()
 
 
+@pytest.mark.parametrize("mode", ["0", "2"])
 @pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
-def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, k):
+def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode):
+    """mode 0: direct probe; mode 2: partitioned probe with small partitions."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
     n_items = sum(len(s) for s in genome) - k + 1
@@ -161,6 +164,71 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, k):
         assert np.array_equal(got_h[:, 0], want_h)
         tot, nk = gb.query_totals(reads, step=step)
         assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+    gb.close()
+
+
+@pytest.mark.parametrize("mode,k,K,nbytes", [("2", 21, 7, 200_003), ("2", 31, 5, 77_777), ("2", 16, 8, 1 << 20),
+                                             ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099)])
+def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mode, k, K, nbytes):
+    """The partitioned rbloom probe (k-mer bit indices binned by filter
+    partition, per-partition lookup, per-read count) against the oracle:
+    hundreds of bucket blocks, ragged and multi-unit reads, empty and short
+    reads, non-ACGT bytes, steps 1 and 3.  mode 1 with 40 MiB takes the
+    default path (20 partitions of 2 MiB); the 2 GiB + 4 KiB filter needs
+    4 MiB partitions (more than 1024 of 2 MiB) and a partial last one."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
+    rng = np.random.default_rng(nbytes % 1000 + k)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genome = [acgt[rng.integers(0, 4, 60_000)].tobytes() for _ in range(3)]
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.upload(bf.bits)
+    reads = []
+    for _ in range(2500):
+        g = genome[int(rng.integers(0, 3))]
+        st = int(rng.integers(0, len(g) - 200))
+        reads.append(g[st:st + int(rng.integers(100, 200))])
+    reads += _reads(rng, 800, k, alphabet="ACGT", max_len=400)
+    reads += _reads(rng, 100, k, alphabet="ACGTacgtNRY")
+    reads += [b"", b"A" * (k - 1), genome[1][:5000], b"", genome[2][:k], genome[0]]
+    order = rng.permutation(len(reads))
+    reads = [reads[i] for i in order]
+    for step in (1, 3):
+        want_h, want_n = bf.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h[:, 0], want_h), int((got_h[:, 0] != want_h).sum())
+        tot, nk = gb.query_totals(reads, step=step)
+        assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+    assert 0 < int(want_h.sum()) < int(want_n.sum())
+    gb.close()
+
+
+def test_bloom_path_follows_member_fraction(xs, oracle_mod, monkeypatch):
+    """Default mode on a 40 MiB filter: the first query takes the partitioned
+    path; after a member-poor query (random reads) the next takes the gather
+    path, and after a member-rich one the partitioned path again.  Every
+    answer equals the oracle's."""
+    from xspect2_amd import _lib
+    monkeypatch.delenv("XSPECT2_AMD_BLOOM_PART", raising=False)
+    rng = np.random.default_rng(9)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genome = [acgt[rng.integers(0, 4, 50_000)].tobytes()]
+    bf = oracle_mod.BloomFilter(np.zeros(40 << 20, dtype=np.uint8), 7, 21)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(21, 40 << 20, 7)
+    gb.upload(bf.bits)
+    members = [genome[0][s:s + 150] for s in rng.integers(0, 49_000, 2000)]
+    foreign = _reads(rng, 2000, 21, alphabet="ACGT", min_len=150, max_len=151)
+    paths = []
+    for reads in (foreign, foreign, members, members):
+        got_h, got_n = gb.query(reads)
+        want_h, want_n = bf.query(reads)
+        assert np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)
+        paths.append(gb.probe_path())
+    P, G = _lib.XS_PATH_PARTITIONED, _lib.XS_PATH_GATHER
+    assert paths == [P, G, G, P], paths
     gb.close()
 
 

@@ -23,6 +23,8 @@ XS_ERR_UNSUPPORTED = -5
 XS_BANK_COBS_CLASSIC = 0
 XS_BANK_COBS_COMPACT = 1
 XS_BANK_RBLOOM = 2
+XS_PATH_GATHER = 0
+XS_PATH_PARTITIONED = 1
 
 XS_BEST_AMBIGUOUS = 0xFFFFFFFF
 
@@ -107,6 +109,7 @@ SIGNATURES = {
     "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_probe_rows": (_int, [_vp, ctypes.POINTER(_u64)]),
+    "xs_bank_probe_path": (_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "xs_bank_close": (None, [_vp]),
     "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _vp, ctypes.c_char_p, _vp,
                                         ctypes.c_char_p, _vp, _vp, _int]),

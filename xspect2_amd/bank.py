@@ -241,6 +241,12 @@ class Bank:
         check(load().xs_bank_probe_rows(self.handle, ctypes.byref(n)))
         return int(n.value)
 
+    def probe_path(self) -> int:
+        """Path of the last query: _lib.XS_PATH_GATHER or _lib.XS_PATH_PARTITIONED."""
+        v = ctypes.c_int(0)
+        check(load().xs_bank_probe_path(self.handle, ctypes.byref(v)))
+        return int(v.value)
+
     # ------------------------------------------------------------ lifetime
     def close(self) -> None:
         if self._h is not None:

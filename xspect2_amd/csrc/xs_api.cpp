@@ -141,6 +141,15 @@ struct xs_bank {
     DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
         best;
     DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
+    DevBuf pk_nkc, pk_kofs, pk_scan, pk_entries, pk_tbl, pk_miss, pk_aux;  // partitioned rbloom probe
+    // rbloom path choice: member fraction of the last query whose totals have
+    // landed (members, k-mers), copied back asynchronously after every query
+    DevBuf bloom_tot;
+    PinnedBuf bloom_tot_h;
+    hipEvent_t bloom_ev = nullptr;
+    bool bloom_pending = false;
+    double member_frac = 1.0;
+    int last_path = XS_PATH_GATHER;
     PinnedBuf stage[2];             // D2H staging ring for large host outputs
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
@@ -465,9 +474,19 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     const int blocks = probe_grid(b);
     uint64_t* partials = nullptr;
     const uint64_t pcols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
-    if (d_totals) {
+    const bool bloom = b->kind == XS_BANK_RBLOOM;
+    if (d_totals || bloom) {  // rbloom always: its totals steer the next query's path
         if (int rc = b->partials.ensure((size_t)blocks * pcols * 8)) return rc;
         partials = b->partials.as<uint64_t>();
+    }
+    if (bloom && b->bloom_pending) {
+        const hipError_t q = hipEventQuery(b->bloom_ev);
+        (void)hipGetLastError();  // hipErrorNotReady is not an error here
+        if (q == hipSuccess) {
+            const uint64_t* t = static_cast<const uint64_t*>(b->bloom_tot_h.p);
+            if (t[1]) b->member_frac = (double)t[0] / (double)t[1];
+            b->bloom_pending = false;
+        }
     }
     if (b->profiling) {
         if (b->events_used == b->events.size()) {
@@ -478,13 +497,40 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         }
         HIPCHK(hipEventRecord(b->events[b->events_used].first, s));
     }
-    if (b->kind == XS_BANK_RBLOOM) HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, partials, blocks, s));
-    else HIPCHK(launch_probe_cobs(rv, b->cobs_view(), d_hits, partials, blocks, s));
+    BloomPartPlan plan;
+    b->last_path = XS_PATH_GATHER;
+    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.seq_bytes, step, b->member_frac, &plan)) {
+        b->last_path = XS_PATH_PARTITIONED;
+        if (int rc = b->pk_nkc.ensure(plan.nkc_bytes)) return rc;
+        if (int rc = b->pk_kofs.ensure(plan.nkc_bytes)) return rc;
+        if (int rc = b->pk_scan.ensure(plan.scan_bytes)) return rc;
+        if (int rc = b->pk_entries.ensure(plan.entry_bytes)) return rc;
+        if (int rc = b->pk_tbl.ensure(plan.tbl_bytes)) return rc;
+        if (int rc = b->pk_miss.ensure(plan.miss_bytes)) return rc;
+        if (int rc = b->pk_aux.ensure(plan.aux_bytes)) return rc;
+        const BloomPartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
+                             b->pk_entries.as<uint64_t>(), b->pk_tbl.as<uint16_t>(), b->pk_miss.as<uint32_t>(),
+                             b->pk_aux.as<uint32_t>()};
+        HIPCHK(launch_probe_bloom_part(rv, b->bloom_view(), plan, ws, d_hits, partials, blocks, s));
+    } else if (b->kind == XS_BANK_RBLOOM) {
+        HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, partials, blocks, s));
+    } else {
+        HIPCHK(launch_probe_cobs(rv, b->cobs_view(), d_hits, partials, blocks, s));
+    }
     if (b->profiling) {
         HIPCHK(hipEventRecord(b->events[b->events_used].second, s));
         ++b->events_used;
     }
     if (d_totals) HIPCHK(launch_reduce_partials(partials, blocks, pcols, d_totals, s));
+    if (bloom && !b->bloom_pending) {
+        if (int rc = b->bloom_tot.ensure(2 * sizeof(uint64_t))) return rc;
+        if (int rc = b->bloom_tot_h.ensure(2 * sizeof(uint64_t))) return rc;
+        if (!b->bloom_ev) HIPCHK(hipEventCreateWithFlags(&b->bloom_ev, hipEventDisableTiming));
+        HIPCHK(launch_reduce_partials(partials, blocks, pcols, b->bloom_tot.as<uint64_t>(), s));
+        HIPCHK(hipMemcpyAsync(b->bloom_tot_h.p, b->bloom_tot.p, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipEventRecord(b->bloom_ev, s));
+        b->bloom_pending = true;
+    }
     return XS_OK;
 }
 
@@ -1063,6 +1109,12 @@ int xs_bank_probe_rows(xs_bank* b, uint64_t* rows) {
     return XS_OK;
 }
 
+int xs_bank_probe_path(const xs_bank* b, int* path) {
+    if (!b || !path) return fail(XS_ERR_ARG, "null argument");
+    *path = b->last_path;
+    return XS_OK;
+}
+
 int xs_bank_last_probe_ms(xs_bank* b, float* ms) {
     if (!b || !ms) return fail(XS_ERR_ARG, "null argument");
     std::lock_guard<std::mutex> lk(b->mu);
@@ -1104,6 +1156,7 @@ void xs_bank_close(xs_bank* b) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->hstage_ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (b->bloom_ev) (void)hipEventDestroy(b->bloom_ev);
     for (auto& ev : b->chunk_ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->events) {
         (void)hipEventDestroy(ev.first);

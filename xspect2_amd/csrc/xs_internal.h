@@ -81,6 +81,38 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
                              uint64_t* partials, int blocks, hipStream_t s);
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
                               uint64_t* partials, int blocks, hipStream_t s);
+// Partitioned rbloom probe (xs_probe_bloompart.hip): k-mers per bucket block,
+// most hash functions it takes, most filter partitions.
+constexpr int kPartKmers = 1024;
+constexpr int kPartKMax = 8;
+constexpr uint32_t kPartMax = 1024;
+struct BloomPartPlan {
+    uint32_t shift;      // log2 filter bits per partition
+    uint32_t P;          // partitions
+    uint64_t tstride;    // bucket blocks (>= the call's k-mers / kPartKmers)
+    uint64_t kbound;     // upper bound of the call's sampled k-mers
+    size_t entry_bytes, tbl_bytes, miss_bytes, nkc_bytes, scan_bytes, aux_bytes;
+};
+struct BloomPartWs {
+    uint64_t* nkc;       // n+1 per-read k-mer counts
+    uint64_t* kofs;      // n+1 exclusive scan: first k-mer id of each read
+    void* scan_tmp;
+    size_t scan_bytes;
+    uint64_t* entries;   // tstride regions of kPartKmers*K entries: u32 offsets, u16 k-mer ids, u8 miss flags
+    uint16_t* tbl;       // (P+1) x tstride partition starts per bucket block
+    uint32_t* miss;      // one bit per k-mer id: some filter bit was zero
+    uint32_t* aux;       // bucket block -> read holding its first k-mer (tstride+1), then per-partition queue counters
+};
+// False when the direct probe should run (small filter, K > kPartKMax, a
+// batch too large for the transient workspace, member-poor input -- the
+// previous query's member fraction below kPartMinMembers -- or
+// XSPECT2_AMD_BLOOM_PART=0).
+constexpr double kPartMinMembers = 0.35;
+bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32_t step, double member_frac,
+                     BloomPartPlan* plan);
+hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,
+                                   const BloomPartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
+                                   hipStream_t s);
 hipError_t launch_reduce_partials(const uint64_t* partials, int blocks, uint64_t cols,
                                   uint64_t* totals, hipStream_t s);
 hipError_t launch_build_cobs(const ReadView& rv, const uint32_t* rec_doc, const CobsView& bv,

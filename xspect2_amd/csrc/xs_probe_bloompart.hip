@@ -1,0 +1,494 @@
+// xs_probe_bloompart.hip — partitioned rbloom probe for filters far larger than L2.
+//
+// The direct probe (probe_bloom_kernel) gathers ~6 random filter words per
+// k-mer; every one is a 128-B line fill from HBM, so it runs at the chip's
+// random line-fill rate (~58 G lines/s).  Here the same membership test is
+// reorganised around the filter instead of the k-mers:
+//
+//   counts  : per read k-mer count, exclusive scan -> global k-mer id g
+//   bucket  : one block per 1024 k-mers: canonical k-mer, XXH3-64, the K
+//             LCG bit indices (exactly as probe_bloom_kernel, kept in
+//             registers), each binned by filter partition (1 MiB of filter =
+//             2^23 bits, or larger for filters > 1 GiB) with LDS counters, a
+//             block scan and LDS-sorted placement.  The block copies its
+//             entries (u32 bit offset in the partition, u16 k-mer id)
+//             partition-ordered into its own region with coalesced stores and
+//             one u16 start per partition into a partition-major table.
+//   lookup  : the workgroups of one XCD work through one partition at a time
+//             (blocks b and b+8 share an XCD) from a per-partition queue, so
+//             the filter bytes they test stay in that XCD's 4 MiB L2 while the
+//             entries stream past; a zero bit sets the entry's miss byte.
+//   resolve : per bucket block, miss bytes -> miss bits of its 1024 k-mers.
+//   count   : per work unit, sampled k-mers minus missed k-mers -> hits per
+//             read (direct store or atomicAdd for multi-unit reads) + totals.
+//
+// A k-mer is a member iff none of its K bits is zero: the same answer as
+// rbloom's `kmer in bf` (probabilistic_single_filter_model.py:122-124), which
+// stops at the first zero bit.  Parity: tests/test_gpu_parity.py (rbloom
+// cases run through this path and the direct one).
+#include <hipcub/hipcub.hpp>
+
+#include "xs_device.h"
+
+namespace xs {
+
+namespace {
+
+constexpr int kTK = kPartKmers;  // k-mers per bucket block
+constexpr int kBucketThreads = 512;
+constexpr uint32_t kStageReads = 256;  // read offsets a bucket block keeps in LDS
+
+__global__ void part_counts_kernel(const uint64_t* __restrict__ offs, uint64_t n, uint32_t k, uint32_t step,
+                                   uint64_t* __restrict__ nkc) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r <= n;
+         r += (uint64_t)gridDim.x * blockDim.x)
+        nkc[r] = r < n ? num_kmers(offs[r + 1] - offs[r], k, step) : 0;
+}
+
+// Largest r in [lo, hi] with kofs[r] <= g (kofs non-decreasing, kofs[lo] <= g).
+__device__ __forceinline__ uint64_t read_of(const uint64_t* __restrict__ kofs, uint64_t lo, uint64_t hi,
+                                            uint64_t g) {
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi + 1) >> 1;
+        if (kofs[mid] <= g) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+// blk_read[b] = the read holding k-mer b*kTK (the first k-mer of bucket block b).
+__global__ void part_map_kernel(const uint64_t* __restrict__ kofs, uint64_t n, uint32_t* __restrict__ blk_read) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t fb = (kofs[r] + kTK - 1) / kTK, lb = (kofs[r + 1] + kTK - 1) / kTK;
+        for (uint64_t b = fb; b < lb; ++b) blk_read[b] = (uint32_t)r;
+    }
+}
+
+template <int KT, int KB>
+__global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView rv, BloomView bv,
+                                                                      const uint64_t* __restrict__ kofs,
+                                                                      uint32_t shift, uint32_t P, uint64_t tstride,
+                                                                      uint32_t* __restrict__ eoff,
+                                                                      uint16_t* __restrict__ eid,
+                                                                      uint16_t* __restrict__ tbm,
+                                                                      const uint32_t* __restrict__ blk_read, int dbg) {
+    using Scan = hipcub::BlockScan<uint32_t, kBucketThreads>;
+    constexpr int ITEMS = kPartMax / kBucketThreads;
+    constexpr int PER = kTK / kBucketThreads;  // k-mers per thread
+    constexpr int NK = KB ? KB : kPartKMax;
+    __shared__ uint32_t s_off[kTK * NK];  // partition-ordered bit offsets
+    __shared__ uint16_t s_id[kTK * NK];   // their k-mer (0..kTK-1)
+    __shared__ uint32_t cur[kPartMax];
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ uint64_t s_kofs[kStageReads], s_offs[kStageReads];
+    const int tid = threadIdx.x;
+    const uint32_t K = KB ? KB : bv.K;
+    const uint32_t k = KT ? KT : rv.k;
+    const uint64_t Nk = kofs[rv.n];
+    const uint64_t g0 = (uint64_t)blockIdx.x * kTK;
+    if (g0 >= Nk) return;  // uniform per block
+    const uint32_t m = (uint32_t)min((uint64_t)kTK, Nk - g0);
+    for (uint32_t i = tid; i < kPartMax; i += kBucketThreads) cur[i] = 0;
+    // reads of this block: from the one holding k-mer g0 to the one holding the
+    // next block's first k-mer (or the last read); their k-mer and byte
+    // offsets go to LDS when they fit, so a k-mer costs one global load (its
+    // window) and every thread's windows are in flight together
+    const uint64_t lo = blk_read[blockIdx.x];
+    const uint64_t hi = g0 + kTK < Nk ? blk_read[blockIdx.x + 1] : rv.n - 1;
+    const uint64_t nr = hi - lo + 2;  // kofs/offs entries lo .. hi+1
+    const bool staged = nr <= kStageReads;
+    if (staged)
+        for (uint32_t x = tid; x < nr; x += kBucketThreads) {
+            s_kofs[x] = kofs[lo + x];
+            s_offs[x] = rv.offs[lo + x];
+        }
+    __syncthreads();
+    const uint64_t omask = (1ull << shift) - 1;
+    Kmer c[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * kBucketThreads;
+        if (i < m) {
+            const uint64_t g = g0 + i;
+            uint64_t r, o0, o1, kr;
+            if (staged) {
+                uint32_t a = 0, b = (uint32_t)(nr - 2);  // largest x with s_kofs[x] <= g
+                while (a < b) {
+                    const uint32_t mid = (a + b + 1) >> 1;
+                    if (s_kofs[mid] <= g) a = mid;
+                    else b = mid - 1;
+                }
+                kr = s_kofs[a];
+                o0 = s_offs[a];
+                o1 = s_offs[a + 1];
+            } else {
+                r = read_of(kofs, lo, hi, g);
+                kr = kofs[r];
+                o0 = rv.offs[r];
+                o1 = rv.offs[r + 1];
+            }
+            kmer_at<KT, kKmerBio>(rv, o0, o1 - o0, (g - kr) * rv.step, k, c[q]);
+        }
+    }
+    uint64_t idx[PER][NK];  // the K bit indices of this thread's k-mers stay in registers
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * kBucketThreads;
+        if (i < m) {
+            uint64_t sl = xxh3_kmer<KT>(c[q], k), sh = 0;
+#pragma unroll
+            for (int j = 0; j < NK; ++j) {
+                if ((uint32_t)j < K) {
+                    const uint64_t p = sl * kLcgMl;
+                    const uint64_t nl = p + kLcgCl;
+                    const uint64_t carry = nl < p;
+                    sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
+                    sl = nl;
+                    idx[q][j] = (dbg & 32) ? ((uint64_t)(i * 7 + j) * 2654435761ull) % bv.mbits
+                                           : fastmod(sh, bv.mbits, bv.magic);
+                    atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t v[ITEMS];
+#pragma unroll
+    for (int q = 0; q < ITEMS; ++q) v[q] = cur[tid * ITEMS + q];
+    Scan(scan_tmp).ExclusiveSum(v, v);
+    __syncthreads();  // every counter read before it becomes a cursor
+#pragma unroll
+    for (int q = 0; q < ITEMS; ++q) {
+        const uint32_t p = tid * ITEMS + q;
+        if (p < P) {
+            cur[p] = v[q];
+            tbm[(uint64_t)blockIdx.x * (P + 1) + p] = (uint16_t)v[q];
+        }
+    }
+    if (tid == 0) tbm[(uint64_t)blockIdx.x * (P + 1) + P] = (uint16_t)(m * K);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * kBucketThreads;
+        if (i < m) {
+#pragma unroll
+            for (int j = 0; j < NK; ++j) {
+                if ((uint32_t)j < K) {
+                    const uint32_t pos = atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
+                    s_off[pos] = (uint32_t)(idx[q][j] & omask);
+                    s_id[pos] = (uint16_t)i;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // coalesced copy-out (regions are kTK*K entries: 16-B aligned for both arrays)
+    const uint64_t base = (uint64_t)blockIdx.x * kTK * K;
+    const uint32_t tot = m * K;
+    for (uint32_t e = tid * 4; e < tot; e += kBucketThreads * 4) {
+        if (e + 4 <= tot) {
+            *reinterpret_cast<uint4*>(eoff + base + e) = *reinterpret_cast<const uint4*>(s_off + e);
+            *reinterpret_cast<uint2*>(eid + base + e) = *reinterpret_cast<const uint2*>(s_id + e);
+        } else {
+            for (uint32_t x = e; x < tot; ++x) {
+                eoff[base + x] = s_off[x];
+                eid[base + x] = s_id[x];
+            }
+        }
+    }
+}
+
+// Block-major partition starts (one coalesced row per bucket block) ->
+// partition-major (the lookup reads 64 blocks' starts of one partition as one
+// line), through a 64 x 64 LDS tile.
+__global__ void __launch_bounds__(256) part_transpose_kernel(const uint16_t* __restrict__ tbm, uint32_t P1,
+                                                             uint64_t tstride, uint16_t* __restrict__ tbl) {
+    __shared__ uint16_t t[64][65];
+    const uint64_t b0 = (uint64_t)blockIdx.x * 64;
+    const uint32_t p0 = blockIdx.y * 64;
+    for (uint32_t x = threadIdx.x; x < 64 * 64; x += 256) {
+        const uint32_t bi = x / 64, pi = x % 64;
+        if (b0 + bi < tstride && p0 + pi < P1) t[bi][pi] = tbm[(b0 + bi) * P1 + p0 + pi];
+    }
+    __syncthreads();
+    for (uint32_t x = threadIdx.x; x < 64 * 64; x += 256) {
+        const uint32_t pi = x / 64, bi = x % 64;
+        if (b0 + bi < tstride && p0 + pi < P1) tbl[(p0 + pi) * tstride + b0 + bi] = t[bi][pi];
+    }
+}
+
+// The waves of one XCD work through one partition at a time (its filter
+// bytes stay in the XCD's 4 MiB L2 while the entries stream past), taking
+// groups of 64 bucket blocks from the partition's queue counter.  A queue
+// self-balances: with a static deal the wave scheduler lets some waves run
+// partitions ahead and the L2 hit rate fell from 84 % to 44 %.  Each counter
+// sits on its own 128-B line (a line's atomics are serialised at the memory
+// side).  Every lane keeps kLookupUnroll entries in flight.
+constexpr uint32_t kQStride = 32;  // u32 per queue counter
+
+template <int kLookupUnroll>
+__global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const uint64_t* __restrict__ kofs,
+                                                           uint64_t n, uint32_t K, uint32_t shift, uint32_t P,
+                                                           uint64_t tstride, const uint32_t* __restrict__ eoff,
+                                                           const uint16_t* __restrict__ tbl,
+                                                           uint8_t* __restrict__ emiss, uint32_t* qctr, int dbg) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nblk = (kofs[n] + kTK - 1) / kTK;
+    const uint64_t cap = (uint64_t)kTK * K;
+    const uint32_t xcd = blockIdx.x & 7;
+    for (uint64_t p = xcd; p < P; p += 8) {
+        const uint32_t* pb = bv.bits + (p << (shift - 5));
+        const uint16_t* t0 = tbl + p * tstride;
+        const uint16_t* t1 = t0 + tstride;
+        for (;;) {
+            uint32_t grp = 0;
+            if (lane == 0) grp = atomicAdd(&qctr[p * kQStride], 1u);
+            const uint64_t b0 = (uint64_t)__builtin_amdgcn_readfirstlane(grp) * 64;
+            if (b0 >= nblk) break;
+        {
+            const uint64_t b = b0 + lane;
+            uint32_t s = 0, len = 0;
+            if (b < nblk) {
+                s = t0[b];
+                len = (uint32_t)t1[b] - s;
+            }
+            uint32_t inc = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc += t;
+            }
+            const uint32_t pre = inc - len;
+            const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+            for (uint32_t i0 = 0; i0 < total; i0 += 64 * kLookupUnroll) {
+                uint64_t pos[kLookupUnroll];
+                uint32_t off[kLookupUnroll], w[kLookupUnroll];
+#pragma unroll
+                for (int u = 0; u < kLookupUnroll; ++u) {
+                    const uint32_t i = i0 + u * 64 + lane;
+                    int j = 0;
+#pragma unroll
+                    for (int st = 32; st; st >>= 1) {
+                        const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
+                        if (pv <= i) j += st;
+                    }
+                    const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
+                    const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
+                    pos[u] = (b0 + j) * cap + sj + (i - pj);
+                }
+#pragma unroll
+                for (int u = 0; u < kLookupUnroll; ++u)
+                    off[u] = i0 + u * 64 + lane < total ? ((dbg & 4) ? (uint32_t)pos[u] * 97u & 0xFFFFFu : eoff[pos[u]]) : 0u;
+#pragma unroll
+                for (int u = 0; u < kLookupUnroll; ++u)
+                    w[u] = i0 + u * 64 + lane < total ? ((dbg & 2) ? off[u] * 0x9E3779B1u : pb[off[u] >> 5]) : ~0u;
+#pragma unroll
+                for (int u = 0; u < kLookupUnroll; ++u)
+                    if (!((w[u] >> (off[u] & 31)) & 1u) && !(dbg & 1)) emiss[pos[u]] = 1;
+            }
+        }
+        }
+    }
+}
+
+// Per bucket block: its entries' miss bytes -> the miss bits of its 1024 k-mers.
+__global__ void __launch_bounds__(256) bloom_resolve_kernel(const uint64_t* __restrict__ kofs, uint64_t n,
+                                                            uint32_t K, const uint16_t* __restrict__ eid,
+                                                            const uint8_t* __restrict__ emiss,
+                                                            uint32_t* __restrict__ miss) {
+    __shared__ uint32_t s_m[kTK / 32];
+    const uint64_t Nk = kofs[n];
+    const uint64_t g0 = (uint64_t)blockIdx.x * kTK;
+    if (g0 >= Nk) return;
+    const uint32_t tot = (uint32_t)min((uint64_t)kTK, Nk - g0) * K;
+    if (threadIdx.x < kTK / 32) s_m[threadIdx.x] = 0;
+    __syncthreads();
+    // 4 entries per lane: regions are multiples of 4 entries, and miss bytes
+    // past `tot` are zero (memset per call, never written)
+    const uint64_t base = (uint64_t)blockIdx.x * kTK * K;
+    for (uint32_t e = threadIdx.x * 4; e < tot; e += blockDim.x * 4) {
+        const uint32_t f = *reinterpret_cast<const uint32_t*>(emiss + base + e);
+        if (f) {
+            const uint2 ids = *reinterpret_cast<const uint2*>(eid + base + e);
+            const uint32_t id4[4] = {ids.x & 0xFFFFu, ids.x >> 16, ids.y & 0xFFFFu, ids.y >> 16};
+#pragma unroll
+            for (int x = 0; x < 4; ++x)
+                if ((f >> (8 * x)) & 0xFFu) atomicOr(&s_m[id4[x] >> 5], 1u << (id4[x] & 31));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kTK / 32) miss[(g0 >> 5) + threadIdx.x] = s_m[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(256) bloom_count_kernel(ReadView rv, const uint64_t* __restrict__ kofs,
+                                                          const uint32_t* __restrict__ miss, uint32_t K,
+                                                          uint32_t* __restrict__ hits,
+                                                          uint64_t* __restrict__ partials,
+                                                          uint64_t* __restrict__ rows_read) {
+    __shared__ uint64_t s_h[4], s_k[4];
+    const uint32_t k = rv.k;
+    const uint64_t U = rv.queue[0];
+    uint64_t hit_total = 0, kmer_total = 0;
+    for (uint64_t u = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; u < U;
+         u += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t r = rv.unit_read[u];
+        const uint64_t seg = u - rv.unit_ofs[r];
+        const uint64_t nk = num_kmers(rv.offs[r + 1] - rv.offs[r], k, rv.step);
+        const uint64_t t0 = seg * kSegKmers;
+        const uint32_t cnt = (uint32_t)min((uint64_t)kSegKmers, nk - t0);
+        const uint64_t g = kofs[r] + t0, ge = g + cnt;
+        uint32_t missed = 0;
+        for (uint64_t q = g; q < ge;) {
+            const uint32_t bit = (uint32_t)(q & 31);
+            const uint32_t take = (uint32_t)min((uint64_t)(32 - bit), ge - q);
+            const uint32_t w = miss[q >> 5] >> bit;
+            missed += (uint32_t)__popc(take == 32 ? w : (w & ((1u << take) - 1u)));
+            q += take;
+        }
+        const uint32_t c = cnt - missed;
+        if (hits) {
+            if (nk <= kSegKmers) hits[r] = c;
+            else if (c) atomicAdd(&hits[r], c);
+        }
+        hit_total += c;
+        kmer_total += cnt;
+    }
+    // wave sums, then block sums
+    for (int d = 32; d; d >>= 1) {
+        hit_total += (uint64_t)__shfl_xor((long long)hit_total, d, 64);
+        kmer_total += (uint64_t)__shfl_xor((long long)kmer_total, d, 64);
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) {
+        s_h[wid] = hit_total;
+        s_k[wid] = kmer_total;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint64_t a = s_h[0] + s_h[1] + s_h[2] + s_h[3];
+        const uint64_t b = s_k[0] + s_k[1] + s_k[2] + s_k[3];
+        if (partials) {
+            partials[blockIdx.x * 2ull] = a;
+            partials[blockIdx.x * 2ull + 1] = b;
+        }
+        if (rows_read && b) atomicAdd(reinterpret_cast<unsigned long long*>(rows_read), (unsigned long long)(b * K));
+    }
+}
+
+}  // namespace
+
+// XSPECT2_AMD_BLOOM_PART: 0 = direct probe only; 1 (default) = partitioned
+// probe for filters of >= 16 partitions (16 MiB) on member-rich input; 2 = partitioned for every filter,
+// with partitions down to 1024 bits (tests reach many partitions on small
+// filters, whatever the input).  Read per call.
+static int part_env() {
+    const char* e = getenv("XSPECT2_AMD_BLOOM_PART");
+    return e ? atoi(e) : 1;
+}
+
+// Partition shift for a filter of `mbits` bits: 2^23-bit (1 MiB) partitions,
+// doubled until at most kPartMax of them cover the filter.
+static uint32_t part_shift(uint64_t mbits, uint32_t min_shift) {
+    uint32_t s = min_shift;
+    while (((mbits + (1ull << s) - 1) >> s) > kPartMax) ++s;
+    return s;
+}
+
+bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32_t step, double member_frac,
+                     BloomPartPlan* plan) {
+    const int mode = part_env();
+    if (mode <= 0 || bv.K == 0 || bv.K > (uint32_t)kPartKMax) return false;
+    // member-poor input: the direct probe's early exit (2 bits first) wins
+    if (mode == 1 && member_frac < kPartMinMembers) return false;
+    const uint32_t shift = part_shift(bv.mbits, mode >= 2 ? 10 : 23);
+    const uint64_t P = (bv.mbits + (1ull << shift) - 1) >> shift;
+    // small filters stay L2/MALL resident: the direct probe is faster there
+    const uint64_t min_parts = mode >= 2 ? 1 : 16;
+    if (P < min_parts || shift > 32) return false;
+    const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
+    if (kbound >= (1ull << 32)) return false;
+    const uint64_t nblk = (kbound + kTK - 1) / kTK;
+    plan->shift = shift;
+    plan->P = (uint32_t)P;
+    plan->tstride = nblk;
+    plan->kbound = kbound;
+    plan->entry_bytes = nblk * kTK * bv.K * (sizeof(uint32_t) + sizeof(uint16_t) + sizeof(uint8_t));
+    plan->tbl_bytes = 2 * (P + 1) * nblk * sizeof(uint16_t);  // partition-major + block-major
+    plan->miss_bytes = nblk * (kTK / 32) * sizeof(uint32_t);
+    plan->aux_bytes = (nblk + 1 + kQStride) * sizeof(uint32_t) + (size_t)P * kQStride * sizeof(uint32_t);
+    plan->nkc_bytes = (n + 1) * sizeof(uint64_t);
+    size_t sb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(n + 1));
+    plan->scan_bytes = sb;
+    // entries are transient: cap the workspace (larger batches take the direct probe)
+    return plan->entry_bytes <= (24ull << 30);
+}
+
+// Timing experiments only (results are wrong when set): XSPECT2_AMD_BLOOM_DBG
+// bit 0 skips the miss stores, bit 1 the filter loads, bit 2 the entry loads,
+// bit 5 the bucket kernel's hashing (indices from the k-mer number instead).
+static int dbg_env() {
+    const char* e = getenv("XSPECT2_AMD_BLOOM_DBG");
+    return e ? atoi(e) : 0;
+}
+
+static int lookup_unroll() {
+    const char* e = getenv("XSPECT2_AMD_BLOOM_UNROLL");
+    const int u = e ? atoi(e) : 16;
+    return (u == 4 || u == 8 || u == 16) ? u : 16;
+}
+
+template <int U>
+static int lookup_grid() {
+    static std::atomic<int> cache{0};
+    return cached_grid(cache, [] {
+        const int g = resident_grid(bloom_lookup_kernel<U>, 256, 0);
+        return g >= 8 ? g / 8 * 8 : 8;
+    });
+}
+
+hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,
+                                   const BloomPartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
+                                   hipStream_t s) {
+    part_counts_kernel<<<grid_for(rv.n + 1, 256, 4096), 256, 0, s>>>(rv.offs, rv.n, rv.k, rv.step, ws.nkc);
+    size_t sb = ws.scan_bytes;
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, sb, ws.nkc, ws.kofs, (int)(rv.n + 1), s);
+    if (e != hipSuccess) return e;
+    const uint64_t ne = plan.tstride * kTK * bv.K;
+    uint32_t* eoff = reinterpret_cast<uint32_t*>(ws.entries);
+    uint16_t* eid = reinterpret_cast<uint16_t*>(eoff + ne);
+    uint8_t* emiss = reinterpret_cast<uint8_t*>(eid + ne);
+    if ((e = hipMemsetAsync(emiss, 0, ne, s)) != hipSuccess) return e;
+    uint32_t* blk_read = ws.aux;
+    uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.tstride;  // block-major copy
+    part_map_kernel<<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
+    if (rv.k == 21 && bv.K == 7)
+        bloom_bucket_kernel<21, 7><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
+            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read, dbg_env());
+    else
+        bloom_bucket_kernel<0, 0><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
+            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read, dbg_env());
+    part_transpose_kernel<<<dim3((unsigned)((plan.tstride + 63) / 64), (plan.P + 1 + 63) / 64), 256, 0, s>>>(
+        tbm, plan.P + 1, plan.tstride, ws.tbl);
+    uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
+    if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
+    switch (lookup_unroll()) {
+        case 4:
+            bloom_lookup_kernel<4><<<lookup_grid<4>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
+            break;
+        case 8:
+            bloom_lookup_kernel<8><<<lookup_grid<8>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
+            break;
+        default:
+            bloom_lookup_kernel<16><<<lookup_grid<16>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                      plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
+    }
+    bloom_resolve_kernel<<<(unsigned)plan.tstride, 256, 0, s>>>(ws.kofs, rv.n, bv.K, eid, emiss, ws.miss);
+    bloom_count_kernel<<<blocks, 256, 0, s>>>(rv, ws.kofs, ws.miss, bv.K, hits, partials, bv.rows_read);
+    return hipGetLastError();
+}
+
+}  // namespace xs
