@@ -28,6 +28,8 @@
 // cases run through this path and the direct one).
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "xs_device.h"
 
 namespace xs {
@@ -72,7 +74,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
                                                                       uint32_t* __restrict__ eoff,
                                                                       uint16_t* __restrict__ eid,
                                                                       uint16_t* __restrict__ tbm,
-                                                                      const uint32_t* __restrict__ blk_read, int dbg) {
+                                                                      const uint32_t* __restrict__ blk_read) {
     using Scan = hipcub::BlockScan<uint32_t, kBucketThreads>;
     constexpr int ITEMS = kPartMax / kBucketThreads;
     constexpr int PER = kTK / kBucketThreads;  // k-mers per thread
@@ -145,8 +147,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
                     const uint64_t carry = nl < p;
                     sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
                     sl = nl;
-                    idx[q][j] = (dbg & 32) ? ((uint64_t)(i * 7 + j) * 2654435761ull) % bv.mbits
-                                           : fastmod(sh, bv.mbits, bv.magic);
+                    idx[q][j] = fastmod(sh, bv.mbits, bv.magic);
                     atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
                 }
             }
@@ -232,7 +233,7 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
                                                            uint64_t n, uint32_t K, uint32_t shift, uint32_t P,
                                                            uint64_t tstride, const uint32_t* __restrict__ eoff,
                                                            const uint16_t* __restrict__ tbl,
-                                                           uint8_t* __restrict__ emiss, uint32_t* qctr, int dbg) {
+                                                           uint8_t* __restrict__ emiss, uint32_t* qctr) {
     const int lane = threadIdx.x & 63;
     const uint64_t nblk = (kofs[n] + kTK - 1) / kTK;
     const uint64_t cap = (uint64_t)kTK * K;
@@ -279,13 +280,13 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
                 }
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
-                    off[u] = i0 + u * 64 + lane < total ? ((dbg & 4) ? (uint32_t)pos[u] * 97u & 0xFFFFFu : eoff[pos[u]]) : 0u;
+                    off[u] = i0 + u * 64 + lane < total ? eoff[pos[u]] : 0u;
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
-                    w[u] = i0 + u * 64 + lane < total ? ((dbg & 2) ? off[u] * 0x9E3779B1u : pb[off[u] >> 5]) : ~0u;
+                    w[u] = i0 + u * 64 + lane < total ? pb[off[u] >> 5] : ~0u;
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
-                    if (!((w[u] >> (off[u] & 31)) & 1u) && !(dbg & 1)) emiss[pos[u]] = 1;
+                    if (!((w[u] >> (off[u] & 31)) & 1u)) emiss[pos[u]] = 1;
             }
         }
         }
@@ -425,26 +426,26 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
     return plan->entry_bytes <= (24ull << 30);
 }
 
-// Timing experiments only (results are wrong when set): XSPECT2_AMD_BLOOM_DBG
-// bit 0 skips the miss stores, bit 1 the filter loads, bit 2 the entry loads,
-// bit 5 the bucket kernel's hashing (indices from the k-mer number instead).
-static int dbg_env() {
-    const char* e = getenv("XSPECT2_AMD_BLOOM_DBG");
-    return e ? atoi(e) : 0;
-}
+// Entries in flight per lane: 4 / 8 / 16 measured 10.67 / 10.59 / 10.44 ms per
+// config-2 step.  Blocks per CU: 3 (9.53 ms) beat the resident 5 (10.36 ms) and
+// 2 (9.60 ms): fewer waves keep more of each partition in L2.  Running the
+// bucket pass of sub-batch i+1 on a second stream beside the lookup of i
+// saved a further 0.1 ms only, and is not done.
+constexpr int kUnroll = 16;
+constexpr int kLookupPerCu = 3;
 
-static int lookup_unroll() {
-    const char* e = getenv("XSPECT2_AMD_BLOOM_UNROLL");
-    const int u = e ? atoi(e) : 16;
-    return (u == 4 || u == 8 || u == 16) ? u : 16;
-}
-
-template <int U>
 static int lookup_grid() {
     static std::atomic<int> cache{0};
     return cached_grid(cache, [] {
-        const int g = resident_grid(bloom_lookup_kernel<U>, 256, 0);
-        return g >= 8 ? g / 8 * 8 : 8;
+        int dev = 0;
+        hipDeviceProp_t prop;
+        int per_cu = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 768;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bloom_lookup_kernel<kUnroll>, 256, 0) !=
+                hipSuccess || per_cu < 1)
+            per_cu = 1;
+        const int g = std::min(per_cu, kLookupPerCu) * prop.multiProcessorCount;
+        return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
     });
 }
 
@@ -465,27 +466,16 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
     part_map_kernel<<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
     if (rv.k == 21 && bv.K == 7)
         bloom_bucket_kernel<21, 7><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
-            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read, dbg_env());
+            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read);
     else
         bloom_bucket_kernel<0, 0><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
-            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read, dbg_env());
+            rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read);
     part_transpose_kernel<<<dim3((unsigned)((plan.tstride + 63) / 64), (plan.P + 1 + 63) / 64), 256, 0, s>>>(
         tbm, plan.P + 1, plan.tstride, ws.tbl);
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
-    switch (lookup_unroll()) {
-        case 4:
-            bloom_lookup_kernel<4><<<lookup_grid<4>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
-            break;
-        case 8:
-            bloom_lookup_kernel<8><<<lookup_grid<8>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
-            break;
-        default:
-            bloom_lookup_kernel<16><<<lookup_grid<16>(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                      plan.tstride, eoff, ws.tbl, emiss, qctr, dbg_env());
-    }
+    bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                plan.tstride, eoff, ws.tbl, emiss, qctr);
     bloom_resolve_kernel<<<(unsigned)plan.tstride, 256, 0, s>>>(ws.kofs, rv.n, bv.K, eid, emiss, ws.miss);
     bloom_count_kernel<<<blocks, 256, 0, s>>>(rv, ws.kofs, ws.miss, bv.K, hits, partials, bv.rows_read);
     return hipGetLastError();
