@@ -98,6 +98,8 @@ def parse():
                     help="mlst: fraction of reads from outside every locus (WGS-like input: ~1.0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the PCIe-inclusive host-buffer runs (profiling: only full-size probe launches)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_traffic.json"))
@@ -364,7 +366,7 @@ def main():
 
     if wl.partitioned:
         traffic = None  # r01_traffic.json was measured on the gather path
-    host = host_path(wl, args)
+    host = None if args.no_host_path else host_path(wl, args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -12,7 +12,7 @@ for frac in 1.0 0.5 0.1; do
   done
 done
 rm -rf gpurun_out/bp_prof
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/bp_prof" -o bp -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload genus --no-cpu-baseline --steps 10 --warmup 3 > "$GRAFT_REPO_ROOT/gpurun_out/bp_prof.log" 2>&1 || { tail -20 "$GRAFT_REPO_ROOT/gpurun_out/bp_prof.log"; exit 7; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/bp_prof" -o bp -- python3 "$GRAFT_REPO_ROOT/bench.py" --workload genus --no-cpu-baseline --no-host-path --steps 10 --warmup 3 > "$GRAFT_REPO_ROOT/gpurun_out/bp_prof.log" 2>&1 || { tail -20 "$GRAFT_REPO_ROOT/gpurun_out/bp_prof.log"; exit 7; }
 cd "$GRAFT_REPO_ROOT" && python3 - <<'PY'
 import csv, glob
 rows = list(csv.DictReader(open(glob.glob('gpurun_out/bp_prof/*kernel_trace.csv')[0])))
