@@ -205,6 +205,32 @@ def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mod
     gb.close()
 
 
+@pytest.mark.parametrize("step", [1, 2])
+def test_bloom_partitioned_many_short_reads(xs, oracle_mod, monkeypatch, step):
+    """Bucket blocks spanning more reads than they stage in LDS (reads of
+    k..k+3 bytes: 1-4 k-mers each, so a 1024-k-mer block holds hundreds of
+    reads) take the global read search; mixed with empty and sub-k reads."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    rng = np.random.default_rng(31 + step)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genome = [acgt[rng.integers(0, 4, 20_000)].tobytes()]
+    bf = oracle_mod.BloomFilter(np.zeros(300_007, dtype=np.uint8), 7, 21)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(21, 300_007, 7)
+    gb.upload(bf.bits)
+    reads = []
+    for _ in range(6000):
+        L = int(rng.integers(15, 25))
+        st = int(rng.integers(0, 19_000))
+        reads.append(genome[0][st:st + L] if rng.random() < 0.6 else acgt[rng.integers(0, 4, L)].tobytes())
+    reads[100:140] = [b""] * 40
+    want_h, want_n = bf.query(reads, step=step)
+    got_h, got_n = gb.query(reads, step=step)
+    assert np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)
+    assert gb.probe_path() == 1
+    gb.close()
+
+
 def test_bloom_path_follows_member_fraction(xs, oracle_mod, monkeypatch):
     """Default mode on a 40 MiB filter: the first query takes the partitioned
     path; after a member-poor query (random reads) the next takes the gather
