@@ -337,6 +337,8 @@ def main():
         tot = t.cpu().numpy().view(np.uint64)
         want = wl.kmers * (world if args.workload != "multigenus" else 1)
         assert int(tot[-1]) == want, f"k-mer total {int(tot[-1])} != {want}"
+    if args.workload == "genus":  # member k-mers / sampled k-mers (steers the rbloom probe path)
+        wl.config["member_fraction"] = round(int(tot[0]) / max(1, int(tot[-1])), 4)
 
     value = wl.probes_per_step() * args.steps / elapsed
     from xspect2_amd._lib import XS_PATH_PARTITIONED

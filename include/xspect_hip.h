@@ -186,7 +186,7 @@ int xs_bank_probe_rows(xs_bank* bank, uint64_t* rows);
  * filter/row gather per hash, every bank kind) or XS_PATH_PARTITIONED (rbloom
  * filters of >= 16 MiB: k-mer bit indices binned by 1 MiB filter partition,
  * each partition tested from one XCD's L2).  The partitioned path is taken
- * while the handle's previous query found at least 35 % of its k-mers in the
+ * while the handle's previous query found at least 24 % of its k-mers in the
  * filter (member-rich input, where it is faster); XSPECT2_AMD_BLOOM_PART=0
  * disables it.  Both give identical results. */
 #define XS_PATH_GATHER 0

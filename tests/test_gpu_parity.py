@@ -142,10 +142,10 @@ def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
     gb2.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "2"])
+@pytest.mark.parametrize("mode", ["0", "3"])
 @pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
 def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode):
-    """mode 0: direct probe; mode 2: partitioned probe with small partitions."""
+    """mode 0: direct probe; mode 3: partitioned probe with small partitions."""
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
@@ -167,7 +167,7 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
     gb.close()
 
 
-@pytest.mark.parametrize("mode,k,K,nbytes", [("2", 21, 7, 200_003), ("2", 31, 5, 77_777), ("2", 16, 8, 1 << 20),
+@pytest.mark.parametrize("mode,k,K,nbytes", [("3", 21, 7, 200_003), ("3", 31, 5, 77_777), ("3", 16, 8, 1 << 20),
                                              ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099)])
 def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mode, k, K, nbytes):
     """The partitioned rbloom probe (k-mer bit indices binned by filter
@@ -210,7 +210,7 @@ def test_bloom_partitioned_many_short_reads(xs, oracle_mod, monkeypatch, step):
     """Bucket blocks spanning more reads than they stage in LDS (reads of
     k..k+3 bytes: 1-4 k-mers each, so a 1024-k-mer block holds hundreds of
     reads) take the global read search; mixed with empty and sub-k reads."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
     rng = np.random.default_rng(31 + step)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = [acgt[rng.integers(0, 4, 20_000)].tobytes()]

@@ -107,7 +107,7 @@ struct BloomPartWs {
 // batch too large for the transient workspace, member-poor input -- the
 // previous query's member fraction below kPartMinMembers -- or
 // XSPECT2_AMD_BLOOM_PART=0).
-constexpr double kPartMinMembers = 0.35;
+constexpr double kPartMinMembers = 0.24;  // measured crossover, profiles/r01_bloom_crossover.txt
 bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32_t step, double member_frac,
                      BloomPartPlan* plan);
 hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,

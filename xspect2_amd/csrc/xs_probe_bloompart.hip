@@ -380,9 +380,10 @@ __global__ void __launch_bounds__(256) bloom_count_kernel(ReadView rv, const uin
 }  // namespace
 
 // XSPECT2_AMD_BLOOM_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for filters of >= 16 partitions (16 MiB) on member-rich input; 2 = partitioned for every filter,
-// with partitions down to 1024 bits (tests reach many partitions on small
-// filters, whatever the input).  Read per call.
+// probe for filters of >= 16 partitions (16 MiB) on member-rich input; 2 =
+// partitioned for such filters whatever the input; 3 = partitioned for every
+// filter, with partitions down to 1024 bits (tests reach many partitions on
+// small filters).  Read per call.
 static int part_env() {
     const char* e = getenv("XSPECT2_AMD_BLOOM_PART");
     return e ? atoi(e) : 1;
@@ -402,10 +403,10 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
     if (mode <= 0 || bv.K == 0 || bv.K > (uint32_t)kPartKMax) return false;
     // member-poor input: the direct probe's early exit (2 bits first) wins
     if (mode == 1 && member_frac < kPartMinMembers) return false;
-    const uint32_t shift = part_shift(bv.mbits, mode >= 2 ? 10 : 23);
+    const uint32_t shift = part_shift(bv.mbits, mode >= 3 ? 10 : 23);
     const uint64_t P = (bv.mbits + (1ull << shift) - 1) >> shift;
     // small filters stay L2/MALL resident: the direct probe is faster there
-    const uint64_t min_parts = mode >= 2 ? 1 : 16;
+    const uint64_t min_parts = mode >= 3 ? 1 : 16;
     if (P < min_parts || shift > 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
     if (kbound >= (1ull << 32)) return false;
