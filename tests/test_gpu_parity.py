@@ -201,8 +201,73 @@ def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mod
         assert np.array_equal(got_h[:, 0], want_h), int((got_h[:, 0] != want_h).sum())
         tot, nk = gb.query_totals(reads, step=step)
         assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+        best, bh, bnk, btot = gb.query_best(reads, step=step, want_totals=True)
+        assert np.array_equal(bh, want_h) and np.array_equal(bnk, want_n)
+        assert int(btot[0]) == int(want_h.sum()) and int(btot[1]) == int(want_n.sum())
     assert 0 < int(want_h.sum()) < int(want_n.sum())
     gb.close()
+
+
+def test_bloom_partitioned_threads_and_torch_stream(xs, oracle_mod, monkeypatch):
+    """Partitioned probe from 4 host threads on one handle (serialised by its
+    mutex) and on a second handle at once, then through the device API on a
+    torch stream: every answer equals the oracle's."""
+    import threading
+
+    import torch
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    rng = np.random.default_rng(44)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genome = [acgt[rng.integers(0, 4, 80_000)].tobytes()]
+    nbytes = 20 << 20
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), 7, 21)
+    bf.build(genome)
+    banks = [xs.Bank.create_bloom(21, nbytes, 7) for _ in range(2)]
+    for b in banks:
+        b.upload(bf.bits)
+    sets = []
+    for t in range(6):
+        reads = [genome[0][s:s + 150] for s in rng.integers(0, 79_000, 3000)]
+        reads += _reads(rng, 500, 21, min_len=100, max_len=200)
+        sets.append((reads, bf.query(reads)))
+    errors = []
+
+    def work(b, items):
+        try:
+            for reads, (want_h, want_n) in items:
+                got_h, got_n = b.query(reads)
+                if not (np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)):
+                    errors.append("mismatch")
+                if b.probe_path() != 1:
+                    errors.append("path")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(banks[i % 2], sets[i::4])) for i in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    # device API on a torch stream
+    from xspect2_amd.packing import pack_sequences
+    reads, (want_h, want_n) = sets[0]
+    pr = pack_sequences(reads)
+    dev = torch.device("cuda", 0)
+    d_seq = torch.from_numpy(pr.buf.copy()).to(dev)
+    d_off = torch.from_numpy(pr.offsets.astype(np.int64)).to(dev)
+    d_hits = torch.empty((pr.n, 1), dtype=torch.int32, device=dev)
+    d_nk = torch.empty(pr.n, dtype=torch.int64, device=dev)
+    d_tot = torch.zeros(2, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    banks[0].query_device(d_seq, d_seq.numel(), d_off, pr.n, 1, d_hits, d_nk, d_tot, stream=st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(d_hits.cpu().numpy()[:, 0].astype(np.uint32), want_h)
+    assert np.array_equal(d_nk.cpu().numpy().astype(np.uint64), want_n)
+    assert int(d_tot[0]) == int(want_h.sum()) and int(d_tot[1]) == int(want_n.sum())
+    assert banks[0].probe_path() == 1
+    for b in banks:
+        b.close()
 
 
 @pytest.mark.parametrize("step", [1, 2])
