@@ -12,6 +12,7 @@
 //          same partition at once.
 // Reports ms and GB/s of streamed bytes (entries + results + rows once).
 //   hipcc -O3 --offload-arch=gfx950 tools/partgather.hip -o tools/partgather
+//   tools/partgather [entries] [P] [blocks per CU]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -79,6 +80,7 @@ int main(int argc, char** argv) {
     const uint64_t nrows = 38371628;                     // config-2 bank rows
     const uint64_t nent = argc > 1 ? strtoull(argv[1], 0, 10) : 910000000ull;
     const int P = argc > 2 ? atoi(argv[2]) : 256;
+    const int per_cu = argc > 3 ? atoi(argv[3]) : 8;  // blocks per CU
     hipDeviceProp_t prop;
     CHK(hipGetDeviceProperties(&prop, 0));
     const int cus = prop.multiProcessorCount;
@@ -147,9 +149,9 @@ int main(int argc, char** argv) {
             CHK(hipMemset(d_cnt, 0, 32));
             CHK(hipEventRecord(a));
             if (xcd)
-                gather<true><<<cus * 8, 256>>>(rows, ent, d_ps, d_r0, P, d_items, d_list, d_off, d_pref, d_cnt, out);
+                gather<true><<<cus * per_cu, 256>>>(rows, ent, d_ps, d_r0, P, d_items, d_list, d_off, d_pref, d_cnt, out);
             else
-                gather<false><<<cus * 8, 256>>>(rows, ent, d_ps, d_r0, P, d_items, d_list, d_off, d_pref, d_cnt, out);
+                gather<false><<<cus * per_cu, 256>>>(rows, ent, d_ps, d_r0, P, d_items, d_list, d_off, d_pref, d_cnt, out);
             CHK(hipEventRecord(b));
             CHK(hipEventSynchronize(b));
             float ms;
@@ -157,8 +159,8 @@ int main(int argc, char** argv) {
             if (ms < best) best = ms;
         }
         const double bytes = nent * 20.0 + nrows * 16.0;
-        printf("{\"order\": \"%s\", \"P\": %d, \"entries\": %llu, \"ms\": %.3f, \"GBps\": %.0f, \"Gentries_per_s\": %.1f}\n",
-               xcd ? "xcd" : "flat", P, (unsigned long long)nent, best, bytes / best / 1e6, nent / best / 1e6);
+        printf("{\"order\": \"%s\", \"P\": %d, \"blocks_per_cu\": %d, \"entries\": %llu, \"ms\": %.3f, \"GBps\": %.0f, \"Gentries_per_s\": %.1f}\n",
+               xcd ? "xcd" : "flat", P, per_cu, (unsigned long long)nent, best, bytes / best / 1e6, nent / best / 1e6);
         hipFree(d_ps); hipFree(d_r0); hipFree(d_items); hipFree(d_list); hipFree(d_off); hipFree(d_pref); hipFree(d_cnt);
     };
     run(true);
