@@ -344,7 +344,7 @@ def main():
     from xspect2_amd._lib import XS_PATH_PARTITIONED
     wl.partitioned = args.workload == "genus" and wl.banks[0].probe_path() == XS_PATH_PARTITIONED
     if wl.partitioned:
-        wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 1 MiB filter partition) -> "
+        wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 2 MiB filter partition) -> "
                      "bloom_lookup (per-XCD L2-resident partition) -> resolve -> count")
         wl.row_bytes = None
         wl.roofline_note = ("streamed bytes of the partitioned pipeline (13 B per filter bit tested + filter + "

@@ -184,7 +184,7 @@ int xs_bank_probe_rows(xs_bank* bank, uint64_t* rows);
 
 /* Probe path of the last query on this handle: XS_PATH_GATHER (one random
  * filter/row gather per hash, every bank kind) or XS_PATH_PARTITIONED (rbloom
- * filters of >= 16 MiB: k-mer bit indices binned by 1 MiB filter partition,
+ * filters of >= 16 MiB: k-mer bit indices binned by 2 MiB filter partition,
  * each partition tested from one XCD's L2).  The partitioned path is taken
  * while the handle's previous query found at least 24 % of its k-mers in the
  * filter (member-rich input, where it is faster); XSPECT2_AMD_BLOOM_PART=0

@@ -8,8 +8,8 @@
 //   counts  : per read k-mer count, exclusive scan -> global k-mer id g
 //   bucket  : one block per 1024 k-mers: canonical k-mer, XXH3-64, the K
 //             LCG bit indices (exactly as probe_bloom_kernel, kept in
-//             registers), each binned by filter partition (1 MiB of filter =
-//             2^23 bits, or larger for filters > 1 GiB) with LDS counters, a
+//             registers), each binned by filter partition (2 MiB of filter =
+//             2^24 bits; smaller for filters under 128 MiB, larger over 2 GiB) with LDS counters, a
 //             block scan and LDS-sorted placement.  The block copies its
 //             entries (u32 bit offset in the partition, u16 k-mer id)
 //             partition-ordered into its own region with coalesced stores and
@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(256) bloom_count_kernel(ReadView rv, const uin
 }  // namespace
 
 // XSPECT2_AMD_BLOOM_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for filters of >= 16 partitions (16 MiB) on member-rich input; 2 =
+// probe for filters of >= 16 MiB on member-rich input; 2 =
 // partitioned for such filters whatever the input; 3 = partitioned for every
 // filter, with partitions down to 1024 bits (tests reach many partitions on
 // small filters).  Read per call.
@@ -389,11 +389,15 @@ static int part_env() {
     return e ? atoi(e) : 1;
 }
 
-// Partition shift for a filter of `mbits` bits: 2^23-bit (1 MiB) partitions,
-// doubled until at most kPartMax of them cover the filter.
-static uint32_t part_shift(uint64_t mbits, uint32_t min_shift) {
-    uint32_t s = min_shift;
-    while (((mbits + (1ull << s) - 1) >> s) > kPartMax) ++s;
+// Partition shift for a filter of `mbits` bits: 2^24-bit (2 MiB) partitions
+// (2 MiB: 8.92 ms per config-2 step; 1 MiB 9.31, 512 KiB 10.86, 4 MiB 10.00),
+// halved down to 2^20 bits while that leaves fewer than 64 partitions (8 per
+// XCD keep the XCDs evenly loaded), doubled while more than kPartMax.
+static uint32_t part_shift(uint64_t mbits, uint32_t pref, uint32_t floor) {
+    auto parts = [mbits](uint32_t s) { return (mbits + (1ull << s) - 1) >> s; };
+    uint32_t s = pref;
+    while (s > floor && parts(s) < 64) --s;
+    while (parts(s) > kPartMax) ++s;
     return s;
 }
 
@@ -403,11 +407,10 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
     if (mode <= 0 || bv.K == 0 || bv.K > (uint32_t)kPartKMax) return false;
     // member-poor input: the direct probe's early exit (2 bits first) wins
     if (mode == 1 && member_frac < kPartMinMembers) return false;
-    const uint32_t shift = part_shift(bv.mbits, mode >= 3 ? 10 : 23);
+    const uint32_t shift = mode >= 3 ? part_shift(bv.mbits, 10, 10) : part_shift(bv.mbits, 24, 20);
     const uint64_t P = (bv.mbits + (1ull << shift) - 1) >> shift;
-    // small filters stay L2/MALL resident: the direct probe is faster there
-    const uint64_t min_parts = mode >= 3 ? 1 : 16;
-    if (P < min_parts || shift > 32) return false;
+    // filters under 16 MiB stay L2/MALL resident: the direct probe is faster there
+    if ((mode < 3 && bv.mbits < (128ull << 20)) || shift > 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
     if (kbound >= (1ull << 32)) return false;
     const uint64_t nblk = (kbound + kTK - 1) / kTK;
