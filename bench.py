@@ -366,8 +366,14 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:
-        traffic = None  # r01_traffic.json was measured on the gather path
+    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu_pmc_traffic_part.sh)
+        traffic = None
+        try:
+            tp = json.loads(tj.read_text()).get("genus_partitioned") or {}
+            if tp.get("reads") == wl.n:
+                traffic = tp.get("hbm_bytes_per_step")
+        except Exception:
+            traffic = None
     host = None if args.no_host_path else host_path(wl, args)
 
     cpu = None
