@@ -168,7 +168,8 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
 
 
 @pytest.mark.parametrize("mode,k,K,nbytes", [("3", 21, 7, 200_003), ("3", 31, 5, 77_777), ("3", 16, 8, 1 << 20),
-                                             ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099)])
+                                             ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099),
+                                             ("3", 21, 10, 100_003)])  # K > 8: gather path
 def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mode, k, K, nbytes):
     """The partitioned rbloom probe (k-mer bit indices binned by filter
     partition, per-partition lookup, per-read count) against the oracle:
