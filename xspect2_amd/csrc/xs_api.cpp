@@ -498,16 +498,20 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         HIPCHK(hipEventRecord(b->events[b->events_used].first, s));
     }
     BloomPartPlan plan;
-    b->last_path = XS_PATH_GATHER;
-    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.seq_bytes, step, b->member_frac, &plan)) {
-        b->last_path = XS_PATH_PARTITIONED;
-        if (int rc = b->pk_nkc.ensure(plan.nkc_bytes)) return rc;
-        if (int rc = b->pk_kofs.ensure(plan.nkc_bytes)) return rc;
-        if (int rc = b->pk_scan.ensure(plan.scan_bytes)) return rc;
-        if (int rc = b->pk_entries.ensure(plan.entry_bytes)) return rc;
-        if (int rc = b->pk_tbl.ensure(plan.tbl_bytes)) return rc;
-        if (int rc = b->pk_miss.ensure(plan.miss_bytes)) return rc;
-        if (int rc = b->pk_aux.ensure(plan.aux_bytes)) return rc;
+    int path = XS_PATH_GATHER;
+    // The partitioned path's workspace is transient: when HBM cannot hold it,
+    // the query takes the gather path instead of failing.
+    auto part_ws = [&]() -> bool {
+        if (b->pk_nkc.ensure(plan.nkc_bytes) || b->pk_kofs.ensure(plan.nkc_bytes) ||
+            b->pk_scan.ensure(plan.scan_bytes) || b->pk_entries.ensure(plan.entry_bytes) ||
+            b->pk_tbl.ensure(plan.tbl_bytes) || b->pk_miss.ensure(plan.miss_bytes) || b->pk_aux.ensure(plan.aux_bytes)) {
+            (void)hipGetLastError();
+            return false;
+        }
+        return true;
+    };
+    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.seq_bytes, step, b->member_frac, &plan) && part_ws()) {
+        path = XS_PATH_PARTITIONED;
         const BloomPartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                              b->pk_entries.as<uint64_t>(), b->pk_tbl.as<uint16_t>(), b->pk_miss.as<uint32_t>(),
                              b->pk_aux.as<uint32_t>()};
@@ -517,6 +521,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     } else {
         HIPCHK(launch_probe_cobs(rv, b->cobs_view(), d_hits, partials, blocks, s));
     }
+    b->last_path = path;
     if (b->profiling) {
         HIPCHK(hipEventRecord(b->events[b->events_used].second, s));
         ++b->events_used;
@@ -1111,6 +1116,7 @@ int xs_bank_probe_rows(xs_bank* b, uint64_t* rows) {
 
 int xs_bank_probe_path(const xs_bank* b, int* path) {
     if (!b || !path) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);  // after any query in flight on the handle
     *path = b->last_path;
     return XS_OK;
 }
