@@ -8,9 +8,9 @@
 //   counts  : per read k-mer count, exclusive scan -> global k-mer id g
 //   bucket  : one block per 1024 k-mers: canonical k-mer, XXH3-64, the K
 //             LCG bit indices (exactly as probe_bloom_kernel, kept in
-//             registers), each binned by filter partition (2 MiB of filter =
-//             2^24 bits; smaller for filters under 128 MiB, larger over 2 GiB) with LDS counters, a
-//             block scan and LDS-sorted placement.  The block copies its
+//             registers), each binned by filter partition (2 MiB of
+//             filter = 2^24 bits; smaller under 128 MiB, larger over 2 GiB)
+//             with LDS counters, a block scan and LDS-sorted placement.  The block copies its
 //             entries (u32 bit offset in the partition, u16 k-mer id)
 //             partition-ordered into its own region with coalesced stores and
 //             one u16 start per partition into a partition-major table.
@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256) part_transpose_kernel(const uint16_t* __r
 // bytes stay in the XCD's 4 MiB L2 while the entries stream past), taking
 // groups of 64 bucket blocks from the partition's queue counter.  A queue
 // self-balances: with a static deal the wave scheduler lets some waves run
-// partitions ahead and the L2 hit rate fell from 84 % to 44 %.  Each counter
+// partitions ahead and the L2 hit rate fell from 86 % to 44 %.  Each counter
 // sits on its own 128-B line (a line's atomics are serialised at the memory
 // side).  Every lane keeps kLookupUnroll entries in flight.
 constexpr uint32_t kQStride = 32;  // u32 per queue counter
