@@ -58,6 +58,21 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t x, uint64_t d, uint64_t m) 
     return r >= d ? r - d : r;
 }
 
+// One step of the 128-bit LCG (state sh:sl): state = state * M + C mod 2^128.
+// sl * Ml is formed once from four 32 x 32 partial products and gives both
+// the low word and the carry into the high word.
+__device__ __forceinline__ void lcg_step(uint64_t& sl, uint64_t& sh) {
+    constexpr uint64_t ml = (uint32_t)kLcgMl, mh = kLcgMl >> 32;
+    const uint64_t al = (uint32_t)sl, ah = sl >> 32;
+    const uint64_t ll = al * ml, lh = al * mh, hl = ah * ml, hh = ah * mh;
+    const uint64_t mid = (ll >> 32) + (uint32_t)lh + (uint32_t)hl;  // < 3 * 2^32
+    const uint64_t plo = (mid << 32) | (uint32_t)ll;
+    const uint64_t phi = hh + (lh >> 32) + (hl >> 32) + (mid >> 32);
+    const uint64_t nl = plo + kLcgCl;
+    sh = sh * kLcgMl + sl * kLcgMh + phi + kLcgCh + (nl < plo);
+    sl = nl;
+}
+
 // Canonical k-mer, held as 8 little-endian dwords (bytes >= k are zero) + a
 // zero guard word.
 struct Kmer {

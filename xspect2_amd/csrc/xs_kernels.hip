@@ -69,11 +69,7 @@ __device__ __forceinline__ uint32_t bloom_member(const Kmer& c, uint32_t k, cons
 #pragma unroll
     for (int j = 0; j < NK; ++j) {
         if ((uint32_t)j < K) {
-            const uint64_t p = sl * kLcgMl;
-            const uint64_t nl = p + kLcgCl;
-            const uint64_t carry = nl < p;
-            sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
-            sl = nl;
+            lcg_step(sl, sh);
             idx[j] = fastmod(sh, bv.mbits, bv.magic);
         }
     }
@@ -226,11 +222,7 @@ __global__ void __launch_bounds__(kProbeThreads) build_bloom_kernel(ReadView rv,
                 kmer_at<KT, kKmerBio>(rv, o0, len, t0 + tb + lane, k, c);
                 uint64_t sl = xxh3_kmer<KT>(c, k), sh = 0;
                 for (uint32_t j = 0; j < bv.K; ++j) {
-                    const uint64_t pm = sl * kLcgMl;
-                    const uint64_t nl = pm + kLcgCl;
-                    const uint64_t carry = nl < pm;
-                    sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
-                    sl = nl;
+                    lcg_step(sl, sh);
                     const uint64_t idx = fastmod(sh, bv.mbits, bv.magic);
                     atomicOr(&bits[idx >> 5], 1u << (idx & 31));
                 }

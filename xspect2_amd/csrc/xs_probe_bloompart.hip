@@ -142,11 +142,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
 #pragma unroll
             for (int j = 0; j < NK; ++j) {
                 if ((uint32_t)j < K) {
-                    const uint64_t p = sl * kLcgMl;
-                    const uint64_t nl = p + kLcgCl;
-                    const uint64_t carry = nl < p;
-                    sh = sh * kLcgMl + sl * kLcgMh + __umul64hi(sl, kLcgMl) + kLcgCh + carry;
-                    sl = nl;
+                    lcg_step(sl, sh);
                     idx[q][j] = fastmod(sh, bv.mbits, bv.magic);
                     atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
                 }
