@@ -226,6 +226,14 @@ __device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
 }
 __device__ __forceinline__ uint32_t bytes_equal(uint32_t x, uint32_t c) { return zero_bytes(x ^ (c * 0x01010101u)); }
 
+// 0x80 in every byte of x that is A, C, G, T or N.  Their low 3 bits (1, 3,
+// 7, 4, 6) are distinct, so v_perm_b32 looks up the one byte each could be
+// in an 8-byte table {-, 'A', -, 'C', 'T', -, 'N', 'G'} (- = 0xFF, which no
+// byte with those low bits equals) and the byte must equal its entry.
+__device__ __forceinline__ uint32_t acgtn_bytes(uint32_t x) {
+    return zero_bytes(__builtin_amdgcn_perm(0x474EFF54u, 0x43FF41FFu, x & 0x07070707u) ^ x);
+}
+
 // COBS normalisation of 4 bytes.  (b & 0xDF) is one of A/C/G/T only for
 // A/C/G/T/a/c/g/t, so the upper-cased test is exact.
 __device__ __forceinline__ uint32_t cobs_norm4(uint32_t x) {
@@ -404,8 +412,7 @@ __device__ __forceinline__ void kmer_at(const ReadView& rv, uint64_t o0, uint64_
         for (int i = 0; i < 8; ++i) {
             const uint32_t m = tail_mask(i, kk);
             f[i] &= m;
-            const uint32_t ok = bytes_equal(f[i], 'A') | bytes_equal(f[i], 'C') | bytes_equal(f[i], 'G') |
-                                bytes_equal(f[i], 'T') | bytes_equal(f[i], 'N');
+            const uint32_t ok = acgtn_bytes(f[i]);
             fast = fast && ((ok | ~m) & 0x80808080u) == 0x80808080u;
         }
         if (fast) {
