@@ -34,7 +34,11 @@
  * failure on the calling thread.  Host buffers are borrowed for the duration of
  * the call only.  A bank handle owns its device memory and one HIP stream;
  * calls on one handle are serialised by an internal mutex, distinct handles are
- * independent.  No callbacks into the caller.
+ * independent.  The handle's device workspace is shared by all its calls: a
+ * call enqueued on a different stream than the handle's previous call (the
+ * *_device entry points take the caller's stream) is ordered after that call
+ * on the device, so one handle may be used from several streams.  No
+ * callbacks into the caller.
  */
 #ifndef XSPECT_HIP_H
 #define XSPECT_HIP_H

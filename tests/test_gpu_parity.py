@@ -167,6 +167,37 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
     gb.close()
 
 
+@pytest.mark.parametrize("mode", ["0", "3"])
+@pytest.mark.parametrize("k", [21, 31])
+def test_bloom_single_odd_byte_at_every_window_position(xs, oracle_mod, monkeypatch, k, mode):
+    """Uppercase ACGT reads with one N, lower-case or IUPAC byte: the read is
+    2k-1 long with the odd byte in the middle, so its k windows hold that byte
+    at every window position 0..k-1.  Windows with an N take the permute
+    complement, the others the per-byte Biopython table; half the reads are in
+    the filter, so hits are non-trivial.  Both probe paths."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
+    rng = np.random.default_rng(k + 5)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    odd = b"NnacgtRYKMSWBDHVXU-*."
+    reads = []
+    for rep in range(4):
+        for c in odd:
+            r = bytearray(acgt[rng.integers(0, 4, 2 * k - 1)].tobytes())
+            r[k - 1] = c
+            reads.append(bytes(r))
+    members = reads[::2]
+    bf = oracle_mod.BloomFilter(np.zeros(50_021, dtype=np.uint8), 7, k)
+    bf.build(members)
+    gb = xs.Bank.create_bloom(k, 50_021, 7)
+    gb.build(members)
+    assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
+    want_h, want_n = bf.query(reads)
+    got_h, got_n = gb.query(reads)
+    assert np.array_equal(got_n, want_n)
+    assert np.array_equal(got_h[:, 0], want_h)
+    assert int(want_h[::2].sum()) == k * len(members)  # every window of a member read is a member
+
+
 @pytest.mark.parametrize("mode,k,K,nbytes", [("3", 21, 7, 200_003), ("3", 31, 5, 77_777), ("3", 16, 8, 1 << 20),
                                              ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099),
                                              ("3", 21, 10, 100_003)])  # K > 8: gather path
@@ -362,6 +393,64 @@ def test_device_api_with_torch_stream(xs, oracle_mod):
     tot = d_tot.cpu().numpy().view(np.uint64)
     assert np.array_equal(tot[:100], want_h.sum(axis=0, dtype=np.uint64))
     assert int(tot[100]) == int(want_n.sum())
+    gb.close()
+
+
+@pytest.mark.parametrize("kind", ["cobs", "bloom"])
+def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
+    """Queries on one handle from two torch streams and the handle's own host
+    API, back to back with no synchronisation in between and growing batches
+    (the shared workspace is reallocated mid-sequence): the library orders
+    each call after the previous one on the device, so every answer equals
+    the oracle's."""
+    torch = pytest.importorskip("torch")
+    from xspect2_amd.packing import pack_sequences
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    rng = np.random.default_rng(77)
+    if kind == "cobs":
+        ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)
+        src = seqs
+        cols = 100
+    else:
+        acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+        src = [acgt[rng.integers(0, 4, 60_000)].tobytes()]
+        ob = oracle_mod.BloomFilter(np.zeros(20 << 20, dtype=np.uint8), 7, 21)
+        ob.build(src)
+        gb = xs.Bank.create_bloom(21, 20 << 20, 7)
+        gb.upload(ob.bits)
+        cols = 1
+    dev = torch.device("cuda", 0)
+    streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+    jobs = []
+    for i, n in enumerate([200, 3000, 500, 12_000, 800, 20_000]):
+        reads = []
+        for _ in range(n):
+            g = src[int(rng.integers(0, len(src)))]
+            st = int(rng.integers(0, max(1, len(g) - 160)))
+            reads.append(g[st:st + int(rng.integers(21, 160))])
+        reads += _reads(rng, n // 4, 21, min_len=0, max_len=200)
+        pr = pack_sequences(reads)
+        d_seq = torch.from_numpy(pr.buf[:max(1, int(pr.offsets[-1]))].copy()).to(dev)
+        d_off = torch.from_numpy(pr.offsets.astype(np.int64)).to(dev)
+        d_hits = torch.empty((pr.n, cols), dtype=torch.int32, device=dev)
+        d_nk = torch.empty(pr.n, dtype=torch.int64, device=dev)
+        jobs.append((reads, pr, d_seq, d_off, d_hits, d_nk))
+    torch.cuda.synchronize()
+    host = []
+    for i, (reads, pr, d_seq, d_off, d_hits, d_nk) in enumerate(jobs):
+        gb.query_device(d_seq, int(pr.offsets[-1]), d_off, pr.n, 1, d_hits, d_nk, None,
+                        stream=streams[i % 2].cuda_stream)
+        if i == 2:  # the handle's own stream in between, still no sync of the caller's
+            host.append((jobs[0][0], gb.query(jobs[0][0])))
+    torch.cuda.synchronize()
+    host.append((jobs[3][0], gb.query(jobs[3][0])))
+    for reads, pr, d_seq, d_off, d_hits, d_nk in jobs:
+        want_h, want_n = ob.query(reads)
+        assert np.array_equal(d_nk.cpu().numpy().view(np.uint64), want_n)
+        assert np.array_equal(d_hits.cpu().numpy().view(np.uint32).reshape(-1), want_h.reshape(-1))
+    for reads, (got_h, got_n) in host:
+        want_h, want_n = ob.query(reads)
+        assert np.array_equal(got_n, want_n) and np.array_equal(got_h.reshape(-1), want_h.reshape(-1))
     gb.close()
 
 

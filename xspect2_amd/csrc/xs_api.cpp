@@ -67,7 +67,12 @@ struct DevBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return XS_OK;
-        if (p) (void)hipFree(p);
+        if (p) {
+            // Growth only: work queued earlier on any stream (a device query on
+            // the caller's stream) may still read the old buffer.
+            (void)hipDeviceSynchronize();
+            (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
         size_t want = bytes < 256 ? 256 : bytes;
@@ -156,6 +161,12 @@ struct xs_bank {
     hipEvent_t hstage_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr, d2h_stream = nullptr;
     std::vector<hipEvent_t> chunk_ev;  // probe of batch chunk i done
+    // The workspace above is shared by every query and build on the handle.  A
+    // call enqueued on a different stream than the previous one waits for that
+    // one's work on the device (ws_ev), so callers may mix streams freely.
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_stream = nullptr;
+    bool ws_used = false;
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
@@ -195,6 +206,19 @@ struct xs_bank {
 };
 
 namespace {
+
+// Order the handle's next enqueue on stream s after its previous one.
+int ws_enter(xs_bank* b, hipStream_t s) {
+    if (b->ws_used && b->ws_stream != s) HIPCHK(hipStreamWaitEvent(s, b->ws_ev, 0));
+    return XS_OK;
+}
+int ws_leave(xs_bank* b, hipStream_t s) {
+    if (!b->ws_ev) HIPCHK(hipEventCreateWithFlags(&b->ws_ev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(b->ws_ev, s));
+    b->ws_stream = s;
+    b->ws_used = true;
+    return XS_OK;
+}
 
 int validate_geometry(xs_bank* b) {
     if (b->k < 1 || b->k > kMaxK)
@@ -262,6 +286,7 @@ int upload_payload(xs_bank* b, const void* host, uint64_t nbytes) {
         return fail(XS_ERR_ARG, "payload of %llu bytes, bank expects %llu",
                     (unsigned long long)nbytes, (unsigned long long)b->payload_bytes());
     HIPCHK(hipSetDevice(b->device));
+    if (int rc = ws_enter(b, b->stream)) return rc;
     if (b->kind == XS_BANK_RBLOOM) {
         HIPCHK(hipMemcpyAsync(b->image.p, host, nbytes, hipMemcpyHostToDevice, b->stream));
     } else if (b->pitch == b->page) {
@@ -281,6 +306,7 @@ int download_payload(xs_bank* b, void* host, uint64_t nbytes) {
         return fail(XS_ERR_ARG, "buffer of %llu bytes, payload is %llu",
                     (unsigned long long)nbytes, (unsigned long long)b->payload_bytes());
     HIPCHK(hipSetDevice(b->device));
+    if (int rc = ws_enter(b, b->stream)) return rc;
     if (b->kind == XS_BANK_RBLOOM || b->pitch == b->page) {
         HIPCHK(hipMemcpyAsync(host, b->image.p, nbytes, hipMemcpyDeviceToHost, b->stream));
     } else {
@@ -469,6 +495,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
     if (in.n >= (1ull << 31)) return fail(XS_ERR_ARG, "at most 2^31-1 reads per call");
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    if (int rc = ws_enter(b, s)) return rc;
     ReadView rv;
     if (int rc = prepare_units(b, in, step, d_nk, d_hits, cols, s, &rv)) return rc;
     const int blocks = probe_grid(b);
@@ -536,7 +563,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         HIPCHK(hipEventRecord(b->bloom_ev, s));
         b->bloom_pending = true;
     }
-    return XS_OK;
+    return ws_leave(b, s);
 }
 
 // Copy host reads to the handle's device buffers (offsets rebased to 0).
@@ -844,6 +871,7 @@ int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32
 }
 
 static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipStream_t s) {
+    if (int rc = ws_enter(b, s)) return rc;
     ReadView rv;
     if (int rc = prepare_units(b, in, 1, nullptr, nullptr, 0, s, &rv)) return rc;
     const int blocks = probe_grid(b);
@@ -851,7 +879,7 @@ static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipSt
         HIPCHK(launch_build_bloom(rv, b->bloom_view(), b->image.as<uint32_t>(), blocks, s));
     else
         HIPCHK(launch_build_cobs(rv, d_doc, b->cobs_view(), b->image.as<uint32_t>(), blocks, s));
-    return XS_OK;
+    return ws_leave(b, s);
 }
 
 int xs_bank_build(xs_bank* b, const char* seqs, const uint64_t* offsets, const uint32_t* rec_doc,
@@ -1074,6 +1102,7 @@ int xs_mlst_sum(xs_bank* b, const uint32_t* hits, const uint32_t* seq_of_chunk, 
     for (uint64_t c = 0; c < n_chunks; ++c)
         if (seq_of_chunk[c] >= n_seqs) return fail(XS_ERR_ARG, "seq_of_chunk[%llu] out of range", (unsigned long long)c);
     if (n_seqs == 0) return XS_OK;
+    if (int rc = ws_enter(b, b->stream)) return rc;
     if (int rc = b->hits.ensure(n_chunks * D * 4 + 4)) return rc;
     if (int rc = b->tmp.ensure(n_chunks * 4 + 4)) return rc;
     if (int rc = b->totals.ensure(n_seqs * D * 8)) return rc;
@@ -1155,6 +1184,8 @@ int xs_bank_probe_stats(xs_bank* b, uint64_t* count, double* total_ms, float* ma
 void xs_bank_close(xs_bank* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
+    if (b->ws_used) (void)hipEventSynchronize(b->ws_ev);  // the last call's stream may be the caller's
+    if (b->ws_ev) (void)hipEventDestroy(b->ws_ev);
     if (b->stream) (void)hipStreamSynchronize(b->stream);
     for (hipStream_t st : {b->copy_stream, b->d2h_stream})
         if (st) (void)hipStreamSynchronize(st);

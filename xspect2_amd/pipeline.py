@@ -24,6 +24,7 @@ the same names and the same bytes:
 """
 from __future__ import annotations
 
+import os
 import uuid
 from pathlib import Path
 
@@ -76,11 +77,42 @@ class _Collector:
         return MatrixResult(slug, self.ids, labels, hits.reshape(-1, D), nk, sparse_sampling_step=step, **kw)
 
 
+def _partial(fasta_out: Path) -> Path:
+    """Where a file's filtered FASTA is written until its pass completes (its
+    name ends in no FASTA/FASTQ ending, so a directory glob never sees it)."""
+    return fasta_out.with_name(fasta_out.name + ".partial")
+
+
+def _short_read_error() -> ValueError:
+    return ValueError("Invalid sequence, must be longer than k")
+
+
 def _fused_file(path: Path, genus, species, threshold: float, step: int, fasta_out: Path,
                 batch_bytes: int | None, display_names: bool):
     """One parse of `path`: genus result (all reads), species result (kept
     reads), filtered FASTA.  Returns (genus MatrixResult, species MatrixResult
-    or None, records written)."""
+    or None, records written, species error or None).
+
+    Side effects follow the reference's order (main.py:93-160): genus predict
+    covers the whole file before anything is written, so a read of length
+    <= genus.k raises with no filtered FASTA left behind; the filtered FASTA
+    is complete before species predict runs, so a kept read of length
+    <= species.k does not stop the genus pass or the FASTA - its ValueError is
+    returned and raised by run_pipeline where classify_species would raise it."""
+    partial = _partial(fasta_out)
+    try:
+        gres, sres, written, serr = _fused_pass(path, genus, species, threshold, step, partial, batch_bytes,
+                                                display_names)
+    except BaseException:
+        partial.unlink(missing_ok=True)
+        raise
+    if written:
+        os.replace(partial, fasta_out)
+    return gres, sres, written, serr
+
+
+def _fused_pass(path: Path, genus, species, threshold: float, step: int, fasta_out: Path,
+                batch_bytes: int | None, display_names: bool):
     import torch
 
     gbank, sbank = genus.bf, species.index
@@ -92,10 +124,11 @@ def _fused_file(path: Path, genus, species, threshold: float, step: int, fasta_o
     D = sbank.num_docs
     gcol, scol = _Collector(), _Collector()
     written = 0
+    serr = None
     for b in read_batches(path, batch_bytes, pinned=True):
         L = b.lengths()
         if (L <= genus.k).any():  # genus predict on every read (:224-225)
-            raise ValueError("Invalid sequence, must be longer than k")
+            raise _short_read_error()
         n = b.n
         nbytes = int(b.packed.offsets[-1])
         d_seq = torch.from_numpy(b.packed.buf[:max(nbytes, 1)]).to(dev, non_blocking=True)
@@ -112,8 +145,13 @@ def _fused_file(path: Path, genus, species, threshold: float, step: int, fasta_o
         m = int(idx.size)
         if not m:
             continue
-        if (L[idx] <= species.k).any():  # species predict on the kept reads
-            raise ValueError("Invalid sequence, must be longer than k")
+        fasta_out.parent.mkdir(parents=True, exist_ok=True)
+        b.write_fasta(fasta_out, idx, append=written > 0)
+        written += m
+        if serr is None and (L[idx] <= species.k).any():  # species predict on the kept reads
+            serr = _short_read_error()
+        if serr is not None:
+            continue
         out_off = np.zeros(m + 1, dtype=np.uint64)
         np.cumsum(L[idx], out=out_off[1:])
         mbytes = int(out_off[-1])
@@ -127,9 +165,6 @@ def _fused_file(path: Path, genus, species, threshold: float, step: int, fasta_o
         sh = d_sh.cpu().numpy().view(np.uint32)
         snk = d_snk.cpu().numpy().view(np.uint64)
         scol.add([ids[i] for i in idx.tolist()], sh, snk)
-        fasta_out.parent.mkdir(parents=True, exist_ok=True)
-        b.write_fasta(fasta_out, idx, append=written > 0)
-        written += m
     gres = gcol.result(genus.slug(), genus._labels(False), step)
     if len(set(gres.ids)) != len(gcol.ids):
         # duplicate read ids: the reference filters by id over the whole file
@@ -137,9 +172,9 @@ def _fused_file(path: Path, genus, species, threshold: float, step: int, fasta_o
         return _by_id_fallback(path, genus, species, gres, threshold, step, fasta_out, batch_bytes,
                                display_names)
     sres = None
-    if written:
+    if written and serr is None:
         sres = scol.result(species.slug(), species._labels(display_names), step)
-    return gres, sres, written
+    return gres, sres, written, serr
 
 
 def _by_id_fallback(path, genus, species, gres, threshold, step, fasta_out, batch_bytes, display_names):
@@ -149,6 +184,7 @@ def _by_id_fallback(path, genus, species, gres, threshold, step, fasta_out, batc
 
     included = {rid for rid, keep in zip(gres.ids, keep_mask(gres.hits[:, 0], gres.num_kmers, threshold)) if keep}
     written = 0
+    serr = None
     scol = _Collector()
     for b in read_batches(path, batch_bytes):
         ids = b.ids()
@@ -157,14 +193,18 @@ def _by_id_fallback(path, genus, species, gres, threshold, step, fasta_out, batc
             continue
         fasta_out.parent.mkdir(parents=True, exist_ok=True)
         b.write_fasta(fasta_out, idx, append=written > 0)
+        written += int(idx.size)
+        if serr is None and (b.lengths()[idx] <= species.k).any():
+            serr = _short_read_error()
+        if serr is not None:
+            continue
         raw = b.packed.buf
         o = b.packed.offsets
         seqs = [raw[o[i]:o[i + 1]].tobytes() for i in idx.tolist()]
         h, nk = species.index.query(pack_sequences(seqs), step=step)
         scol.add([ids[i] for i in idx.tolist()], h, nk)
-        written += int(idx.size)
-    sres = scol.result(species.slug(), species._labels(display_names), step) if written else None
-    return gres, sres, written
+    sres = scol.result(species.slug(), species._labels(display_names), step) if written and serr is None else None
+    return gres, sres, written, serr
 
 
 def _svm_predict(species, sres: MatrixResult) -> None:
@@ -196,10 +236,10 @@ def run_pipeline(genus, species, input_path: Path, output_dir: Path | None = Non
     # step 1 (+ the species probe of the kept reads, same pass)
     log(f"Step 1/3: Filtering for genus {genus.model_display_name}...")
     inputs, get_out = prepare_input_output_paths(Path(input_path))
-    species_of: dict[Path, MatrixResult] = {}
+    species_of: dict[Path, MatrixResult | ValueError] = {}
     for idx, current in enumerate(inputs):
         fasta_out = get_out(idx, genus_filtered)
-        gres, sres, written = _fused_file(current, genus, species, threshold, step, fasta_out, batch_bytes,
+        gres, sres, written, serr = _fused_file(current, genus, species, threshold, step, fasta_out, batch_bytes,
                                           display_names)
         gres.input_source = current.name
         cls_out = get_out(idx, genus_cls)
@@ -209,7 +249,7 @@ def run_pipeline(genus, species, input_path: Path, output_dir: Path | None = Non
         if not written:
             log(f"No sequences found for the given genus in {current.name}.")
             continue
-        species_of[fasta_out.resolve()] = sres
+        species_of[fasta_out.resolve()] = sres if serr is None else serr
         out["filtered"].append(fasta_out)
         log(f"Saved filtered sequences from {current.name} as {fasta_out.name}")
 
@@ -225,6 +265,8 @@ def run_pipeline(genus, species, input_path: Path, output_dir: Path | None = Non
     predictions = []
     for idx, f in enumerate(finputs):
         sres = species_of.get(f.resolve())
+        if isinstance(sres, ValueError):  # species predict of this file raises here (classify.py:78-92)
+            raise sres
         if sres is None:  # a file of an earlier run in the same directory
             sres = species.predict_columnar(f, step=step, display_name=display_names)
         else:
