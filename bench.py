@@ -19,13 +19,15 @@ Other workloads (SURVEY.md §8(d) configs 4/5 and the genus path):
               per-read hit vectors all-gathered over RCCL (docs sharded)
 
 metric = k-mer x filter probes/s = sum(ceil((L-k+1)/step)) x docs / second,
-whole job.  roofline prices the probe kernel alone (HIP events on its launch
-stream around every launch of the timed region) at its algorithmic bytes:
-one 128-byte L2 line fill per random row (COBS: h rows per k-mer and doc
-group; rbloom: K dwords per k-mer; MLST: the 64-byte rows themselves, its
-banks being Infinity-Cache resident) + the read bytes, hit matrix and
-per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per launch from
-profiles/r01_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
+whole job.  roofline prices the probe alone (HIP events on its launch
+stream around every probe of the timed region) at its algorithmic bytes.
+Species banks over 256 MiB take the partitioned COBS pipeline (bucket ->
+per-XCD L2 lookup -> resolve): SURVEY.md §8(d)'s h x 64 B per k-mer.  The
+direct kernels: one 128-byte L2 line fill per random row (COBS: h rows per
+k-mer and doc group; rbloom: K dwords per k-mer; MLST: the 64-byte rows
+themselves, its banks being Infinity-Cache resident).  Both + the read bytes,
+hit matrix and per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per
+probe from profiles/r02_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
 OpenMP) on a bounded sample of the same reads and bank (rank 0, N=1 only);
 its hits are also compared with the GPU's; plus the reference's per-read loop
 shape on one core.  host_path: the same step from host buffers (PCIe).
@@ -52,6 +54,9 @@ METRIC = "k-mer\u00d7filter probes/s (150bp reads, ~100-species Bloom bank) at 1
 # shows 128 B fills"; profiles/r01_pmc_probe.txt shows TCC_EA0_RDREQ_128B ==
 # TCC_EA0_RDREQ (915.9 M per launch, 32B/64B requests ~0), so 128 B it is.
 ROW_BYTES = 128
+# SURVEY.md §8(d)'s per-row figure, used for the partitioned COBS pipeline,
+# which reads rows from L2-resident bank partitions instead of random lines.
+SURVEY_ROW_BYTES = 64
 # Rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo
 # collectives through host copies (RCCL does not share a device between ranks).
 SHARE_GPU = os.environ.get("XSPECT_BENCH_SHARE_GPU") == "1"
@@ -102,7 +107,7 @@ def parse():
                     help="skip the PCIe-inclusive host-buffer runs (profiling: only full-size probe launches)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r01_traffic.json"))
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r02_traffic.json"))
     return ap.parse_args()
 
 
@@ -260,6 +265,14 @@ class Workload:
 
     def algo_bytes_per_launch(self):
         """Bytes one probe launch must move (per bank; averaged over banks)."""
+        if getattr(self, "partitioned", False) == "cobs":
+            # SURVEY.md §8(d)'s algorithmic figure: h rows x 64 B per k-mer (one
+            # random row transaction each), + the read bytes, hit rows and
+            # per-read metadata.  The partitioned pipeline fetches no row as a
+            # random HBM line (PMC traffic per step is below this figure).
+            d = self.docs[0]
+            return (self.kmers * self.rows_per_kmer * SURVEY_ROW_BYTES + self.seq_bytes + self.n * d * 4
+                    + self.n * (8 + 4 + 8 + 8))
         if getattr(self, "partitioned", False):
             # partitioned rbloom pipeline, per filter bit tested: 4-B offset + 2-B
             # k-mer id written and the offset read back, a miss byte zeroed,
@@ -343,7 +356,20 @@ def main():
     value = wl.probes_per_step() * args.steps / elapsed
     from xspect2_amd._lib import XS_PATH_PARTITIONED
     wl.partitioned = args.workload == "genus" and wl.banks[0].probe_path() == XS_PATH_PARTITIONED
-    if wl.partitioned:
+    if args.workload in ("species", "multigenus") and wl.banks[0].probe_path() == XS_PATH_PARTITIONED:
+        wl.partitioned = "cobs"
+        ck = os.environ.get("XSPECT2_AMD_CP_CK", "2048")
+        wl.kernel = (f"COBS partitioned: cobs_bucket<{wl.k},{wl.rows_per_kmer},{ck}> (hash, bin rows by 2 MiB bank "
+                     "partition) -> cobs_lookup (per-XCD L2-resident partition, rows back in entry order) -> "
+                     "cobs_resolve (AND per k-mer in LDS, per-read counts)")
+        wl.row_bytes = SURVEY_ROW_BYTES
+        wl.roofline_note = ("achieved = SURVEY.md §8(d)'s algorithmic bytes (h x 64 B per k-mer + reads, hits, "
+                            "metadata) over the whole probe (HIP events around the pipeline); traffic = PMC HBM "
+                            "bytes of the pipeline per step, below the algorithmic figure: rows come from "
+                            "L2-resident partitions, not random HBM lines.  Per-kernel bounds: bucket = integer "
+                            "multiplies (XXH64 x h + Barrett), lookup = vector-L1 miss path to L2 (TCP pending "
+                            "stalls), resolve = HBM streaming; see DESIGN.md")
+    elif wl.partitioned:
         wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 2 MiB filter partition) -> "
                      "bloom_lookup (per-XCD L2-resident partition) -> resolve -> count")
         wl.row_bytes = None
@@ -366,10 +392,11 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu_pmc_traffic_part.sh)
+    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu_pmc_traffic_part.sh, gpu_cp_pmc2.sh)
         traffic = None
         try:
-            tp = json.loads(tj.read_text()).get("genus_partitioned") or {}
+            key = "species_partitioned" if wl.partitioned == "cobs" else "genus_partitioned"
+            tp = json.loads(tj.read_text()).get(key) or {}
             if tp.get("reads") == wl.n:
                 traffic = tp.get("hbm_bytes_per_step")
         except Exception:

@@ -74,7 +74,27 @@ CLASSIC_CASES = [
 
 
 @pytest.mark.parametrize("D,k,h,sig", CLASSIC_CASES)
-def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
+def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig):
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    _classic_case(xs, oracle_mod, D, k, h, sig)
+
+
+@pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
+                                                                                  (64, 31, 8, [300_007])])
+@pytest.mark.parametrize("ck,sub", [("1024", "1"), ("2048", "1"), ("4096", "1"), ("2048", "3"), ("1024", "8")])
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, sub):
+    """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
+    L2-resident lookup, per-block AND + count) with partitions down to 1024
+    rows, every bucket block size, and bucket-block ranges pipelined over
+    three streams, on the classic cases of <= 128 docs: same hits, counts and
+    totals."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
+    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
+    monkeypatch.setenv("XSPECT2_AMD_CP_SUB", sub)
+    _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
+
+
+def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D * 31 + k)
     rng = np.random.default_rng(D + k + h)
     reads = _reads(rng, 300, k)
@@ -87,6 +107,8 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
         got_h, got_n = gb.query(reads, step=step)
         assert np.array_equal(got_n, want_n), f"num_kmers differ (step {step})"
         assert np.array_equal(got_h, want_h), _explain(got_h, want_h, reads)
+        if want_path is not None:
+            assert gb.probe_path() == want_path
         tot, nk = gb.query_totals(reads, step=step)
         assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64))
         assert nk == int(want_n.sum())

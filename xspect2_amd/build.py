@@ -12,8 +12,9 @@ CSRC = PKG / "csrc"
 SO_PATH = PKG / "libxspect_hip.so"
 SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_json.cpp", CSRC / "xs_kernels.hip",
            CSRC / "xs_probe_fast.hip", CSRC / "xs_probe_wide.hip", CSRC / "xs_probe_slots.hip",
-           CSRC / "xs_probe_general.hip", CSRC / "xs_probe_bloompart.hip"]
-HEADERS = [CSRC / "xs_internal.h", CSRC / "xs_device.h", ROOT / "include" / "xspect_hip.h"]
+           CSRC / "xs_probe_general.hip", CSRC / "xs_probe_bloompart.hip",
+           CSRC / "xs_probe_cobspart.hip"]
+HEADERS = [CSRC / "xs_internal.h", CSRC / "xs_device.h", CSRC / "xs_part.h", ROOT / "include" / "xspect_hip.h"]
 OBJ_DIR = PKG / "_build"
 ARCH = os.environ.get("XSPECT2_AMD_ARCH", "gfx950")
 

@@ -30,42 +30,11 @@
 
 #include <algorithm>
 
-#include "xs_device.h"
+#include "xs_part.h"
 
 namespace xs {
 
 namespace {
-
-constexpr int kTK = kPartKmers;  // k-mers per bucket block
-constexpr int kBucketThreads = 512;
-constexpr uint32_t kStageReads = 256;  // read offsets a bucket block keeps in LDS
-
-__global__ void part_counts_kernel(const uint64_t* __restrict__ offs, uint64_t n, uint32_t k, uint32_t step,
-                                   uint64_t* __restrict__ nkc) {
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r <= n;
-         r += (uint64_t)gridDim.x * blockDim.x)
-        nkc[r] = r < n ? num_kmers(offs[r + 1] - offs[r], k, step) : 0;
-}
-
-// Largest r in [lo, hi] with kofs[r] <= g (kofs non-decreasing, kofs[lo] <= g).
-__device__ __forceinline__ uint64_t read_of(const uint64_t* __restrict__ kofs, uint64_t lo, uint64_t hi,
-                                            uint64_t g) {
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi + 1) >> 1;
-        if (kofs[mid] <= g) lo = mid;
-        else hi = mid - 1;
-    }
-    return lo;
-}
-
-// blk_read[b] = the read holding k-mer b*kTK (the first k-mer of bucket block b).
-__global__ void part_map_kernel(const uint64_t* __restrict__ kofs, uint64_t n, uint32_t* __restrict__ blk_read) {
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t fb = (kofs[r] + kTK - 1) / kTK, lb = (kofs[r + 1] + kTK - 1) / kTK;
-        for (uint64_t b = fb; b < lb; ++b) blk_read[b] = (uint32_t)r;
-    }
-}
 
 template <int KT, int KB>
 __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView rv, BloomView bv,
@@ -196,25 +165,6 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
     }
 }
 
-// Block-major partition starts (one coalesced row per bucket block) ->
-// partition-major (the lookup reads 64 blocks' starts of one partition as one
-// line), through a 64 x 64 LDS tile.
-__global__ void __launch_bounds__(256) part_transpose_kernel(const uint16_t* __restrict__ tbm, uint32_t P1,
-                                                             uint64_t tstride, uint16_t* __restrict__ tbl) {
-    __shared__ uint16_t t[64][65];
-    const uint64_t b0 = (uint64_t)blockIdx.x * 64;
-    const uint32_t p0 = blockIdx.y * 64;
-    for (uint32_t x = threadIdx.x; x < 64 * 64; x += 256) {
-        const uint32_t bi = x / 64, pi = x % 64;
-        if (b0 + bi < tstride && p0 + pi < P1) t[bi][pi] = tbm[(b0 + bi) * P1 + p0 + pi];
-    }
-    __syncthreads();
-    for (uint32_t x = threadIdx.x; x < 64 * 64; x += 256) {
-        const uint32_t pi = x / 64, bi = x % 64;
-        if (b0 + bi < tstride && p0 + pi < P1) tbl[(p0 + pi) * tstride + b0 + bi] = t[bi][pi];
-    }
-}
-
 // The waves of one XCD work through one partition at a time (its filter
 // bytes stay in the XCD's 4 MiB L2 while the entries stream past), taking
 // groups of 64 bucket blocks from the partition's queue counter.  A queue
@@ -222,7 +172,6 @@ __global__ void __launch_bounds__(256) part_transpose_kernel(const uint16_t* __r
 // partitions ahead and the L2 hit rate fell from 86 % to 44 %.  Each counter
 // sits on its own 128-B line (a line's atomics are serialised at the memory
 // side).  Every lane keeps kLookupUnroll entries in flight.
-constexpr uint32_t kQStride = 32;  // u32 per queue counter
 
 template <int kLookupUnroll>
 __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const uint64_t* __restrict__ kofs,
@@ -471,7 +420,7 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
         bloom_bucket_kernel<0, 0><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
             rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read);
     part_transpose_kernel<<<dim3((unsigned)((plan.tstride + 63) / 64), (plan.P + 1 + 63) / 64), 256, 0, s>>>(
-        tbm, plan.P + 1, plan.tstride, ws.tbl);
+        tbm, plan.P + 1, plan.tstride, ws.tbl, 0, plan.tstride);
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
     bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,

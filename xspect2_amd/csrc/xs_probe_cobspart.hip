@@ -1,0 +1,591 @@
+// xs_probe_cobspart.hip — partitioned COBS probe for classic banks far larger
+// than L2 (species banks: D <= 128 docs, one 16-byte row per hash).
+//
+// The direct probe (probe_cobs_fast) gathers h random 16-B rows per k-mer;
+// each is a 128-B line fill, so it runs at the chip's random line-fill rate
+// (~57 G lines/s, 0.92 of HBM bandwidth at 128 B a line, 16 B of it used).
+// Here the probe is reorganised around the bank, as the partitioned rbloom
+// probe is (xs_probe_bloompart.hip):
+//
+//   counts  : per read k-mer count, exclusive scan -> global k-mer id g
+//   bucket  : one block per 1024 k-mers: canonical k-mer, the h XXH64 rows
+//             (exactly as the direct probe), each binned by bank partition
+//             (2 MiB of rows) with LDS counters, a block scan and LDS-sorted
+//             placement; one u32 entry per row = (row in partition << 10 |
+//             k-mer in block), copied out partition-ordered per block, plus
+//             one u16 start per partition into a partition-major table.
+//   lookup  : the workgroups of one XCD work through one partition at a time
+//             from a per-partition queue, so its 2 MiB of rows stay in that
+//             XCD's 4 MiB L2 while the entries stream past; each entry's
+//             16-B row is written back in entry order (coalesced).
+//   resolve : per bucket block: AND the h rows of each of its k-mers in LDS,
+//             then count per (read, doc) with the column-popcount transpose
+//             of the direct probe; reads inside the block are stored, reads
+//             crossing a block edge are added atomically; per-doc totals.
+//
+// Same answer as the direct probe and the oracle (score[d] = number of
+// sampled positions whose h rows all hold bit d; probabilistic_filter_model.py
+// :227 -> cobs Search.search).  Parity: tests/test_gpu_parity.py runs the
+// classic cases through both paths.
+#include "xs_part.h"
+
+namespace xs {
+
+namespace {
+
+// CK k-mers per bucket block (1024 or 2048); an entry's low IDB bits name
+// its k-mer within the block.
+template <int CK>
+constexpr int id_bits() { return CK == 4096 ? 12 : CK == 2048 ? 11 : 10; }
+template <int CK>
+constexpr int bucket_threads() { return CK / 2 < 1024 ? CK / 2 : 1024; }
+constexpr int kMaxH = 8;     // rows per k-mer on this path
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 load_nt(const uint4* p) {
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+struct PartBank {
+    const uint4* rows;  // 16-B rows
+    uint64_t sig, magic;
+    uint32_t D, nwords;
+};
+
+template <int KT, int HT, int CK>
+__global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadView rv, PartBank pb, uint32_t h,
+                                                                     const uint64_t* __restrict__ kofs,
+                                                                     uint32_t shift, uint32_t P,
+                                                                     uint32_t* __restrict__ ent,
+                                                                     uint16_t* __restrict__ tbm,
+                                                                     const uint32_t* __restrict__ blk_read,
+                                                                     uint64_t b_begin) {
+    constexpr int BT = bucket_threads<CK>();
+    constexpr int IDB = id_bits<CK>();
+    using Scan = hipcub::BlockScan<uint32_t, BT>;
+    constexpr int ITEMS = kPartMax / BT;
+    constexpr int PER = CK / BT;  // k-mers per thread
+    constexpr int NH = HT ? HT : kMaxH;
+    __shared__ uint32_t s_ent[CK * NH];  // partition-ordered entries
+    __shared__ uint32_t cur[kPartMax];
+    __shared__ typename Scan::TempStorage scan_tmp;
+    __shared__ uint64_t s_kofs[kStageReads], s_offs[kStageReads];
+    const int tid = threadIdx.x;
+    const uint32_t H = HT ? HT : h;
+    const uint32_t k = KT ? KT : rv.k;
+    const uint64_t Nk = kofs[rv.n];
+    const uint64_t B = b_begin + blockIdx.x;  // bucket block
+    const uint64_t g0 = B * CK;
+    if (g0 >= Nk) return;  // uniform per block
+    const uint32_t m = (uint32_t)min((uint64_t)CK, Nk - g0);
+    for (uint32_t i = tid; i < kPartMax; i += BT) cur[i] = 0;
+    // reads of this block staged in LDS when they fit (one global load per k-mer: its window)
+    const uint64_t lo = blk_read[B];
+    const uint64_t hi = g0 + CK < Nk ? blk_read[B + 1] : rv.n - 1;
+    const uint64_t nr = hi - lo + 2;
+    const bool staged = nr <= kStageReads;
+    if (staged)
+        for (uint32_t x = tid; x < nr; x += BT) {
+            s_kofs[x] = kofs[lo + x];
+            s_offs[x] = rv.offs[lo + x];
+        }
+    __syncthreads();
+    Kmer c[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * BT;
+        if (i < m) {
+            const uint64_t g = g0 + i;
+            uint64_t kr, o0, o1;
+            if (staged) {
+                uint32_t a = 0, b = (uint32_t)(nr - 2);  // largest x with s_kofs[x] <= g
+                while (a < b) {
+                    const uint32_t mid = (a + b + 1) >> 1;
+                    if (s_kofs[mid] <= g) a = mid;
+                    else b = mid - 1;
+                }
+                kr = s_kofs[a];
+                o0 = s_offs[a];
+                o1 = s_offs[a + 1];
+            } else {
+                const uint64_t r = read_of(kofs, lo, hi, g);
+                kr = kofs[r];
+                o0 = rv.offs[r];
+                o1 = rv.offs[r + 1];
+            }
+            kmer_at<KT, kKmerCobs>(rv, o0, o1 - o0, (g - kr) * rv.step, k, c[q]);
+        }
+    }
+    uint32_t row[PER][NH];  // the h rows of this thread's k-mers stay in registers
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * BT;
+        if (i < m) {
+            Xxh64Pre pre;
+            xxh64_pre<KT>(c[q], k, pre);
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                if ((uint32_t)j < H) {
+                    row[q][j] = (uint32_t)fastmod(xxh64_seed<KT>(c[q], pre, k, (uint64_t)j), pb.sig, pb.magic);
+                    atomicAdd(&cur[row[q][j] >> shift], 1u);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t v[ITEMS];
+#pragma unroll
+    for (int q = 0; q < ITEMS; ++q) v[q] = cur[tid * ITEMS + q];
+    Scan(scan_tmp).ExclusiveSum(v, v);
+    __syncthreads();  // every counter read before it becomes a cursor
+#pragma unroll
+    for (int q = 0; q < ITEMS; ++q) {
+        const uint32_t p = tid * ITEMS + q;
+        if (p < P) {
+            cur[p] = v[q];
+            tbm[B * (P + 1) + p] = (uint16_t)v[q];
+        }
+    }
+    if (tid == 0) tbm[B * (P + 1) + P] = (uint16_t)(m * H);
+    __syncthreads();
+    const uint32_t omask = (1u << shift) - 1;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const uint32_t i = tid + q * BT;
+        if (i < m) {
+#pragma unroll
+            for (int j = 0; j < NH; ++j) {
+                if ((uint32_t)j < H) {
+                    const uint32_t pos = atomicAdd(&cur[row[q][j] >> shift], 1u);
+                    s_ent[pos] = ((row[q][j] & omask) << IDB) | i;
+                }
+            }
+        }
+    }
+    __syncthreads();
+    // coalesced copy-out (regions of CK*H entries: 16-B aligned)
+    const uint64_t base = B * CK * H;
+    const uint32_t tot = m * H;
+    for (uint32_t e = tid * 4; e < tot; e += BT * 4) {
+        if (e + 4 <= tot) {
+            *reinterpret_cast<uint4*>(ent + base + e) = *reinterpret_cast<const uint4*>(s_ent + e);
+        } else {
+            for (uint32_t x = e; x < tot; ++x) ent[base + x] = s_ent[x];
+        }
+    }
+}
+
+// The waves of one XCD work through one partition at a time (its rows stay in
+// the XCD's L2 while the entries stream past), taking groups of 64 bucket
+// blocks from the partition's queue counter (the rbloom lookup's scheme,
+// xs_probe_bloompart.hip).  Each entry's row goes back in entry order; with
+// EMB (D <= kEmbMaxDocs) the entry's k-mer id rides in the row's unused top
+// bits (docs 118..127), so the resolve pass need not read the entries again.
+template <int CK>
+constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
+template <int kUnroll, int STORE, bool EMB, int CK>
+__global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
+                                                          uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
+                                                          uint64_t tstride, const uint32_t* __restrict__ ent,
+                                                          const uint16_t* __restrict__ tbl,
+                                                          uint4* __restrict__ out, uint32_t* qctr,
+                                                          uint64_t b_begin, uint64_t b_end) {
+    constexpr int IDB = id_bits<CK>();
+    const int lane = threadIdx.x & 63;
+    // this call's bucket blocks: b_begin .. b_end-1, those past the batch's last k-mer excluded
+    const uint64_t nblk = min(b_end, (kofs[n] + CK - 1) / CK);
+    const uint64_t cap = (uint64_t)CK * H;
+    const uint32_t xcd = blockIdx.x & 7;
+    for (uint64_t p = xcd; p < P; p += 8) {
+        const uint4* prow = pb.rows + (p << shift);
+        const uint16_t* t0 = tbl + p * tstride;
+        const uint16_t* t1 = t0 + tstride;
+        for (;;) {
+            uint32_t grp = 0;
+            if (lane == 0) grp = atomicAdd(&qctr[p * kQStride], 1u);
+            const uint64_t b0 = b_begin + (uint64_t)__builtin_amdgcn_readfirstlane(grp) * 64;
+            if (b0 >= nblk) break;
+            const uint64_t b = b0 + lane;
+            uint32_t s = 0, len = 0;
+            if (b < nblk) {
+                s = t0[b];
+                len = (uint32_t)t1[b] - s;
+            }
+            uint32_t inc = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc += t;
+            }
+            const uint32_t pre = inc - len;
+            const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+            for (uint32_t i0 = 0; i0 < total; i0 += 64 * kUnroll) {
+                uint64_t pos[kUnroll];
+                uint32_t e[kUnroll];
+                uint4 v[kUnroll];
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u) {
+                    const uint32_t i = i0 + u * 64 + lane;
+                    int j = 0;
+#pragma unroll
+                    for (int st = 32; st; st >>= 1) {
+                        const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
+                        if (pv <= i) j += st;
+                    }
+                    const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
+                    const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
+                    pos[u] = (b0 + j) * cap + sj + (i - pj);
+                }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    e[u] = i0 + u * 64 + lane < total ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    if (i0 + u * 64 + lane < total) {
+                        v[u] = prow[e[u] >> IDB];
+                    }
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    if (i0 + u * 64 + lane < total) {
+                        if constexpr (EMB) v[u].w = (v[u].w & (0xFFFFFFFFu >> IDB)) | (e[u] << (32 - IDB));
+                        if constexpr (STORE == 0) {
+                            // non-temporal dword stores: 7.8 vs 10.1 ms for one dwordx4 (tools/partgather.hip)
+                            uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
+                            __builtin_nontemporal_store(v[u].x, o);
+                            __builtin_nontemporal_store(v[u].y, o + 1);
+                            __builtin_nontemporal_store(v[u].z, o + 2);
+                            __builtin_nontemporal_store(v[u].w, o + 3);
+                        } else if constexpr (STORE == 2) {
+                            u32x4 w4 = {v[u].x, v[u].y, v[u].z, v[u].w};
+                            __builtin_nontemporal_store(w4, reinterpret_cast<u32x4*>(out + pos[u]));
+                        } else {
+                            out[pos[u]] = v[u];
+                        }
+                    }
+            }
+        }
+    }
+}
+
+// Per bucket block: AND each k-mer's h rows in LDS, then count per (read, doc).
+// Reads of the block whose k-mers all lie in it get their counts stored; the
+// (at most two) reads crossing its edges are added atomically (hits zeroed
+// beforehand).  Blocks with more reads than LDS counter rows (short reads)
+// add every count atomically.
+template <int CK>
+constexpr int resolve_threads() { return CK / 4 < 1024 ? CK / 4 : 1024; }
+template <int CK>
+constexpr uint32_t cnt_reads() { return CK / 64; }  // reads per block with LDS counters
+constexpr int kResolveUnroll = 8;
+
+
+template <bool EMB, int CK>
+__global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(ReadView rv, const uint64_t* __restrict__ kofs,
+                                                                       uint32_t H, uint32_t D, uint32_t nwords,
+                                                                       const uint32_t* __restrict__ ent,
+                                                                       const uint4* __restrict__ rowv,
+                                                                       const uint32_t* __restrict__ blk_read,
+                                                                       uint32_t* __restrict__ hits,
+                                                                       uint64_t* __restrict__ partials, int pblocks,
+                                                                       uint64_t b_begin) {
+    __shared__ uint32_t acc[4][CK];
+    constexpr int kResolveThreads = resolve_threads<CK>();
+    constexpr uint32_t kCntReads = cnt_reads<CK>();
+    __shared__ uint32_t cnt[kCntReads][128];
+    __shared__ uint64_t s_kofs[kCntReads + 1];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint64_t n = rv.n;
+    const uint64_t Nk = kofs[n];
+    const uint64_t B = b_begin + blockIdx.x;  // bucket block
+    const uint64_t g0 = B * CK;
+    if (g0 >= Nk) return;
+    const uint32_t m = (uint32_t)min((uint64_t)CK, Nk - g0);
+    const uint64_t lo = blk_read[B];
+    const uint64_t hi = g0 + CK < Nk ? blk_read[B + 1] : n - 1;
+    // reads lo..hi hold the block's k-mers (empty reads between them hold none)
+    const uint64_t nr = hi - lo + 1;
+    const bool lds_cnt = nr <= kCntReads;
+    for (uint32_t i = tid; i < CK; i += kResolveThreads) {
+        acc[0][i] = ~0u;
+        acc[1][i] = ~0u;
+        acc[2][i] = ~0u;
+        acc[3][i] = ~0u;
+    }
+    if (lds_cnt) {
+        for (uint32_t x = tid; x < kCntReads * 128; x += kResolveThreads) (&cnt[0][0])[x] = 0;
+        for (uint32_t x = tid; x <= nr; x += kResolveThreads) s_kofs[x] = kofs[lo + x];
+    }
+    __syncthreads();
+    const uint64_t base = B * CK * H;
+    const uint32_t tot = m * H;
+    // kResolveUnroll rows in flight per lane, then their LDS ANDs
+    for (uint32_t e0 = tid; e0 < tot; e0 += kResolveThreads * kResolveUnroll) {
+        uint4 v[kResolveUnroll];
+        uint32_t id[kResolveUnroll];
+#pragma unroll
+        for (int u = 0; u < kResolveUnroll; ++u) {
+            const uint32_t e = e0 + u * kResolveThreads;
+            if (e < tot) {
+                v[u] = load_nt(rowv + base + e);
+                if (!EMB) id[u] = __builtin_nontemporal_load(ent + base + e) & (CK - 1);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kResolveUnroll; ++u) {
+            if (e0 + u * kResolveThreads < tot) {
+                const uint32_t i = EMB ? v[u].w >> (32 - id_bits<CK>()) : id[u];
+                atomicAnd(&acc[0][i], v[u].x);
+                if (nwords > 1) atomicAnd(&acc[1][i], v[u].y);
+                if (nwords > 2) atomicAnd(&acc[2][i], v[u].z);
+                if (nwords > 3) atomicAnd(&acc[3][i], v[u].w);
+            }
+        }
+    }
+    __syncthreads();
+    Xpose X;
+    xpose_init(lane, X);
+    uint64_t doc_tot[4] = {0, 0, 0, 0};  // lane < 32: doc 32q + lane
+    for (uint32_t t0 = (uint32_t)wid * 64; t0 < m; t0 += kResolveThreads) {
+        const uint32_t i = t0 + lane;
+        const bool valid = i < m;
+        const uint64_t g = g0 + i;
+        // read of each lane's k-mer
+        uint64_t r;
+        if (lds_cnt) {
+            uint32_t a = 0, b = (uint32_t)(nr - 1);
+            while (a < b) {
+                const uint32_t mid = (a + b + 1) >> 1;
+                if (s_kofs[mid] <= g) a = mid;
+                else b = mid - 1;
+            }
+            r = lo + a;
+        } else {
+            r = read_of(kofs, lo, hi, valid ? g : g0);
+        }
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = valid ? acc[q][i] : 0u;
+        // reads of this 64-k-mer tile: from lane 0's to the last valid lane's
+        const uint64_t rfirst = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(r >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)r);
+        const uint32_t last = min(m - 1, t0 + 63) - t0;
+        const uint64_t rlast = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r >> 32), (int)last, 64) << 32) |
+                               (uint32_t)__shfl((int)(uint32_t)r, (int)last, 64);
+        for (uint64_t rr = rfirst; rr <= rlast; ++rr) {
+            const bool mine = valid && r == rr;
+            if (!__any(mine)) continue;  // an empty read between two others
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if ((uint32_t)q >= nwords) break;
+                const uint32_t c = fold_halves(column_popc32(mine ? w[q] : 0u, X));
+                const uint32_t d = q * 32 + (uint32_t)lane;
+                if (lane < 32 && d < D && c) {
+                    doc_tot[q] += c;
+                    if (hits) {
+                        if (lds_cnt) atomicAdd(&cnt[rr - lo][d], c);
+                        else atomicAdd(&hits[rr * D + d], c);
+                    }
+                }
+            }
+        }
+    }
+    // per-doc totals of the block (lanes < 32 of each wave) and its k-mer count
+    if (partials) {
+        uint64_t* out = partials + (B % (uint32_t)pblocks) * (D + 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t d = q * 32 + (uint32_t)lane;
+            if (lane < 32 && d < D && doc_tot[q])
+                atomicAdd(reinterpret_cast<unsigned long long*>(out + d), (unsigned long long)doc_tot[q]);
+        }
+        if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + D), (unsigned long long)m);
+    }
+    if (!hits || !lds_cnt) return;
+    __syncthreads();
+    // reads wholly inside the block: stored; the edge reads: added
+    for (uint32_t x = tid; x < nr * D; x += kResolveThreads) {
+        const uint32_t ri = x / D, d = x - ri * D;
+        const uint64_t rr = lo + ri;
+        const bool inside = s_kofs[ri] >= g0 && s_kofs[ri + 1] <= g0 + m;
+        const uint32_t c = cnt[ri][d];
+        if (inside) hits[rr * D + d] = c;
+        else if (c) atomicAdd(&hits[rr * D + d], c);
+    }
+}
+
+}  // namespace
+
+// XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
+// probe for classic banks of <= 128 docs larger than the Infinity Cache;
+// 2 = partitioned for such banks of any size; 3 = as 2 with partitions down
+// to 1024 rows (tests reach many partitions on small banks).  Read per call.
+static int cobs_part_env() {
+    const char* e = getenv("XSPECT2_AMD_COBS_PART");
+    return e ? atoi(e) : 1;
+}
+
+// Bucket block k-mers: XSPECT2_AMD_CP_CK = 1024, 2048 (default) or 4096 (read per call).
+static int env_int(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
+bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
+                    CobsPartPlan* plan) {
+    const int mode = cobs_part_env();
+    if (mode <= 0) return false;
+    if (bv.G != 1 || bv.pitch != 16 || bv.D > 128 || bv.h == 0 || bv.h > (uint32_t)kMaxH || k > kMaxK) return false;
+    const uint64_t sig = bv.sig0;
+    if (sig >= (1ull << 32)) return false;
+    // banks under 256 MiB stay Infinity-Cache resident: the direct probe is faster there
+    if (mode == 1 && sig * 16 < (256ull << 20)) return false;
+    const int ck_env = env_int("XSPECT2_AMD_CP_CK", 2048);
+    const uint32_t ck = ck_env == 4096 ? 4096 : ck_env == 1024 ? 1024 : 2048;
+    const uint32_t idb = ck == 4096 ? 12 : ck == 2048 ? 11 : 10;
+    // 2^17 rows (2 MiB) per partition, fewer rows while that leaves under 64
+    // partitions (8 per XCD), more while over kPartMax
+    const uint32_t floor_shift = mode >= 3 ? 10 : 13;
+    uint32_t shift = 17;
+    auto parts = [sig](uint32_t s) { return (sig + (1ull << s) - 1) >> s; };
+    while (shift > floor_shift && parts(shift) < 64) --shift;
+    while (parts(shift) > kPartMax) ++shift;
+    if (shift + idb > 32) return false;
+    const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
+    if (kbound >= (1ull << 32)) return false;
+    const uint64_t nblk = (kbound + ck - 1) / ck;
+    const uint64_t P = parts(shift);
+    plan->ck = ck;
+    plan->nsub = (uint32_t)std::min(std::max(env_int("XSPECT2_AMD_CP_SUB", 1), 1), (int)kCobsPartMaxSub);
+    plan->shift = shift;
+    plan->P = (uint32_t)P;
+    plan->tstride = nblk;
+    plan->kbound = kbound;
+    plan->entry_bytes = nblk * ck * bv.h * (sizeof(uint32_t) + sizeof(uint4));  // entries, then their rows
+    plan->tbl_bytes = 2 * (P + 1) * nblk * sizeof(uint16_t);                    // partition- + block-major
+    plan->aux_bytes = (nblk + 1 + kQStride) * sizeof(uint32_t) + (size_t)P * kQStride * kCobsPartMaxSub * sizeof(uint32_t);
+    plan->nkc_bytes = (n + 1) * sizeof(uint64_t);
+    size_t sb = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(n + 1));
+    plan->scan_bytes = sb;
+    // entries are transient: cap the workspace (larger batches take the direct probe)
+    return plan->entry_bytes <= (48ull << 30);
+}
+
+static int cobs_lookup_grid(int per_cu_want) {
+    static std::atomic<int> cache{0};
+    const int per_cu_res = cached_grid(cache, [] {
+        int per_cu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, 0, true, 1024>, 256, 0) !=
+                hipSuccess || per_cu < 1)
+            per_cu = 1;
+        return per_cu;
+    });
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 768;
+    const int g = std::min(per_cu_res, std::max(1, per_cu_want)) * prop.multiProcessorCount;
+    return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
+}
+
+// Lookup variants for A/B (XSPECT2_AMD_CP_LOOKUP): unroll x store kind.
+// XSPECT2_AMD_CP_PERCU: lookup blocks per CU (default 3).
+template <int U, int ST, int CK>
+static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
+                          const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
+                          uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
+    if (emb)
+        cobs_lookup_kernel<U, ST, true, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.tstride,
+                                                                 ent, tbl, rowv, qctr, b0, b1);
+    else
+        cobs_lookup_kernel<U, ST, false, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.tstride,
+                                                                  ent, tbl, rowv, qctr, b0, b1);
+}
+
+// Bucket blocks are processed in plan.nsub consecutive ranges.  With more than
+// one, range i's bucket (VALU-bound hashing) runs on ws.hs while range i-1's
+// lookup (L2 gathers) runs on ws.ls and range i-2's resolve (streaming) on the
+// caller's stream s, so the three passes overlap.
+template <int CK>
+static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uint32_t H, const CobsPartPlan& plan,
+                                     const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
+                                     hipStream_t s) {
+    hipError_t e;
+    const uint64_t ne = plan.tstride * CK * H;
+    uint32_t* ent = reinterpret_cast<uint32_t*>(ws.entries);
+    uint4* rowv = reinterpret_cast<uint4*>(ent + (ne + 3) / 4 * 4);
+    uint32_t* blk_read = ws.aux;
+    uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.tstride;  // block-major copy
+    uint32_t* qctr0 = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
+    part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
+    const uint32_t S = plan.nsub;
+    const bool multi = S > 1;
+    hipStream_t hs = multi ? ws.hs : s, ls = multi ? ws.ls : s;
+    if (multi) {
+        if ((e = hipEventRecord(ws.ev_in, s)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(hs, ws.ev_in, 0)) != hipSuccess) return e;
+        if ((e = hipStreamWaitEvent(ls, ws.ev_in, 0)) != hipSuccess) return e;
+    }
+    const bool emb = pb.D <= emb_max_docs<CK>();
+    const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", 3));
+    const int var = env_int("XSPECT2_AMD_CP_LOOKUP", 0);
+    for (uint32_t i = 0; i < S; ++i) {
+        const uint64_t b0 = plan.tstride * i / S, b1 = plan.tstride * (i + 1) / S;
+        if (b1 == b0) continue;
+        const unsigned nb = (unsigned)(b1 - b0);
+        if (rv.k == 21 && H == 7)
+            cobs_bucket_kernel<21, 7, CK><<<nb, bucket_threads<CK>(), 0, hs>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
+                                                                             ent, tbm, blk_read, b0);
+        else
+            cobs_bucket_kernel<0, 0, CK><<<nb, bucket_threads<CK>(), 0, hs>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
+                                                                            ent, tbm, blk_read, b0);
+        part_transpose_kernel<<<dim3((nb + 63) / 64, (plan.P + 1 + 63) / 64), 256, 0, hs>>>(
+            tbm, plan.P + 1, plan.tstride, ws.tbl, b0, b1);
+        uint32_t* qctr = qctr0 + (size_t)i * plan.P * kQStride;
+        if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), hs)) != hipSuccess) return e;
+        if (multi) {
+            if ((e = hipEventRecord(ws.ev_b[i], hs)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(ls, ws.ev_b[i], 0)) != hipSuccess) return e;
+        }
+        switch (var) {
+            case 1: lookup_launch<4, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
+            case 2: lookup_launch<8, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
+            default: lookup_launch<8, 0, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
+        }
+        if (multi) {
+            if ((e = hipEventRecord(ws.ev_l[i], ls)) != hipSuccess) return e;
+            if ((e = hipStreamWaitEvent(s, ws.ev_l[i], 0)) != hipSuccess) return e;
+        }
+        if (emb)
+            cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
+                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0);
+        else
+            cobs_resolve_kernel<false, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
+                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const CobsPartPlan& plan,
+                                  const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
+                                  hipStream_t s) {
+    PartBank pb;
+    pb.rows = reinterpret_cast<const uint4*>(bv.rows);
+    pb.sig = bv.sig0;
+    pb.magic = barrett_magic(bv.sig0);
+    pb.D = (uint32_t)bv.D;
+    pb.nwords = (uint32_t)((bv.D + 31) / 32);
+    hipError_t e;
+    if (hits && (e = hipMemsetAsync(hits, 0, rv.n * bv.D * sizeof(uint32_t), s)) != hipSuccess) return e;
+    if (partials && (e = hipMemsetAsync(partials, 0, (size_t)blocks * (bv.D + 1) * sizeof(uint64_t), s)) != hipSuccess)
+        return e;
+    part_counts_kernel<<<grid_for(rv.n + 1, 256, 4096), 256, 0, s>>>(rv.offs, rv.n, rv.k, rv.step, ws.nkc);
+    size_t sb = ws.scan_bytes;
+    if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, sb, ws.nkc, ws.kofs, (int)(rv.n + 1), s)) != hipSuccess)
+        return e;
+    if (plan.ck == 4096) return cobs_part_pipeline<4096>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
+    if (plan.ck == 2048) return cobs_part_pipeline<2048>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
+    return cobs_part_pipeline<1024>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
+}
+
+}  // namespace xs
