@@ -115,6 +115,58 @@ def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
     gb.close()
 
 
+def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
+    """Default mode on a classic bank larger than the Infinity Cache (17 M
+    rows x 16 B = 272 MB on the device): the query takes the partitioned path
+    by itself; host and device APIs, totals, best doc, steps 1 and 3, reads of
+    every length class (empty, < k, one unit, several units), bit-exact."""
+    torch = pytest.importorskip("torch")
+    from xspect2_amd import _lib
+    from xspect2_amd.packing import pack_sequences
+    monkeypatch.delenv("XSPECT2_AMD_COBS_PART", raising=False)
+    monkeypatch.delenv("XSPECT2_AMD_CP_CK", raising=False)
+    D, k, h, sig = 100, 21, 7, 17_000_011
+    rng = np.random.default_rng(2024)
+    nb = sig * 13
+    rows = (np.frombuffer(rng.bytes(nb), np.uint8) | np.frombuffer(rng.bytes(nb), np.uint8)
+            | np.frombuffer(rng.bytes(nb), np.uint8))  # ~7/8 of the bits set: AND of 7 rows ~0.39
+    rows = rows.reshape(sig, 13).copy()
+    rows[:, 12] &= 0x0F  # docs 100..103 do not exist
+    ob = oracle_mod.CobsBank(rows.reshape(-1), [sig], 13, D, h, k)
+    gb = xs.Bank.create_cobs(k, h, [sig], D, [f"d{i}" for i in range(D)])
+    gb.upload(ob.rows)
+    reads = _reads(rng, 12_000, k, min_len=140, max_len=160)
+    reads += _reads(rng, 300, k, alphabet="ACGTacgtNRY", min_len=0, max_len=400)
+    reads += [b"", b"A" * (k - 1), _reads(rng, 1, k, min_len=5000, max_len=5001)[0]]
+    for step in (1, 3):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert gb.probe_path() == _lib.XS_PATH_PARTITIONED
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h, want_h), int((got_h != want_h).sum())
+        tot, nk = gb.query_totals(reads, step=step)
+        assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+        best, bh, bnk, btot = gb.query_best(reads, step=step, want_totals=True)
+        assert np.array_equal(bh, want_h.max(axis=1)) and np.array_equal(bnk, want_n)
+    assert 0 < int(want_h.sum())
+    # device API on a torch stream
+    pr = pack_sequences(reads)
+    dev = torch.device("cuda", 0)
+    d_seq = torch.from_numpy(pr.buf.copy()).to(dev)
+    d_off = torch.from_numpy(pr.offsets.astype(np.int64)).to(dev)
+    d_hits = torch.empty((pr.n, D), dtype=torch.int32, device=dev)
+    d_nk = torch.empty(pr.n, dtype=torch.int64, device=dev)
+    d_tot = torch.empty(D + 1, dtype=torch.int64, device=dev)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.synchronize()
+    gb.query_device(d_seq, int(pr.offsets[-1]), d_off, pr.n, 3, d_hits, d_nk, d_tot, stream=st.cuda_stream)
+    st.synchronize()
+    assert np.array_equal(d_hits.cpu().numpy().view(np.uint32), want_h)
+    tot = d_tot.cpu().numpy().view(np.uint64)
+    assert np.array_equal(tot[:D], want_h.sum(axis=0, dtype=np.uint64)) and int(tot[D]) == int(want_n.sum())
+    gb.close()
+
+
 @pytest.mark.parametrize("D,k,h,page,G", [(600, 31, 1, 64, 2), (20, 21, 7, 1, 3), (1500, 21, 2, 64, 3),
                                           (70, 25, 3, 3, 3), (2600, 31, 1, 64, 6), (1430, 31, 1, 64, 3),
                                           (600, 31, 1, 32, 3), (100, 21, 3, 2, 7), (2000, 31, 1, 64, 4),
@@ -428,6 +480,8 @@ def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
     torch = pytest.importorskip("torch")
     from xspect2_amd.packing import pack_sequences
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")  # partitioned COBS on the small bank,
+    monkeypatch.setenv("XSPECT2_AMD_CP_SUB", "3")     # its block ranges on the handle's own streams
     rng = np.random.default_rng(77)
     if kind == "cobs":
         ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)
