@@ -81,16 +81,17 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
 
 @pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
                                                                                   (64, 31, 8, [300_007])])
-@pytest.mark.parametrize("ck,sub", [("1024", "1"), ("2048", "1"), ("4096", "1"), ("2048", "3"), ("1024", "8")])
-def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, sub):
+@pytest.mark.parametrize("ck,ws_mb", [("1024", None), ("2048", None), ("4096", None), ("2048", "1"), ("1024", "2")])
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
     L2-resident lookup, per-block AND + count) with partitions down to 1024
-    rows, every bucket block size, and bucket-block ranges pipelined over
-    three streams, on the classic cases of <= 128 docs: same hits, counts and
-    totals."""
+    rows, every bucket block size, and workspaces of 1-2 MiB (the bucket
+    blocks then run in ranges of a few blocks that reuse it), on the classic
+    cases of <= 128 docs: same hits, counts and totals."""
     monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
     monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
-    monkeypatch.setenv("XSPECT2_AMD_CP_SUB", sub)
+    if ws_mb:
+        monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
 
 
@@ -119,7 +120,8 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     """Default mode on a classic bank larger than the Infinity Cache (17 M
     rows x 16 B = 272 MB on the device): the query takes the partitioned path
     by itself; host and device APIs, totals, best doc, steps 1 and 3, reads of
-    every length class (empty, < k, one unit, several units), bit-exact."""
+    every length class (empty, < k, one unit, several units), bit-exact;
+    then once more in ranges reusing a 64 MiB workspace."""
     torch = pytest.importorskip("torch")
     from xspect2_amd import _lib
     from xspect2_amd.packing import pack_sequences
@@ -149,6 +151,10 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
         best, bh, bnk, btot = gb.query_best(reads, step=step, want_totals=True)
         assert np.array_equal(bh, want_h.max(axis=1)) and np.array_equal(bnk, want_n)
     assert 0 < int(want_h.sum())
+    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "64")
+    got_h, got_n = gb.query(reads, step=3)
+    assert np.array_equal(got_h, want_h) and np.array_equal(got_n, want_n)
+    monkeypatch.delenv("XSPECT2_AMD_CP_WS_MB")
     # device API on a torch stream
     pr = pack_sequences(reads)
     dev = torch.device("cuda", 0)
@@ -481,7 +487,7 @@ def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
     from xspect2_amd.packing import pack_sequences
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
     monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")  # partitioned COBS on the small bank,
-    monkeypatch.setenv("XSPECT2_AMD_CP_SUB", "3")     # its block ranges on the handle's own streams
+    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "4")   # in ranges that reuse a 4 MiB workspace
     rng = np.random.default_rng(77)
     if kind == "cobs":
         ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)

@@ -147,11 +147,6 @@ struct xs_bank {
         best;
     DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
     DevBuf pk_nkc, pk_kofs, pk_scan, pk_entries, pk_tbl, pk_miss, pk_aux;  // partitioned probes (rbloom, COBS)
-    // partitioned COBS probe with pipelined block ranges: bucket and lookup
-    // streams, their events (created on first use)
-    hipStream_t cp_hs = nullptr, cp_ls = nullptr;
-    hipEvent_t cp_ev_in = nullptr;
-    hipEvent_t cp_ev_b[kCobsPartMaxSub] = {}, cp_ev_l[kCobsPartMaxSub] = {};
     // rbloom path choice: member fraction of the last query whose totals have
     // landed (members, k-mers), copied back asynchronously after every query
     DevBuf bloom_tot;
@@ -558,22 +553,8 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
               b->pk_scan.ensure(cplan.scan_bytes) || b->pk_entries.ensure(cplan.entry_bytes) ||
               b->pk_tbl.ensure(cplan.tbl_bytes) || b->pk_aux.ensure(cplan.aux_bytes))) {
             path = XS_PATH_PARTITIONED;
-            if (cplan.nsub > 1 && !b->cp_hs) {
-                HIPCHK(hipStreamCreateWithFlags(&b->cp_hs, hipStreamNonBlocking));
-                HIPCHK(hipStreamCreateWithFlags(&b->cp_ls, hipStreamNonBlocking));
-                HIPCHK(hipEventCreateWithFlags(&b->cp_ev_in, hipEventDisableTiming));
-                for (uint32_t i = 0; i < kCobsPartMaxSub; ++i) {
-                    HIPCHK(hipEventCreateWithFlags(&b->cp_ev_b[i], hipEventDisableTiming));
-                    HIPCHK(hipEventCreateWithFlags(&b->cp_ev_l[i], hipEventDisableTiming));
-                }
-            }
-            PartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
-                      b->pk_entries.p, b->pk_tbl.as<uint16_t>(), b->pk_aux.as<uint32_t>(), b->cp_hs, b->cp_ls,
-                      b->cp_ev_in, {}, {}};
-            for (uint32_t i = 0; i < kCobsPartMaxSub; ++i) {
-                ws.ev_b[i] = b->cp_ev_b[i];
-                ws.ev_l[i] = b->cp_ev_l[i];
-            }
+            const PartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
+                            b->pk_entries.p, b->pk_tbl.as<uint16_t>(), b->pk_aux.as<uint32_t>()};
             HIPCHK(launch_probe_cobs_part(rv, cv, cplan, ws, d_hits, partials, blocks, s));
         } else {
             (void)hipGetLastError();  // a workspace that did not fit: the direct probe
@@ -1226,15 +1207,6 @@ void xs_bank_close(xs_bank* b) {
     for (auto& ev : b->hstage_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (b->bloom_ev) (void)hipEventDestroy(b->bloom_ev);
-    for (hipStream_t st : {b->cp_hs, b->cp_ls})
-        if (st) (void)hipStreamSynchronize(st);
-    if (b->cp_ev_in) (void)hipEventDestroy(b->cp_ev_in);
-    for (uint32_t i = 0; i < kCobsPartMaxSub; ++i) {
-        if (b->cp_ev_b[i]) (void)hipEventDestroy(b->cp_ev_b[i]);
-        if (b->cp_ev_l[i]) (void)hipEventDestroy(b->cp_ev_l[i]);
-    }
-    for (hipStream_t st : {b->cp_hs, b->cp_ls})
-        if (st) (void)hipStreamDestroy(st);
     for (auto& ev : b->chunk_ev) (void)hipEventDestroy(ev);
     for (auto& ev : b->events) {
         (void)hipEventDestroy(ev.first);

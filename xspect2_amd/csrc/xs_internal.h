@@ -115,13 +115,13 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
                                    hipStream_t s);
 // Partitioned COBS probe (xs_probe_cobspart.hip) for classic banks of <= 128
 // docs (16-B rows) larger than the Infinity Cache.
-constexpr uint32_t kCobsPartMaxSub = 8;
+constexpr uint32_t kCobsPartWsMiB = 24 << 10;  // default cap of a range's entries + rows
 struct CobsPartPlan {
     uint32_t ck;         // k-mers per bucket block (1024, 2048 or 4096)
-    uint32_t nsub;       // bucket-block ranges pipelined over three streams (1: one stream)
     uint32_t shift;      // log2 rows per partition
     uint32_t P;          // partitions
-    uint64_t tstride;    // bucket blocks (>= the call's k-mers / kPartKmers)
+    uint64_t nblk;       // bucket blocks (>= the call's k-mers / ck)
+    uint64_t rblk;       // bucket blocks per range (one workspace, reused range after range)
     uint64_t kbound;     // upper bound of the call's sampled k-mers
     size_t entry_bytes, tbl_bytes, nkc_bytes, scan_bytes, aux_bytes;
 };
@@ -130,15 +130,12 @@ struct PartWs {
     uint64_t* kofs;      // n+1 exclusive scan: first k-mer id of each read
     void* scan_tmp;
     size_t scan_bytes;
-    void* entries;       // u32 entries (row in partition << 10 | k-mer in block), then their 16-B rows
-    uint16_t* tbl;       // (P+1) x tstride partition starts per bucket block, + block-major copy
+    void* entries;       // a range's u32 entries (row in partition << id bits | k-mer in block), then their 16-B rows
+    uint16_t* tbl;       // (P+1) x rblk partition starts per bucket block, + block-major copy
     uint32_t* aux;       // bucket block -> read holding its first k-mer, then per-partition queue counters
-    hipStream_t hs, ls;  // bucket and lookup streams when plan.nsub > 1
-    hipEvent_t ev_in;    // the caller's stream has the batch's k-mer map
-    hipEvent_t ev_b[kCobsPartMaxSub], ev_l[kCobsPartMaxSub];  // range i bucketed / looked up
 };
 // False when the direct probe should run (bank not classic 16-B rows, under
-// 256 MiB, h > 8, a batch too large for the workspace, or
+// 256 MiB, h > 8, more than 2^32 k-mers in the call, or
 // XSPECT2_AMD_COBS_PART=0).
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
                     CobsPartPlan* plan);

@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
                                                                      uint16_t* __restrict__ tbm,
                                                                      const uint32_t* __restrict__ blk_read,
                                                                      uint64_t b_begin) {
+    // entries and partition starts of block B go to row B - b_begin of the range's workspace
     constexpr int BT = bucket_threads<CK>();
     constexpr int IDB = id_bits<CK>();
     using Scan = hipcub::BlockScan<uint32_t, BT>;
@@ -144,10 +145,10 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
         const uint32_t p = tid * ITEMS + q;
         if (p < P) {
             cur[p] = v[q];
-            tbm[B * (P + 1) + p] = (uint16_t)v[q];
+            tbm[(B - b_begin) * (P + 1) + p] = (uint16_t)v[q];
         }
     }
-    if (tid == 0) tbm[B * (P + 1) + P] = (uint16_t)(m * H);
+    if (tid == 0) tbm[(B - b_begin) * (P + 1) + P] = (uint16_t)(m * H);
     __syncthreads();
     const uint32_t omask = (1u << shift) - 1;
 #pragma unroll
@@ -165,7 +166,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
     }
     __syncthreads();
     // coalesced copy-out (regions of CK*H entries: 16-B aligned)
-    const uint64_t base = B * CK * H;
+    const uint64_t base = (B - b_begin) * CK * H;  // the range reuses one workspace
     const uint32_t tot = m * H;
     for (uint32_t e = tid * 4; e < tot; e += BT * 4) {
         if (e + 4 <= tot) {
@@ -177,9 +178,10 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
 }
 
 // The waves of one XCD work through one partition at a time (its rows stay in
-// the XCD's L2 while the entries stream past), taking groups of 64 bucket
-// blocks from the partition's queue counter (the rbloom lookup's scheme,
-// xs_probe_bloompart.hip).  Each entry's row goes back in entry order; with
+// the XCD's L2 while the entries stream past), taking groups of gb <= 64
+// bucket blocks from the partition's queue counter (the rbloom lookup's
+// scheme, xs_probe_bloompart.hip; gb shrinks for short ranges so that a
+// partition still has a group for every wave of its XCD).  Each entry's row goes back in entry order; with
 // EMB (D <= kEmbMaxDocs) the entry's k-mer id rides in the row's unused top
 // bits (docs 118..127), so the resolve pass need not read the entries again.
 template <int CK>
@@ -190,11 +192,13 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
                                                           const uint16_t* __restrict__ tbl,
                                                           uint4* __restrict__ out, uint32_t* qctr,
-                                                          uint64_t b_begin, uint64_t b_end) {
+                                                          uint64_t b_begin, uint64_t b_end, uint32_t gb) {
     constexpr int IDB = id_bits<CK>();
     const int lane = threadIdx.x & 63;
-    // this call's bucket blocks: b_begin .. b_end-1, those past the batch's last k-mer excluded
-    const uint64_t nblk = min(b_end, (kofs[n] + CK - 1) / CK);
+    // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
+    // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
+    const uint64_t last = min(b_end, (kofs[n] + CK - 1) / CK);
+    const uint64_t nblk = last > b_begin ? last - b_begin : 0;
     const uint64_t cap = (uint64_t)CK * H;
     const uint32_t xcd = blockIdx.x & 7;
     for (uint64_t p = xcd; p < P; p += 8) {
@@ -204,11 +208,11 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
         for (;;) {
             uint32_t grp = 0;
             if (lane == 0) grp = atomicAdd(&qctr[p * kQStride], 1u);
-            const uint64_t b0 = b_begin + (uint64_t)__builtin_amdgcn_readfirstlane(grp) * 64;
+            const uint64_t b0 = (uint64_t)__builtin_amdgcn_readfirstlane(grp) * gb;
             if (b0 >= nblk) break;
             const uint64_t b = b0 + lane;
             uint32_t s = 0, len = 0;
-            if (b < nblk) {
+            if ((uint32_t)lane < gb && b < nblk) {
                 s = t0[b];
                 len = (uint32_t)t1[b] - s;
             }
@@ -317,7 +321,7 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
         for (uint32_t x = tid; x <= nr; x += kResolveThreads) s_kofs[x] = kofs[lo + x];
     }
     __syncthreads();
-    const uint64_t base = B * CK * H;
+    const uint64_t base = (B - b_begin) * CK * H;
     const uint32_t tot = m * H;
     // kResolveUnroll rows in flight per lane, then their LDS ANDs
     for (uint32_t e0 = tid; e0 < tot; e0 += kResolveThreads * kResolveUnroll) {
@@ -455,21 +459,26 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     if (kbound >= (1ull << 32)) return false;
     const uint64_t nblk = (kbound + ck - 1) / ck;
     const uint64_t P = parts(shift);
+    // The bucket blocks run in ranges that reuse one workspace of at most
+    // XSPECT2_AMD_CP_WS_MB MiB of entries + rows (default kCobsPartWsMiB), so
+    // any batch size fits.
+    const uint64_t per_block = (uint64_t)ck * bv.h * (sizeof(uint32_t) + sizeof(uint4));
+    const uint64_t cap = (uint64_t)std::max(1, env_int("XSPECT2_AMD_CP_WS_MB", (int)kCobsPartWsMiB)) << 20;
+    const uint64_t rblk = std::max<uint64_t>(1, std::min<uint64_t>(nblk, cap / per_block));
     plan->ck = ck;
-    plan->nsub = (uint32_t)std::min(std::max(env_int("XSPECT2_AMD_CP_SUB", 1), 1), (int)kCobsPartMaxSub);
     plan->shift = shift;
     plan->P = (uint32_t)P;
-    plan->tstride = nblk;
+    plan->nblk = nblk;
+    plan->rblk = rblk;
     plan->kbound = kbound;
-    plan->entry_bytes = nblk * ck * bv.h * (sizeof(uint32_t) + sizeof(uint4));  // entries, then their rows
-    plan->tbl_bytes = 2 * (P + 1) * nblk * sizeof(uint16_t);                    // partition- + block-major
-    plan->aux_bytes = (nblk + 1 + kQStride) * sizeof(uint32_t) + (size_t)P * kQStride * kCobsPartMaxSub * sizeof(uint32_t);
+    plan->entry_bytes = rblk * per_block;                            // a range's entries, then their rows
+    plan->tbl_bytes = 2 * (P + 1) * rblk * sizeof(uint16_t);         // partition- + block-major
+    plan->aux_bytes = (nblk + 1 + kQStride) * sizeof(uint32_t) + (size_t)P * kQStride * sizeof(uint32_t);
     plan->nkc_bytes = (n + 1) * sizeof(uint64_t);
     size_t sb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(n + 1));
     plan->scan_bytes = sb;
-    // entries are transient: cap the workspace (larger batches take the direct probe)
-    return plan->entry_bytes <= (48ull << 30);
+    return true;
 }
 
 static int cobs_lookup_grid(int per_cu_want) {
@@ -494,67 +503,50 @@ template <int U, int ST, int CK>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
                           uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
+    // groups per partition >= the XCD's waves (grid / 8 workgroups x 4 waves)
+    const uint64_t waves = (uint64_t)grid / 8 * 4;
+    const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
     if (emb)
-        cobs_lookup_kernel<U, ST, true, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.tstride,
-                                                                 ent, tbl, rowv, qctr, b0, b1);
+        cobs_lookup_kernel<U, ST, true, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+                                                                 ent, tbl, rowv, qctr, b0, b1, gb);
     else
-        cobs_lookup_kernel<U, ST, false, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.tstride,
-                                                                  ent, tbl, rowv, qctr, b0, b1);
+        cobs_lookup_kernel<U, ST, false, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+                                                                  ent, tbl, rowv, qctr, b0, b1, gb);
 }
 
-// Bucket blocks are processed in plan.nsub consecutive ranges.  With more than
-// one, range i's bucket (VALU-bound hashing) runs on ws.hs while range i-1's
-// lookup (L2 gathers) runs on ws.ls and range i-2's resolve (streaming) on the
-// caller's stream s, so the three passes overlap.
+// Ranges of plan.rblk bucket blocks, one after the other on stream s, each
+// through bucket -> transpose -> lookup -> resolve in the same workspace.
 template <int CK>
 static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uint32_t H, const CobsPartPlan& plan,
                                      const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
                                      hipStream_t s) {
     hipError_t e;
-    const uint64_t ne = plan.tstride * CK * H;
+    const uint64_t ne = plan.rblk * CK * H;
     uint32_t* ent = reinterpret_cast<uint32_t*>(ws.entries);
     uint4* rowv = reinterpret_cast<uint4*>(ent + (ne + 3) / 4 * 4);
     uint32_t* blk_read = ws.aux;
-    uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.tstride;  // block-major copy
-    uint32_t* qctr0 = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
+    uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.rblk;  // block-major copy
+    uint32_t* qctr = ws.aux + (plan.nblk + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
-    const uint32_t S = plan.nsub;
-    const bool multi = S > 1;
-    hipStream_t hs = multi ? ws.hs : s, ls = multi ? ws.ls : s;
-    if (multi) {
-        if ((e = hipEventRecord(ws.ev_in, s)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(hs, ws.ev_in, 0)) != hipSuccess) return e;
-        if ((e = hipStreamWaitEvent(ls, ws.ev_in, 0)) != hipSuccess) return e;
-    }
     const bool emb = pb.D <= emb_max_docs<CK>();
     const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", 3));
     const int var = env_int("XSPECT2_AMD_CP_LOOKUP", 0);
-    for (uint32_t i = 0; i < S; ++i) {
-        const uint64_t b0 = plan.tstride * i / S, b1 = plan.tstride * (i + 1) / S;
-        if (b1 == b0) continue;
+    for (uint64_t b0 = 0; b0 < plan.nblk; b0 += plan.rblk) {
+        const uint64_t b1 = std::min(plan.nblk, b0 + plan.rblk);
         const unsigned nb = (unsigned)(b1 - b0);
         if (rv.k == 21 && H == 7)
-            cobs_bucket_kernel<21, 7, CK><<<nb, bucket_threads<CK>(), 0, hs>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
-                                                                             ent, tbm, blk_read, b0);
-        else
-            cobs_bucket_kernel<0, 0, CK><<<nb, bucket_threads<CK>(), 0, hs>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
+            cobs_bucket_kernel<21, 7, CK><<<nb, bucket_threads<CK>(), 0, s>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
                                                                             ent, tbm, blk_read, b0);
-        part_transpose_kernel<<<dim3((nb + 63) / 64, (plan.P + 1 + 63) / 64), 256, 0, hs>>>(
-            tbm, plan.P + 1, plan.tstride, ws.tbl, b0, b1);
-        uint32_t* qctr = qctr0 + (size_t)i * plan.P * kQStride;
-        if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), hs)) != hipSuccess) return e;
-        if (multi) {
-            if ((e = hipEventRecord(ws.ev_b[i], hs)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(ls, ws.ev_b[i], 0)) != hipSuccess) return e;
-        }
+        else
+            cobs_bucket_kernel<0, 0, CK><<<nb, bucket_threads<CK>(), 0, s>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
+                                                                           ent, tbm, blk_read, b0);
+        part_transpose_kernel<<<dim3((nb + 63) / 64, (plan.P + 1 + 63) / 64), 256, 0, s>>>(
+            tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
+        if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
         switch (var) {
-            case 1: lookup_launch<4, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
-            case 2: lookup_launch<8, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
-            default: lookup_launch<8, 0, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, ls); break;
-        }
-        if (multi) {
-            if ((e = hipEventRecord(ws.ev_l[i], ls)) != hipSuccess) return e;
-            if ((e = hipStreamWaitEvent(s, ws.ev_l[i], 0)) != hipSuccess) return e;
+            case 1: lookup_launch<4, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 2: lookup_launch<8, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            default: lookup_launch<8, 0, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
