@@ -137,13 +137,14 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     ob = oracle_mod.CobsBank(rows.reshape(-1), [sig], 13, D, h, k)
     gb = xs.Bank.create_cobs(k, h, [sig], D, [f"d{i}" for i in range(D)])
     gb.upload(ob.rows)
-    reads = _reads(rng, 12_000, k, min_len=140, max_len=160)
+    reads = _reads(rng, 60_000, k, min_len=140, max_len=160)  # > 2^23 k-mers: the default takes the path
     reads += _reads(rng, 300, k, alphabet="ACGTacgtNRY", min_len=0, max_len=400)
     reads += [b"", b"A" * (k - 1), _reads(rng, 1, k, min_len=5000, max_len=5001)[0]]
+    want = {}
     for step in (1, 3):
         want_h, want_n = ob.query(reads, step=step)
-        got_h, got_n = gb.query(reads, step=step)
-        assert gb.probe_path() == _lib.XS_PATH_PARTITIONED
+        want[step] = (want_h, want_n)
+        got_h, got_n = gb.query(reads, step=step)  # host batches: the first 8 MiB chunk takes the path
         assert np.array_equal(got_n, want_n)
         assert np.array_equal(got_h, want_h), int((got_h != want_h).sum())
         tot, nk = gb.query_totals(reads, step=step)
@@ -165,8 +166,10 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     d_tot = torch.empty(D + 1, dtype=torch.int64, device=dev)
     st = torch.cuda.Stream(dev)
     torch.cuda.synchronize()
-    gb.query_device(d_seq, int(pr.offsets[-1]), d_off, pr.n, 3, d_hits, d_nk, d_tot, stream=st.cuda_stream)
+    gb.query_device(d_seq, int(pr.offsets[-1]), d_off, pr.n, 1, d_hits, d_nk, d_tot, stream=st.cuda_stream)
     st.synchronize()
+    assert gb.probe_path() == _lib.XS_PATH_PARTITIONED  # one call of 60 k reads: over the default threshold
+    want_h, want_n = want[1]
     assert np.array_equal(d_hits.cpu().numpy().view(np.uint32), want_h)
     tot = d_tot.cpu().numpy().view(np.uint64)
     assert np.array_equal(tot[:D], want_h.sum(axis=0, dtype=np.uint64)) and int(tot[D]) == int(want_n.sum())

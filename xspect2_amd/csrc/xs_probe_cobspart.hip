@@ -421,7 +421,8 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
 }  // namespace
 
 // XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for classic banks of <= 128 docs larger than the Infinity Cache;
+// probe for classic banks of <= 128 docs larger than the Infinity Cache and
+// batches of at least kCobsPartMinKmers k-mers;
 // 2 = partitioned for such banks of any size; 3 = as 2 with partitions down
 // to 1024 rows (tests reach many partitions on small banks).  Read per call.
 static int cobs_part_env() {
@@ -457,6 +458,9 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     if (shift + idb > 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
     if (kbound >= (1ull << 32)) return false;
+    // small batches: the direct probe is faster below ~60-100 k reads of 150 bp
+    // (profiles/r02_cobspart_small.txt)
+    if (mode == 1 && kbound < kCobsPartMinKmers) return false;
     const uint64_t nblk = (kbound + ck - 1) / ck;
     const uint64_t P = parts(shift);
     // The bucket blocks run in ranges that reuse one workspace of at most
