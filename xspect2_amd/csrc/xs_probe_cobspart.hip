@@ -186,7 +186,10 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
 // bits (docs 118..127), so the resolve pass need not read the entries again.
 template <int CK>
 constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
-template <int kUnroll, int STORE, bool EMB, int CK>
+// GAUX: cache-policy bits of the row gathers (0: a plain global load; else a
+// buffer load with aux = GAUX: 2 nt, 16 sc1, 17 sc0 sc1).  STORE 3: buffer
+// stores with aux = SAUX.  A/B variants (XSPECT2_AMD_CP_LOOKUP).
+template <int kUnroll, int STORE, bool EMB, int CK, int GAUX = 0, int SAUX = 0>
 __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
                                                           uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
@@ -247,7 +250,14 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
-                        v[u] = prow[e[u] >> IDB];
+                        if constexpr (GAUX == 0) {
+                            v[u] = prow[e[u] >> IDB];
+                        } else {
+                            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(prow), (short)0,
+                                                                              (int)(16u << shift), 0x00020000);
+                            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((e[u] >> IDB) * 16u), 0, GAUX);
+                            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                        }
                     }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
@@ -263,6 +273,11 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                         } else if constexpr (STORE == 2) {
                             u32x4 w4 = {v[u].x, v[u].y, v[u].z, v[u].w};
                             __builtin_nontemporal_store(w4, reinterpret_cast<u32x4*>(out + pos[u]));
+                        } else if constexpr (STORE == 3) {  // this group's output region through one rsrc
+                            const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + b0 * cap, (short)0, 0x7FFFFFFF,
+                                                                              0x00020000);
+                            u32x4 w4 = {v[u].x, v[u].y, v[u].z, v[u].w};
+                            __builtin_amdgcn_raw_buffer_store_b128(w4, rs, (int)((pos[u] - b0 * cap) * 16u), 0, SAUX);
                         } else {
                             out[pos[u]] = v[u];
                         }
@@ -503,7 +518,7 @@ static int cobs_lookup_grid(int per_cu_want) {
 
 // Lookup variants for A/B (XSPECT2_AMD_CP_LOOKUP): unroll x store kind.
 // XSPECT2_AMD_CP_PERCU: lookup blocks per CU (default 3).
-template <int U, int ST, int CK>
+template <int U, int ST, int CK, int GA = 0, int SA = 0>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
                           uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
@@ -511,10 +526,10 @@ static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t
     const uint64_t waves = (uint64_t)grid / 8 * 4;
     const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
     if (emb)
-        cobs_lookup_kernel<U, ST, true, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+        cobs_lookup_kernel<U, ST, true, CK, GA, SA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
                                                                  ent, tbl, rowv, qctr, b0, b1, gb);
     else
-        cobs_lookup_kernel<U, ST, false, CK><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+        cobs_lookup_kernel<U, ST, false, CK, GA, SA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
                                                                   ent, tbl, rowv, qctr, b0, b1, gb);
 }
 
