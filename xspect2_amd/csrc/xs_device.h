@@ -94,26 +94,6 @@ __device__ __forceinline__ uint32_t kmer_u8(const Kmer& c, uint32_t off) {
     return (c.w[off >> 2] >> ((off & 3) * 8)) & 0xFF;
 }
 
-// Window of k bytes at byte offset `off` of `base`, as dwords (tail zeroed).
-template <int KT>
-__device__ __forceinline__ void load_window(const uint8_t* base, uint64_t off, uint32_t k,
-                                            uint32_t (&w)[8]) {
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(base + (off & ~3ull));
-    const uint32_t sh = (uint32_t)(off & 3);
-    const uint32_t nw = KT ? (KT + 3) / 4 : (k + 3) / 4;
-    uint32_t raw[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) raw[i] = (i <= (int)nw) ? p[i] : 0u;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        uint32_t v = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
-        const int kk = KT ? KT : (int)k;
-        const int valid = kk - 4 * i;  // bytes of word i that belong to the k-mer
-        v = valid >= 4 ? v : (valid <= 0 ? 0u : (v & ((1u << (8 * valid)) - 1u)));
-        w[i] = v;
-    }
-}
-
 // Byte-lexicographic min of the forward and reverse-complement windows.
 __device__ __forceinline__ void canonical_select(const uint32_t (&f)[8], const uint32_t (&r)[8],
                                                  Kmer& c) {
@@ -235,11 +215,16 @@ __device__ __forceinline__ uint32_t acgtn_bytes(uint32_t x) {
 }
 
 // COBS normalisation of 4 bytes.  (b & 0xDF) is one of A/C/G/T only for
-// A/C/G/T/a/c/g/t, so the upper-cased test is exact.
+// A/C/G/T/a/c/g/t, so the upper-cased test is exact.  A, C, G, T have the
+// distinct low 3 bits 1, 3, 7, 4: as in acgtn_bytes, v_perm_b32 looks up the
+// one letter an upper-cased byte could be in {-, 'A', -, 'C', 'T', -, -, 'G'}
+// (- = 0xFF) and the byte must equal it.
+__device__ __forceinline__ uint32_t acgt_bytes(uint32_t u) {
+    return zero_bytes(__builtin_amdgcn_perm(0x47FFFF54u, 0x43FF41FFu, u & 0x07070707u) ^ u);
+}
 __device__ __forceinline__ uint32_t cobs_norm4(uint32_t x) {
     const uint32_t u = x & 0xDFDFDFDFu;
-    const uint32_t ok = bytes_equal(u, 'A') | bytes_equal(u, 'C') | bytes_equal(u, 'G') | bytes_equal(u, 'T');
-    const uint32_t m = (ok >> 7) * 0xFFu;
+    const uint32_t m = (acgt_bytes(u) >> 7) * 0xFFu;
     return (u & m) | (0x4E4E4E4Eu & ~m);
 }
 
@@ -282,14 +267,21 @@ template <int KT>
 __device__ __forceinline__ void load_window(const uint8_t* seq, uint64_t seq_bytes, uint64_t off,
                                             uint32_t k, uint32_t (&w)[8]) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(seq) + off;
-    const uint32_t* p = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+    // global address space: plain global loads, counted on vmcnt only
+    const __attribute__((address_space(1))) uint32_t* p =
+        reinterpret_cast<const __attribute__((address_space(1))) uint32_t*>(a & ~(uintptr_t)3);
     const uint32_t sh = (uint32_t)(a & 3);
     const uintptr_t lim = reinterpret_cast<uintptr_t>(seq) + seq_bytes;
     const uint32_t nw = KT ? (KT + 3) / 4 : (k + 3) / 4;
     uint32_t raw[9];
+    if (reinterpret_cast<uintptr_t>(p + nw) < lim) {  // every dword starts inside the buffer: no per-load guard
 #pragma unroll
-    for (int i = 0; i < 9; ++i)
-        raw[i] = (i <= (int)nw && reinterpret_cast<uintptr_t>(p + i) < lim) ? p[i] : 0u;
+        for (int i = 0; i < 9; ++i) raw[i] = i <= (int)nw ? p[i] : 0u;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 9; ++i)
+            raw[i] = (i <= (int)nw && reinterpret_cast<uintptr_t>(p + i) < lim) ? p[i] : 0u;
+    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) w[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
 }
