@@ -186,7 +186,8 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
 // bits (docs 118..127), so the resolve pass need not read the entries again.
 template <int CK>
 constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
-// GAUX: cache-policy bits of the row gathers (0: a plain global load; else a
+// GAUX: cache-policy bits of the row gathers (0: a plain global load; 1: LDS-DMA
+// into per-wave slots; else a
 // buffer load with aux = GAUX: 2 nt, 16 sc1, 17 sc0 sc1).  STORE 3: buffer
 // stores with aux = SAUX.  A/B variants (XSPECT2_AMD_CP_LOOKUP).
 template <int kUnroll, int STORE, bool EMB, int CK, int GAUX = 0, int SAUX = 0>
@@ -198,6 +199,9 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                                                           uint64_t b_begin, uint64_t b_end, uint32_t gb) {
     constexpr int IDB = id_bits<CK>();
     const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    __shared__ uint4 s_rows[GAUX == 1 ? 4 : 1][GAUX == 1 ? kUnroll : 1][64];  // LDS-DMA landing slots
+    (void)wid;
     // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
     // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
     const uint64_t last = min(b_end, (kofs[n] + CK - 1) / CK);
@@ -252,6 +256,10 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                     if (i0 + u * 64 + lane < total) {
                         if constexpr (GAUX == 0) {
                             v[u] = prow[e[u] >> IDB];
+                        } else if constexpr (GAUX == 1) {  // LDS-DMA: the row lands in this wave's slot u
+#if defined(__HIP_DEVICE_COMPILE__)  // a device-only builtin: the host pass must not see it
+                            __builtin_amdgcn_global_load_lds(prow + (e[u] >> IDB), &s_rows[wid][u][0], 16, 0, 0);
+#endif
                         } else {
                             const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(prow), (short)0,
                                                                               (int)(16u << shift), 0x00020000);
@@ -259,6 +267,11 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                             v[u] = make_uint4(w[0], w[1], w[2], w[3]);
                         }
                     }
+                if constexpr (GAUX == 1) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int u = 0; u < kUnroll; ++u) v[u] = s_rows[wid][u][lane];
+                }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
@@ -516,8 +529,6 @@ static int cobs_lookup_grid(int per_cu_want) {
     return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
 }
 
-// Lookup variants for A/B (XSPECT2_AMD_CP_LOOKUP): unroll x store kind.
-// XSPECT2_AMD_CP_PERCU: lookup blocks per CU (default 3).
 template <int U, int ST, int CK, int GA = 0, int SA = 0>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
@@ -548,8 +559,11 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
     uint32_t* qctr = ws.aux + (plan.nblk + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
     const bool emb = pb.D <= emb_max_docs<CK>();
-    const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", 3));
+    // lookup: 0 (default) LDS-DMA row gathers, 6 in flight per lane, 2 workgroups
+    // per CU; 1 register gathers, 8 in flight, 3 per CU (the first build).
+    // XSPECT2_AMD_CP_PERCU overrides the workgroups per CU.
     const int var = env_int("XSPECT2_AMD_CP_LOOKUP", 0);
+    const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", var == 1 ? 3 : 2));
     for (uint64_t b0 = 0; b0 < plan.nblk; b0 += plan.rblk) {
         const uint64_t b1 = std::min(plan.nblk, b0 + plan.rblk);
         const unsigned nb = (unsigned)(b1 - b0);
@@ -563,9 +577,8 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
         if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
         switch (var) {
-            case 1: lookup_launch<4, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 2: lookup_launch<8, 2, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            default: lookup_launch<8, 0, CK>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 1: lookup_launch<8, 0, CK, 0>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            default: lookup_launch<6, 0, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
