@@ -136,8 +136,8 @@ struct PartWs {
     uint32_t* aux;       // bucket block -> read holding its first k-mer, then per-partition queue counters
 };
 // False when the direct probe should run (bank not classic 16-B rows, under
-// 256 MiB, h > 8, fewer than kCobsPartMinKmers or more than 2^32 k-mers in
-// the call, or XSPECT2_AMD_COBS_PART=0).
+// 256 MiB, h > 8, fewer than kCobsPartMinKmers k-mers in the call, or
+// XSPECT2_AMD_COBS_PART=0).
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
                     CobsPartPlan* plan);
 hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const CobsPartPlan& plan,

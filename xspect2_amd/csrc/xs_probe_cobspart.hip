@@ -485,7 +485,6 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     while (parts(shift) > kPartMax) ++shift;
     if (shift + idb > 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
-    if (kbound >= (1ull << 32)) return false;
     // small batches: the direct probe is faster below ~60-100 k reads of 150 bp
     // (profiles/r02_cobspart_small.txt)
     if (mode == 1 && kbound < kCobsPartMinKmers) return false;
