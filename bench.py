@@ -21,7 +21,7 @@ Other workloads (SURVEY.md §8(d) configs 4/5 and the genus path):
 metric = k-mer x filter probes/s = sum(ceil((L-k+1)/step)) x docs / second,
 whole job.  roofline prices the probe alone (HIP events on its launch
 stream around every probe of the timed region) at its algorithmic bytes.
-Species banks over 256 MiB take the partitioned COBS pipeline (bucket ->
+Species banks of 32 MiB and more take the partitioned COBS pipeline (bucket ->
 per-XCD L2 lookup -> resolve): SURVEY.md §8(d)'s h x 64 B per k-mer.  The
 direct kernels: one 128-byte L2 line fill per random row (COBS: h rows per
 k-mer and doc group; rbloom: K dwords per k-mer; MLST: the 64-byte rows

@@ -117,6 +117,7 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
 // docs (16-B rows) larger than the Infinity Cache.
 constexpr uint32_t kCobsPartWsMiB = 24 << 10;  // default cap of a range's entries + rows
 constexpr uint64_t kCobsPartMinKmers = 1ull << 23;  // default mode: smaller batches take the direct probe
+constexpr uint64_t kCobsPartMinBankMiB = 32;         // default mode: smaller banks take the direct probe
 struct CobsPartPlan {
     uint32_t ck;         // k-mers per bucket block (1024, 2048 or 4096)
     uint32_t shift;      // log2 rows per partition
@@ -136,7 +137,7 @@ struct PartWs {
     uint32_t* aux;       // bucket block -> read holding its first k-mer, then per-partition queue counters
 };
 // False when the direct probe should run (bank not classic 16-B rows, under
-// 256 MiB, h > 8, fewer than kCobsPartMinKmers k-mers in the call, or
+// kCobsPartMinBankMiB, h > 8, fewer than kCobsPartMinKmers k-mers in the call, or
 // XSPECT2_AMD_COBS_PART=0).
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
                     CobsPartPlan* plan);

@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
 }  // namespace
 
 // XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for classic banks of <= 128 docs larger than the Infinity Cache and
+// probe for classic banks of <= 128 docs of at least kCobsPartMinBankMiB and
 // batches of at least kCobsPartMinKmers k-mers;
 // 2 = partitioned for such banks of any size; 3 = as 2 with partitions down
 // to 1024 rows (tests reach many partitions on small banks).  Read per call.
@@ -471,8 +471,9 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     if (bv.G != 1 || bv.pitch != 16 || bv.D > 128 || bv.h == 0 || bv.h > (uint32_t)kMaxH || k > kMaxK) return false;
     const uint64_t sig = bv.sig0;
     if (sig >= (1ull << 32)) return false;
-    // banks under 256 MiB stay Infinity-Cache resident: the direct probe is faster there
-    if (mode == 1 && sig * 16 < (256ull << 20)) return false;
+    // banks that (nearly) fit the XCDs' L2s: the direct probe is as fast there
+    // (15 MB: 11.09 vs 11.03 ms; 61 MB: 14.40 vs 11.53; profiles/r02_cobspart_banksize.txt)
+    if (mode == 1 && sig * 16 < (kCobsPartMinBankMiB << 20)) return false;
     const int ck_env = env_int("XSPECT2_AMD_CP_CK", 2048);
     const uint32_t ck = ck_env == 4096 ? 4096 : ck_env == 1024 ? 1024 : 2048;
     const uint32_t idb = ck == 4096 ? 12 : ck == 2048 ? 11 : 10;
