@@ -116,6 +116,27 @@ def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
     gb.close()
 
 
+@pytest.mark.parametrize("case", ["all_short", "one_read", "one_long_read", "empty_only"])
+def test_partitioned_degenerate_batches(xs, oracle_mod, monkeypatch, case):
+    """Forced partitioned COBS probe on batches with no k-mers at all, a single
+    read, a single read spanning many bucket blocks, and only empty reads:
+    hits, counts and totals equal the oracle's (zeros where no k-mer)."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=12)
+    rng = np.random.default_rng(5)
+    reads = {"all_short": _reads(rng, 500, 21, min_len=0, max_len=21),
+             "one_read": [seqs[0][:150]],
+             "one_long_read": [b"".join(seqs[:4])[:20_000]],
+             "empty_only": [b""] * 7}[case]
+    for step in (1, 2):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n) and np.array_equal(got_h, want_h)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+    gb.close()
+
+
 def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     """Default mode on a classic bank larger than the Infinity Cache (17 M
     rows x 16 B = 272 MB on the device): the query takes the partitioned path
