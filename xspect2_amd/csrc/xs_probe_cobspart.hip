@@ -480,7 +480,7 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     // 2^17 rows (2 MiB) per partition, fewer rows while that leaves under 64
     // partitions (8 per XCD), more while over kPartMax
     const uint32_t floor_shift = mode >= 3 ? 10 : 13;
-    uint32_t shift = 17;
+    uint32_t shift = (uint32_t)std::min(std::max(env_int("XSPECT2_AMD_CP_SHIFT", 17), 10), 21);
     auto parts = [sig](uint32_t s) { return (sig + (1ull << s) - 1) >> s; };
     while (shift > floor_shift && parts(shift) < 64) --shift;
     while (parts(shift) > kPartMax) ++shift;
