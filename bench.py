@@ -190,7 +190,15 @@ class Workload:
         self.nk_read = (args.read_len - self.k + args.step) // args.step
         self.kmers = self.n * self.nk_read
         if w == "multigenus" and world > 1:
-            self.gathered = [torch.empty_like(self.d_hits[0]) for _ in range(world)]
+            # hit rows travel in the narrowest type that holds a read's k-mer count
+            # (1 byte for 150 bp reads; distributed.transport_dtype)
+            from xspect2_amd.distributed import transport_dtype
+            self.wire_dtype = transport_dtype(self.nk_read)
+            self.d_narrow = torch.empty((self.n, self.docs[0]), dtype=self.wire_dtype, device=dev)
+            wire = self.d_narrow.view(torch.float16) if self.wire_dtype == torch.int16 else self.d_narrow
+            self.wire = wire
+            self.gathered = [torch.empty_like(wire) for _ in range(world)]
+            self.config["gather_dtype"] = str(self.wire_dtype).replace("torch.", "")
 
     def _mlst(self, args, dev, s):
         import torch
@@ -254,7 +262,8 @@ class Workload:
                            None if self.args.totals_only else h, self.d_nk, t, stream=self.stream)
         if self.world > 1:
             if self.args.workload == "multigenus":
-                all_gather(self.gathered, self.d_hits[0])  # docs sharded: hit vectors over xGMI
+                self.d_narrow.copy_(self.d_hits[0])      # counts <= k-mers per read: lossless
+                all_gather(self.gathered, self.wire)     # docs sharded: hit vectors over xGMI
             else:
                 for t in self.d_tot:
                     all_reduce(t)  # per-doc totals + k-mer total over all ranks
@@ -414,7 +423,7 @@ def main():
     par = {"species": f"reads sharded x{world}, bank replicated, RCCL all-reduce of D+1 totals",
            "genus": f"reads sharded x{world}, filter replicated, RCCL all-reduce of totals",
            "mlst": f"reads sharded x{world}, loci banks replicated, RCCL all-reduce of totals",
-           "multigenus": f"docs sharded x{world} (one bank per GPU), reads replicated, RCCL all-gather of hits"}
+           "multigenus": f"docs sharded x{world} (one bank per GPU), reads replicated, RCCL all-gather of hit rows in the narrowest exact integer type"}
     line = {
         "metric": METRIC,
         "value": value,

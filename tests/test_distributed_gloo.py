@@ -60,12 +60,18 @@ def _worker(rank: int, world: int, port: int, out_dir: str):
         mine = part_a if rank % 2 == 0 else part_b
         dh, _ = distributed.docs_sharded_hits(
             pr, 1, lambda sl, st: mine.query_packed(sl.buf, sl.offsets, step=st, threads=1))
+        # reads long enough for 2-byte (6,000 bp) and 4-byte (36,000 bp) transport
+        long_reads = reads[:3] + ["".join(reads[i] for i in range(30)) * 2, "".join(reads[:30]) * 12]
+        dl = [distributed.docs_sharded_hits(
+                  pack_sequences(rs), 1, lambda sl, st: mine.query_packed(sl.buf, sl.offsets, step=st, threads=1))[0]
+              for rs in (long_reads[:4], long_reads)]  # int16, then int32 transport
         labels = [f"sp{d:02d}" for d in range(10)][::-1]  # label order differs from doc order
         pred = distributed.reads_sharded_svm_predict(
             pr, 1, labels, lambda sl, st: local_totals(sl, st),
             lambda x: "|".join(f"{v:.2f}" for v in x[0]))  # the vector itself, as the "label"
         np.savez(Path(out_dir) / f"r{rank}.npz", tot=tot, nk=nk, lo=lo, hi=hi, hits=hits,
-                 g_tot=g_tot, g_nk=g_nk, dh=dh, pred=np.array(pred))
+                 g_tot=g_tot, g_nk=g_nk, dh=dh, dl16=dl[0], dl32=dl[1],
+                 pred=np.array(pred))
     finally:
         dist.destroy_process_group()
 
@@ -95,6 +101,15 @@ def test_gloo_reads_and_docs_sharded(tmp_path, world):
     want = np.concatenate([ha if r % 2 == 0 else hb for r in range(world)], axis=1)
     for o in outs:
         assert np.array_equal(o["dh"], want)
+    long_reads = reads[:3] + ["".join(reads[i] for i in range(30)) * 2, "".join(reads[:30]) * 12]
+    for key, rs in (("dl16", long_reads[:4]), ("dl32", long_reads)):
+        ha, na = part_a.query(rs)
+        hb, _ = part_b.query(rs)
+        assert 255 < int(na.max()) <= 32767 if key == "dl16" else int(na.max()) > 32767
+        assert int(ha.max()) > 255  # counts that do not fit a byte travel intact
+        want_l = np.concatenate([ha if r % 2 == 0 else hb for r in range(world)], axis=1)
+        for o in outs:
+            assert np.array_equal(o[key], want_l)
     # SVM vector from the all-reduced totals, formed on rank 0 and broadcast,
     # equals the single-process ModelResult total scores in label order
     from xspect2_amd.result import ModelResult

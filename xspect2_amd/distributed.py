@@ -78,31 +78,55 @@ def reads_sharded_hits(reads: PackedReads, step: int,
     return lo, hi, hits, nk, g_tot, g_nk
 
 
+def transport_dtype(max_count: int):
+    """Narrowest torch dtype that carries hit counts up to `max_count` exactly.
+
+    A read's count for a doc is at most its number of sampled k-mers, so
+    150 bp reads (130 k-mers) travel as one byte per (read, doc) instead of
+    four: the docs-sharded all-gather moves a quarter of the bytes over xGMI."""
+    import torch
+    if max_count <= 255:
+        return torch.uint8
+    if max_count <= 32767:
+        return torch.int16
+    return torch.int32
+
+
 def docs_sharded_hits(reads: PackedReads, step: int,
                       local_query: Callable[[PackedReads, int], tuple[np.ndarray, np.ndarray]],
                       device=None) -> tuple[np.ndarray, np.ndarray]:
-    """Config 5: each rank's bank covers its own docs; gather [n, sum(D_r)] in rank order."""
+    """Config 5: each rank's bank covers its own docs; gather [n, sum(D_r)] in rank order.
+
+    The hit rows travel in the narrowest integer type that holds the largest
+    k-mer count of any read on any rank (agreed by one all-reduce), and are
+    widened back to uint32 on arrival."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
     hits, nk = local_query(reads, step)
     n, d_local = hits.shape
-    dims = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
-    mine = torch.tensor([d_local], dtype=torch.int64)
+    nk = np.asarray(nk)
+    meta = torch.tensor([d_local, int(nk.max()) if nk.size else 0], dtype=torch.int64)
+    dims = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     if device is not None:
         dims = [x.to(device) for x in dims]
-        mine = mine.to(device)
-    dist.all_gather(dims, mine)
-    d_max = max(int(x.item()) for x in dims)
-    pad = np.zeros((n, d_max), dtype=np.int32)
-    pad[:, :d_local] = hits.view(np.int32)
-    t = torch.from_numpy(pad)
+        meta = meta.to(device)
+    dist.all_gather(dims, meta)
+    d_max = max(int(x[0].item()) for x in dims)
+    dt = transport_dtype(max(int(x[1].item()) for x in dims))
+    pad = torch.zeros((n, d_max), dtype=dt)
+    pad[:, :d_local] = torch.from_numpy(hits.astype(np.int64)).to(dt)
     if device is not None:
-        t = t.to(device)
-    parts = [torch.empty_like(t) for _ in range(world)]
-    dist.all_gather(parts, t)
-    cols = [p.cpu().numpy()[:, :int(d.item())] for p, d in zip(parts, dims)]
-    return np.concatenate(cols, axis=1).view(np.uint32), np.asarray(nk)
+        pad = pad.to(device)
+    # gloo and RCCL gather no int16: 2-byte rows travel as float16 bit patterns
+    # (an all-gather copies bits, it does no arithmetic)
+    wire = pad.view(torch.float16) if dt == torch.int16 else pad
+    parts = [torch.empty_like(wire) for _ in range(world)]
+    dist.all_gather(parts, wire)
+    if dt == torch.int16:
+        parts = [p.view(torch.int16) for p in parts]
+    cols = [p.cpu().to(torch.int64).numpy()[:, :int(d[0].item())] for p, d in zip(parts, dims)]
+    return np.concatenate(cols, axis=1).astype(np.uint32), nk
 
 
 def svm_vector(labels: list[str], totals, total_kmers: int) -> list[float]:
