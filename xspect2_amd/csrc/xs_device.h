@@ -57,6 +57,14 @@ __device__ __forceinline__ uint64_t fastmod(uint64_t x, uint64_t d, uint64_t m) 
     r = r >= d ? r - d : r;
     return r >= d ? r - d : r;
 }
+// The same for d < 2^30: the remainder before correction is below 3d < 2^32,
+// so x - q*d is exact in 32 bits (the high words cancel) and the corrections
+// are 32-bit compares.  Callers check d on the host.
+__device__ __forceinline__ uint32_t fastmod_small(uint64_t x, uint32_t d, uint64_t m) {
+    uint32_t r = (uint32_t)x - (uint32_t)__umul64hi(x, m) * d;
+    r = r >= d ? r - d : r;
+    return r >= d ? r - d : r;
+}
 
 // One step of the 128-bit LCG (state sh:sl): state = state * M + C mod 2^128.
 // sl * Ml is formed once from four 32 x 32 partial products and gives both

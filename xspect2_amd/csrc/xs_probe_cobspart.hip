@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
 #pragma unroll
             for (int j = 0; j < NH; ++j) {
                 if ((uint32_t)j < H) {
-                    row[q][j] = (uint32_t)fastmod(xxh64_seed<KT>(c[q], pre, k, (uint64_t)j), pb.sig, pb.magic);
+                    row[q][j] = fastmod_small(xxh64_seed<KT>(c[q], pre, k, (uint64_t)j), (uint32_t)pb.sig, pb.magic);
                     atomicAdd(&cur[row[q][j] >> shift], 1u);
                 }
             }
@@ -470,7 +470,7 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     if (mode <= 0) return false;
     if (bv.G != 1 || bv.pitch != 16 || bv.D > 128 || bv.h == 0 || bv.h > (uint32_t)kMaxH || k > kMaxK) return false;
     const uint64_t sig = bv.sig0;
-    if (sig >= (1ull << 32)) return false;
+    if (sig >= (1ull << 30)) return false;  // fastmod_small in the bucket pass
     // banks that (nearly) fit the XCDs' L2s: the direct probe is as fast there
     // (15 MB: 11.09 vs 11.03 ms; 61 MB: 14.40 vs 11.53; profiles/r02_cobspart_banksize.txt)
     if (mode == 1 && sig * 16 < (kCobsPartMinBankMiB << 20)) return false;

@@ -71,7 +71,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
                     uint32_t off[HT];
 #pragma unroll
                     for (int j = 0; j < HT; ++j)
-                        off[j] = (uint32_t)fastmod(xxh64_seed<KT>(c, pre, k, (uint64_t)j), fb.sig, fb.magic) * 16u;
+                        off[j] = fastmod_small(xxh64_seed<KT>(c, pre, k, (uint64_t)j), (uint32_t)fb.sig, fb.magic) * 16u;
                     m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                     for (int j = 0; j < HT; ++j)

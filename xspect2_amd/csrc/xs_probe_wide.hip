@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_
     const uint64_t D = bv.D;
     const uint32_t cpg = bv.nchunks;   // data chunks per group, <= C (host-checked)
     const uint64_t gdocs = 8 * bv.page;  // docs per group
-    GroupDesc gd[GM];                  // G == GM, every sig < 2^32 (host-checked): 32-bit row indices
+    GroupDesc gd[GM];                  // G == GM, every sig < 2^30 (host-checked): 32-bit row indices
 #pragma unroll
     for (int g = 0; g < GM; ++g) gd[g] = bv.groups[g];
     const uint32_t pitch = bv.pitch;
@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_
                         if ((uint32_t)j < h) {
                             const uint64_t hv = xxh64_seed<KT>(c, pre, k, (uint64_t)j);
 #pragma unroll
-                            for (int g = 0; g < GM; ++g) ri[g][j] = (uint32_t)fastmod(hv, gd[g].sig, gd[g].magic);
+                            for (int g = 0; g < GM; ++g) ri[g][j] = fastmod_small(hv, (uint32_t)gd[g].sig, gd[g].magic);
                         }
                 }
                 const uint32_t tile = min(64u, cnt - tb);
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_
 // data chunks; compact banks of 2..4 groups whose pages are 2..4 chunks (MLST
 // loci: 3 groups of 64-byte pages).
 int wide_for(const CobsView& bv) {
-    if (bv.G < 1 || bv.G > 4 || bv.nchunks < 2 || bv.sig_max >= (1ull << 32)) return 0;
+    if (bv.G < 1 || bv.G > 4 || bv.nchunks < 2 || bv.sig_max >= (1ull << 30)) return 0;  // fastmod_small
     if (bv.G == 1 && bv.nchunks > 16) return 0;
     if (bv.G > 1 && bv.nchunks > 4) return 0;
     return bv.nchunks == 2 ? 2 : bv.nchunks <= 4 ? 4 : bv.nchunks <= 8 ? 8 : 16;
