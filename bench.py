@@ -22,8 +22,9 @@ metric = k-mer x filter probes/s = sum(ceil((L-k+1)/step)) x docs / second,
 whole job.  roofline prices the probe alone (HIP events on its launch
 stream around every probe of the timed region) at its algorithmic bytes.
 Species banks of 32 MiB and more take the partitioned COBS pipeline (bucket ->
-per-XCD L2 lookup -> resolve): SURVEY.md §8(d)'s h x 64 B per k-mer.  The
-direct kernels: one 128-byte L2 line fill per random row (COBS: h rows per
+per-XCD L2 lookup -> resolve), genus filters of 16 MiB and more on member-rich
+input the partitioned rbloom pipeline: SURVEY.md §8(d)'s 64 B per row or
+filter word (h or K per k-mer).  The direct kernels: one 128-byte L2 line fill per random row (COBS: h rows per
 k-mer and doc group; rbloom: K dwords per k-mer; MLST: the 64-byte rows
 themselves, its banks being Infinity-Cache resident).  Both + the read bytes,
 hit matrix and per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per
@@ -274,20 +275,15 @@ class Workload:
 
     def algo_bytes_per_launch(self):
         """Bytes one probe launch must move (per bank; averaged over banks)."""
-        if getattr(self, "partitioned", False) == "cobs":
-            # SURVEY.md §8(d)'s algorithmic figure: h rows x 64 B per k-mer (one
-            # random row transaction each), + the read bytes, hit rows and
-            # per-read metadata.  The partitioned pipeline fetches no row as a
-            # random HBM line (PMC traffic per step is below this figure).
+        if getattr(self, "partitioned", False):
+            # SURVEY.md §8(d)'s algorithmic figure for both partitioned pipelines:
+            # one random 64-B transaction per row (COBS: h per k-mer) or filter
+            # word (rbloom: K per k-mer), + the read bytes, hit rows and per-read
+            # metadata.  The pipelines fetch no row or word as a random HBM line
+            # (their PMC traffic per step is below this figure).
             d = self.docs[0]
             return (self.kmers * self.rows_per_kmer * SURVEY_ROW_BYTES + self.seq_bytes + self.n * d * 4
                     + self.n * (8 + 4 + 8 + 8))
-        if getattr(self, "partitioned", False):
-            # partitioned rbloom pipeline, per filter bit tested: 4-B offset + 2-B
-            # k-mer id written and the offset read back, a miss byte zeroed,
-            # (sometimes) set and read; plus the filter once and the reads
-            entries = self.kmers * self.rows_per_kmer
-            return entries * 13 + self.banks[0].info.device_bytes + self.seq_bytes + self.n * (8 + 4 + 8 + 8)
         per_bank = []
         for d in self.docs:
             rows = self.rows_per_kmer if self.args.workload != "mlst" else self.rows_per_kmer / len(self.docs)
@@ -381,10 +377,11 @@ def main():
     elif wl.partitioned:
         wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 2 MiB filter partition) -> "
                      "bloom_lookup (per-XCD L2-resident partition) -> resolve -> count")
-        wl.row_bytes = None
-        wl.roofline_note = ("streamed bytes of the partitioned pipeline (13 B per filter bit tested + filter + "
-                            "reads); the bounds are VALU (hashing in bloom_bucket) and the L2 gather rate "
-                            "(bloom_lookup), not HBM: see DESIGN.md")
+        wl.row_bytes = SURVEY_ROW_BYTES
+        wl.roofline_note = ("achieved = SURVEY.md §8(d)'s algorithmic bytes (K x 64 B per k-mer + reads, hits, "
+                            "metadata) over the whole probe (HIP events around the pipeline); traffic = PMC HBM "
+                            "bytes of the pipeline per step, below the algorithmic figure.  Per-kernel bounds: "
+                            "bucket = VALU (XXH3, LCG, Barrett), lookup = vector-L1 miss path to L2; see DESIGN.md")
     elif rows_read:  # rbloom: the data-dependent count of filter words loaded
         wl.rows_per_kmer = rows_read / max(1, launches) / wl.kmers
     algo_bytes = wl.algo_bytes_per_launch()
