@@ -81,8 +81,9 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
 
 @pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
                                                                                   (64, 31, 8, [300_007])])
-@pytest.mark.parametrize("ck,ws_mb", [("1024", None), ("2048", None), ("4096", None), ("2048", "1"), ("1024", "2")])
-def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb):
+@pytest.mark.parametrize("ck,ws_mb,lookup", [("1024", None, None), ("2048", None, None), ("4096", None, None),
+                                             ("2048", "1", None), ("1024", "2", None), ("2048", None, "1")])
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
     L2-resident lookup, per-block AND + count) with partitions down to 1024
     rows, every bucket block size, and workspaces of 1-2 MiB (the bucket
@@ -92,6 +93,8 @@ def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D
     monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
+    if lookup:  # the register-gather lookup instead of LDS-DMA
+        monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
 
 

@@ -186,11 +186,11 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
 // bits (docs 118..127), so the resolve pass need not read the entries again.
 template <int CK>
 constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
-// GAUX: cache-policy bits of the row gathers (0: a plain global load; 1: LDS-DMA
-// into per-wave slots; else a
-// buffer load with aux = GAUX: 2 nt, 16 sc1, 17 sc0 sc1).  STORE 3: buffer
-// stores with aux = SAUX.  A/B variants (XSPECT2_AMD_CP_LOOKUP).
-template <int kUnroll, int STORE, bool EMB, int CK, int GAUX = 0, int SAUX = 0>
+// DMA: rows gathered by LDS-DMA into per-wave slots (default), else into
+// registers.  Rows go back with non-temporal dword stores (7.8 vs 10.1 ms for
+// one plain dwordx4 in tools/partgather.hip; the other store and load cache
+// policies measured no better: profiles/r02_cobspart_ab.txt item 9).
+template <int kUnroll, bool EMB, int CK, bool DMA>
 __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
                                                           uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
     constexpr int IDB = id_bits<CK>();
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    __shared__ uint4 s_rows[GAUX == 1 ? 4 : 1][GAUX == 1 ? kUnroll : 1][64];  // LDS-DMA landing slots
+    __shared__ uint4 s_rows[DMA ? 4 : 1][DMA ? kUnroll : 1][64];  // LDS-DMA landing slots
     (void)wid;
     // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
     // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
@@ -254,20 +254,15 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
-                        if constexpr (GAUX == 0) {
-                            v[u] = prow[e[u] >> IDB];
-                        } else if constexpr (GAUX == 1) {  // LDS-DMA: the row lands in this wave's slot u
+                        if constexpr (DMA) {  // the row lands in this wave's slot u
 #if defined(__HIP_DEVICE_COMPILE__)  // a device-only builtin: the host pass must not see it
                             __builtin_amdgcn_global_load_lds(prow + (e[u] >> IDB), &s_rows[wid][u][0], 16, 0, 0);
 #endif
                         } else {
-                            const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint4*>(prow), (short)0,
-                                                                              (int)(16u << shift), 0x00020000);
-                            const auto w = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((e[u] >> IDB) * 16u), 0, GAUX);
-                            v[u] = make_uint4(w[0], w[1], w[2], w[3]);
+                            v[u] = prow[e[u] >> IDB];
                         }
                     }
-                if constexpr (GAUX == 1) {
+                if constexpr (DMA) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
                     for (int u = 0; u < kUnroll; ++u) v[u] = s_rows[wid][u][lane];
@@ -276,24 +271,11 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
                         if constexpr (EMB) v[u].w = (v[u].w & (0xFFFFFFFFu >> IDB)) | (e[u] << (32 - IDB));
-                        if constexpr (STORE == 0) {
-                            // non-temporal dword stores: 7.8 vs 10.1 ms for one dwordx4 (tools/partgather.hip)
-                            uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
-                            __builtin_nontemporal_store(v[u].x, o);
-                            __builtin_nontemporal_store(v[u].y, o + 1);
-                            __builtin_nontemporal_store(v[u].z, o + 2);
-                            __builtin_nontemporal_store(v[u].w, o + 3);
-                        } else if constexpr (STORE == 2) {
-                            u32x4 w4 = {v[u].x, v[u].y, v[u].z, v[u].w};
-                            __builtin_nontemporal_store(w4, reinterpret_cast<u32x4*>(out + pos[u]));
-                        } else if constexpr (STORE == 3) {  // this group's output region through one rsrc
-                            const auto rs = __builtin_amdgcn_make_buffer_rsrc(out + b0 * cap, (short)0, 0x7FFFFFFF,
-                                                                              0x00020000);
-                            u32x4 w4 = {v[u].x, v[u].y, v[u].z, v[u].w};
-                            __builtin_amdgcn_raw_buffer_store_b128(w4, rs, (int)((pos[u] - b0 * cap) * 16u), 0, SAUX);
-                        } else {
-                            out[pos[u]] = v[u];
-                        }
+                        uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
+                        __builtin_nontemporal_store(v[u].x, o);
+                        __builtin_nontemporal_store(v[u].y, o + 1);
+                        __builtin_nontemporal_store(v[u].z, o + 2);
+                        __builtin_nontemporal_store(v[u].w, o + 3);
                     }
             }
         }
@@ -517,7 +499,7 @@ static int cobs_lookup_grid(int per_cu_want) {
     static std::atomic<int> cache{0};
     const int per_cu_res = cached_grid(cache, [] {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, 0, true, 1024>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, true, 1024, false>, 256, 0) !=
                 hipSuccess || per_cu < 1)
             per_cu = 1;
         return per_cu;
@@ -529,7 +511,7 @@ static int cobs_lookup_grid(int per_cu_want) {
     return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
 }
 
-template <int U, int ST, int CK, int GA = 0, int SA = 0>
+template <int U, int CK, bool DMA>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
                           uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
@@ -537,10 +519,10 @@ static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t
     const uint64_t waves = (uint64_t)grid / 8 * 4;
     const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
     if (emb)
-        cobs_lookup_kernel<U, ST, true, CK, GA, SA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+        cobs_lookup_kernel<U, true, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
                                                                  ent, tbl, rowv, qctr, b0, b1, gb);
     else
-        cobs_lookup_kernel<U, ST, false, CK, GA, SA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+        cobs_lookup_kernel<U, false, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
                                                                   ent, tbl, rowv, qctr, b0, b1, gb);
 }
 
@@ -577,8 +559,8 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
         if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
         switch (var) {
-            case 1: lookup_launch<8, 0, CK, 0>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            default: lookup_launch<6, 0, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 1: lookup_launch<8, CK, false>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            default: lookup_launch<6, CK, true>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
