@@ -122,6 +122,32 @@ def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mo
         loaded.predict([Record("short", "ACGT")])
 
 
+def test_species_model_same_on_both_probe_paths(tmp_path, species_dir, genomes, monkeypatch):
+    """predict(), predict_columnar() and the saved JSON are byte-identical whether
+    the species bank is probed directly (XSPECT2_AMD_COBS_PART=0) or through
+    the partitioned pipeline (=3, forced on this small bank)."""
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+
+    model = ProbabilisticFilterModel(K, "Test Filter", "John Doe", "j@x", "Species", tmp_path / "data")
+    model.fit(species_dir)
+    rng = np.random.default_rng(3)
+    src = [g.tobytes().decode() for g in genomes]
+    recs = [Record(f"read_{i}", src[i % 4][s:s + int(rng.integers(30, 400))])
+            for i, s in enumerate(rng.integers(0, 29_000, 3000))]
+    fa = tmp_path / "reads.fasta"
+    write_fasta(recs, fa)
+    outs = {}
+    for mode in ("0", "3"):
+        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+        res = model.predict(recs, step=2)
+        col = model.predict_columnar(fa)
+        path = tmp_path / f"out_{mode}.json"
+        col.save(path)
+        outs[mode] = (res.hits, res.num_kmers, res.get_scores()["total"], path.read_bytes())
+        assert model.index.probe_path() == int(mode == "3")
+    assert outs["0"] == outs["3"]
+
+
 def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
     from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
 
