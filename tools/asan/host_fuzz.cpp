@@ -1,0 +1,159 @@
+// Host-side sanitizer run (AddressSanitizer + UndefinedBehaviorSanitizer, host
+// code only) of the FASTA/FASTQ reader and the JSON/FASTA writers of
+// libxspect_hip.so: randomised well-formed and malformed inputs, every batch
+// size from one byte up, 1..8 parser threads.  Functional equality with
+// Biopython / json.dumps is tested in tests/test_fastx.py and
+// tests/test_json_writer.py; this driver looks for memory errors only.
+//   make -C tools/asan run
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/xspect_hip.h"
+
+namespace xs {
+int set_error(int code, const char* msg) {  // the library's version lives in xs_api.cpp (GPU side)
+    (void)msg;
+    return code;
+}
+}  // namespace xs
+
+static std::mt19937_64 rng(12345);
+
+static std::string rand_seq(size_t n, const char* alpha) {
+    std::string s;
+    const size_t m = strlen(alpha);
+    for (size_t i = 0; i < n; ++i) s += alpha[rng() % m];
+    return s;
+}
+
+static std::string make_fasta(int recs, bool crlf, bool trailing_nl) {
+    std::string out, nl = crlf ? "\r\n" : "\n";
+    for (int r = 0; r < recs; ++r) {
+        out += ">r" + std::to_string(r) + (rng() % 2 ? " desc words\t x" : "") + nl;
+        const size_t len = rng() % 400;
+        const std::string s = rand_seq(len, "ACGTNacgtRY");
+        const size_t w = 1 + rng() % 90;
+        for (size_t i = 0; i < s.size(); i += w) out += s.substr(i, w) + nl;
+        if (rng() % 7 == 0) out += nl;  // blank line
+    }
+    if (!trailing_nl && !out.empty()) out.resize(out.size() - nl.size());
+    return out;
+}
+
+static std::string make_fastq(int recs, bool wrapped, bool trailing_nl, bool malformed) {
+    std::string out;
+    for (int r = 0; r < recs; ++r) {
+        const size_t len = rng() % 300;
+        const std::string s = rand_seq(len, "ACGTN");
+        std::string q = rand_seq(len, "@+IJ#!");  // '@' and '+' in qualities
+        if (malformed && r == recs / 2) q.resize(q.size() / 2);
+        out += "@r" + std::to_string(r) + " x\n";
+        if (wrapped && len > 10) out += s.substr(0, len / 2) + "\n" + s.substr(len / 2) + "\n";
+        else out += s + "\n";
+        out += "+\n";
+        if (wrapped && q.size() > 10) out += q.substr(0, q.size() / 2) + "\n" + q.substr(q.size() / 2) + "\n";
+        else out += q + "\n";
+    }
+    if (!trailing_nl && !out.empty()) out.pop_back();
+    return out;
+}
+
+static int read_all(const std::string& path, int fmt, int threads, uint64_t batch, uint64_t* recs) {
+    xs_fastx* r = nullptr;
+    int rc = xs_fastx_open(path.c_str(), fmt, threads, 0, &r);
+    if (rc) return rc;
+    *recs = 0;
+    xs_fastx_batch b;
+    for (;;) {
+        rc = xs_fastx_next(r, batch, &b);
+        if (rc || b.n == 0) break;
+        *recs += b.n;
+        // touch everything the batch hands out
+        volatile uint64_t sink = 0;
+        for (uint64_t i = 0; i < b.n; ++i) {
+            for (uint64_t o = b.offsets[i]; o < b.offsets[i + 1]; ++o) sink += (uint8_t)b.seqs[o];
+            for (uint64_t o = b.id_offsets[i]; o < b.id_offsets[i + 1]; ++o) sink += (uint8_t)b.ids[o];
+            for (uint64_t o = b.desc_offsets[i]; o < b.desc_offsets[i + 1]; ++o) sink += (uint8_t)b.descs[o];
+        }
+        std::vector<uint32_t> idx;
+        for (uint64_t i = 0; i < b.n; i += 2) idx.push_back((uint32_t)i);
+        if (xs_write_fasta("/tmp/xs_asan_out.fasta", 0, b.seqs, b.offsets, b.descs, b.desc_offsets, idx.data(),
+                           idx.size(), 60))
+            return -99;
+    }
+    xs_fastx_close(r);
+    return rc;
+}
+
+static void write_file(const std::string& path, const std::string& text) {
+    FILE* f = fopen(path.c_str(), "wb");
+    fwrite(text.data(), 1, text.size(), f);
+    fclose(f);
+}
+
+int main() {
+    const std::string path = "/tmp/xs_asan_in.txt";
+    int files = 0, errors = 0, unexpected = 0;
+    auto sweep = [&](const std::string& text, int fmt, bool must_parse) {
+        write_file(path, text);
+        ++files;
+        for (uint64_t batch : {1ull, 7ull, 64ull, 1000ull, 1ull << 20})
+            for (int threads : {1, 3, 8}) {
+                uint64_t n = 0;
+                const int rc = read_all(path, fmt, threads, batch, &n);
+                if (rc) ++errors;  // malformed inputs must fail with an error code, not a crash
+                if (rc && must_parse) ++unexpected;
+            }
+    };
+    for (int trial = 0; trial < 60; ++trial) {
+        const bool fq = trial % 2;
+        const int recs = (int)(rng() % 40);
+        const bool bad = fq && trial % 11 == 0;
+        const std::string text = fq ? make_fastq(recs, trial % 3 == 0, trial % 5 != 0, bad)
+                                    : make_fasta(recs, trial % 3 == 0, trial % 5 != 0);
+        sweep(text, fq ? XS_FASTX_FASTQ : XS_FASTX_FASTA, !bad);
+        // the same file cut at a random byte, and with random bytes spliced in
+        if (!text.empty()) {
+            sweep(text.substr(0, rng() % text.size()), fq ? XS_FASTX_FASTQ : XS_FASTX_FASTA, !fq);
+            std::string g = text;
+            for (int i = 0; i < 8; ++i) g[rng() % g.size()] = (char)(rng() % 256);
+            sweep(g, fq ? XS_FASTX_FASTQ : XS_FASTX_FASTA, false);
+        }
+    }
+    for (const char* t : {"", ">", "@", ">\n", "@\n", "@r\n", "@r\nACGT\n+", "@r\nACGT\n+\nII", "\n\n\n", ">a\r\n\r\n",
+                          "ACGT\n>x\nAC"})
+        for (int fmt : {XS_FASTX_FASTA, XS_FASTX_FASTQ}) sweep(t, fmt, false);
+    // JSON result sections: random hit matrices, masks, long ids
+    for (int trial = 0; trial < 20; ++trial) {
+        const uint64_t n = 1 + rng() % 300, D = 1 + rng() % 40;
+        std::vector<uint32_t> hits(n * D);
+        std::vector<uint64_t> nk(n);
+        for (auto& h : hits) h = rng() % 200;
+        for (auto& k : nk) k = 1 + rng() % 200;
+        std::string ids, labels;
+        std::vector<uint64_t> io{0}, lo{0};
+        for (uint64_t i = 0; i < n; ++i) {
+            ids += "\"read_" + std::to_string(i) + std::string(rng() % 30, 'x') + "\"";
+            io.push_back(ids.size());
+        }
+        for (uint64_t d = 0; d < D; ++d) {
+            labels += "\"" + std::to_string(470 + d) + "\"";
+            lo.push_back(labels.size());
+        }
+        std::vector<uint8_t> mask(D);
+        for (auto& m : mask) m = rng() % 3 != 0;
+        FILE* f = fopen("/tmp/xs_asan_out.json", "wb");
+        fclose(f);
+        if (xs_write_result_sections("/tmp/xs_asan_out.json", n, D, hits.data(), nk.data(), ids.c_str(), io.data(),
+                                     labels.c_str(), lo.data(), trial % 2 ? mask.data() : nullptr, 1 + trial % 8))
+            ++errors;
+    }
+    printf("host sanitizer run: %d input files x 15 reader configurations, 20 JSON matrices; "
+           "%d clean error returns, %d on well-formed input\n", files, errors, unexpected);
+    return unexpected ? 1 : 0;
+}
