@@ -81,21 +81,39 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
 
 @pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
                                                                                   (64, 31, 8, [300_007])])
-@pytest.mark.parametrize("ck,ws_mb,lookup", [("1024", None, None), ("2048", None, None), ("4096", None, None),
-                                             ("2048", "1", None), ("1024", "2", None), ("2048", None, "1")])
-def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup):
+@pytest.mark.parametrize("ck,ws_mb,lookup,pad", [("1024", None, None, None), ("2048", None, None, None),
+                                                 ("4096", None, None, None), ("2048", "1", None, None),
+                                                 ("1024", "2", None, None), ("2048", None, "1", None),
+                                                 ("2048", None, None, "1"), ("4096", "2", "1", "1")])
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup,
+                                                  pad):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
     L2-resident lookup, per-block AND + count) with partitions down to 1024
     rows, every bucket block size, and workspaces of 1-2 MiB (the bucket
-    blocks then run in ranges of a few blocks that reuse it), on the classic
-    cases of <= 128 docs: same hits, counts and totals."""
+    blocks then run in ranges of a few blocks that reuse it), partition runs
+    padded to 4 entries (default) and unpadded, on the classic cases of <= 128
+    docs: same hits, counts and totals."""
     monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
     monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
     if lookup:  # the register-gather lookup instead of LDS-DMA
         monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
+    if pad:  # runs not padded to 64-B row pieces
+        monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
+
+
+@pytest.mark.parametrize("shift,D", [("10", 100), ("11", 100), ("10", 117), ("11", 128), ("12", 64)])
+def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, shift, D):
+    """A 1 M-row bank cut into 1024-row partitions (977 of them: more than
+    kCobsPadParts = 512, so the runs are not padded) and 2048-/4096-row
+    partitions (489 / 245: padded with all-ones pad rows), with the k-mer id
+    in the row's top bits (D <= 117) and in the entries (D = 128): same hits,
+    counts and totals as the oracle."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
+    monkeypatch.setenv("XSPECT2_AMD_CP_SHIFT", shift)
+    _classic_case(xs, oracle_mod, D, 21, 7, [1_000_003], want_path=1)
 
 
 def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):

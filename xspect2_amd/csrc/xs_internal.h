@@ -125,8 +125,14 @@ struct CobsPartPlan {
     uint64_t nblk;       // bucket blocks (>= the call's k-mers / ck)
     uint64_t rblk;       // bucket blocks per range (one workspace, reused range after range)
     uint64_t kbound;     // upper bound of the call's sampled k-mers
+    uint32_t pad;        // each partition's run of a block padded to a multiple of pad entries (1 or 4)
+    uint64_t stride;     // entries per bucket block region (ck * h, plus the padding, multiple of 8)
     size_t entry_bytes, tbl_bytes, nkc_bytes, scan_bytes, aux_bytes;
 };
+// Runs are padded (64-B aligned rows) only while P <= kCobsPadParts: the pad
+// slots live in the bucket block's LDS.
+constexpr uint32_t kCobsPadParts = 512;
+constexpr uint32_t kCobsPadEntry = 0xFFFFFFFFu;  // pad slot: the lookup writes an all-ones row
 struct PartWs {
     uint64_t* nkc;       // n+1 per-read k-mer counts
     uint64_t* kofs;      // n+1 exclusive scan: first k-mer id of each read

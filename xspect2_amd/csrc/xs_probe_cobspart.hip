@@ -54,21 +54,23 @@ struct PartBank {
 };
 
 template <int KT, int HT, int CK>
-__global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadView rv, PartBank pb, uint32_t h,
+__global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs_bucket_kernel(ReadView rv, PartBank pb, uint32_t h,
                                                                      const uint64_t* __restrict__ kofs,
                                                                      uint32_t shift, uint32_t P,
                                                                      uint32_t* __restrict__ ent,
                                                                      uint16_t* __restrict__ tbm,
                                                                      const uint32_t* __restrict__ blk_read,
-                                                                     uint64_t b_begin) {
-    // entries and partition starts of block B go to row B - b_begin of the range's workspace
+                                                                     uint64_t b_begin, uint64_t stride, uint32_t pad) {
+    // entries and partition starts of block B go to row B - b_begin of the range's workspace;
+    // with pad = 4 each partition's run is padded with kCobsPadEntry slots to a multiple
+    // of 4 entries, so that the lookup's row runs are whole 64-B pieces (P <= kCobsPadParts)
     constexpr int BT = bucket_threads<CK>();
     constexpr int IDB = id_bits<CK>();
     using Scan = hipcub::BlockScan<uint32_t, BT>;
     constexpr int ITEMS = kPartMax / BT;
     constexpr int PER = CK / BT;  // k-mers per thread
     constexpr int NH = HT ? HT : kMaxH;
-    __shared__ uint32_t s_ent[CK * NH];  // partition-ordered entries
+    __shared__ uint32_t s_ent[CK * NH + 3 * kCobsPadParts];  // partition-ordered entries (+ pad slots)
     __shared__ uint32_t cur[kPartMax];
     __shared__ typename Scan::TempStorage scan_tmp;
     __shared__ uint64_t s_kofs[kStageReads], s_offs[kStageReads];
@@ -135,10 +137,15 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
         }
     }
     __syncthreads();
-    uint32_t v[ITEMS];
+    uint32_t v[ITEMS], c0[ITEMS], c1[ITEMS];
 #pragma unroll
-    for (int q = 0; q < ITEMS; ++q) v[q] = cur[tid * ITEMS + q];
-    Scan(scan_tmp).ExclusiveSum(v, v);
+    for (int q = 0; q < ITEMS; ++q) {
+        c0[q] = cur[tid * ITEMS + q];
+        c1[q] = (c0[q] + pad - 1) & ~(pad - 1);
+        v[q] = c1[q];
+    }
+    uint32_t tot;  // entries of the block, pad slots included
+    Scan(scan_tmp).ExclusiveSum(v, v, tot);
     __syncthreads();  // every counter read before it becomes a cursor
 #pragma unroll
     for (int q = 0; q < ITEMS; ++q) {
@@ -146,9 +153,10 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
         if (p < P) {
             cur[p] = v[q];
             tbm[(B - b_begin) * (P + 1) + p] = (uint16_t)v[q];
+            for (uint32_t x = c0[q]; x < c1[q]; ++x) s_ent[v[q] + x] = kCobsPadEntry;
         }
     }
-    if (tid == 0) tbm[(B - b_begin) * (P + 1) + P] = (uint16_t)(m * H);
+    if (tid == 0) tbm[(B - b_begin) * (P + 1) + P] = (uint16_t)tot;
     __syncthreads();
     const uint32_t omask = (1u << shift) - 1;
 #pragma unroll
@@ -165,9 +173,8 @@ __global__ void __launch_bounds__(bucket_threads<CK>()) cobs_bucket_kernel(ReadV
         }
     }
     __syncthreads();
-    // coalesced copy-out (regions of CK*H entries: 16-B aligned)
-    const uint64_t base = (B - b_begin) * CK * H;  // the range reuses one workspace
-    const uint32_t tot = m * H;
+    // coalesced copy-out (regions of stride entries: 16-B aligned)
+    const uint64_t base = (B - b_begin) * stride;  // the range reuses one workspace
     for (uint32_t e = tid * 4; e < tot; e += BT * 4) {
         if (e + 4 <= tot) {
             *reinterpret_cast<uint4*>(ent + base + e) = *reinterpret_cast<const uint4*>(s_ent + e);
@@ -190,23 +197,23 @@ constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
 // registers.  Rows go back with non-temporal dword stores (7.8 vs 10.1 ms for
 // one plain dwordx4 in tools/partgather.hip; the other store and load cache
 // policies measured no better: profiles/r02_cobspart_ab.txt item 9).
-template <int kUnroll, bool EMB, int CK, bool DMA>
+template <int kUnroll, bool EMB, int CK, int DMA>
 __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
                                                           uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
                                                           const uint16_t* __restrict__ tbl,
                                                           uint4* __restrict__ out, uint32_t* qctr,
-                                                          uint64_t b_begin, uint64_t b_end, uint32_t gb) {
+                                                          uint64_t b_begin, uint64_t b_end, uint32_t gb,
+                                                          uint64_t stride) {
     constexpr int IDB = id_bits<CK>();
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    __shared__ uint4 s_rows[DMA ? 4 : 1][DMA ? kUnroll : 1][64];  // LDS-DMA landing slots
+    __shared__ uint4 s_rows[DMA > 0 ? 4 : 1][DMA > 0 ? kUnroll : 1][64];  // LDS-DMA landing slots
     (void)wid;
     // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
     // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
     const uint64_t last = min(b_end, (kofs[n] + CK - 1) / CK);
     const uint64_t nblk = last > b_begin ? last - b_begin : 0;
-    const uint64_t cap = (uint64_t)CK * H;
     const uint32_t xcd = blockIdx.x & 7;
     for (uint64_t p = xcd; p < P; p += 8) {
         const uint4* prow = pb.rows + (p << shift);
@@ -246,27 +253,36 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                     }
                     const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
                     const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
-                    pos[u] = (b0 + j) * cap + sj + (i - pj);
+                    pos[u] = (b0 + j) * stride + sj + (i - pj);
                 }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     e[u] = i0 + u * 64 + lane < total ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    if (i0 + u * 64 + lane < total) {
-                        if constexpr (DMA) {  // the row lands in this wave's slot u
+                    if (i0 + u * 64 + lane < total && e[u] != kCobsPadEntry) {
+                        if constexpr (DMA > 0) {  // the row lands in this wave's slot u
 #if defined(__HIP_DEVICE_COMPILE__)  // a device-only builtin: the host pass must not see it
+                            // DMA 1: one row gather in flight per wave (each waits for the one before);
+                            // 3, 4: two, three in flight; 2: all kUnroll
+                            if constexpr (DMA == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            if constexpr (DMA == 3) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+                            if constexpr (DMA == 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
                             __builtin_amdgcn_global_load_lds(prow + (e[u] >> IDB), &s_rows[wid][u][0], 16, 0, 0);
 #endif
                         } else {
                             v[u] = prow[e[u] >> IDB];
                         }
                     }
-                if constexpr (DMA) {
+                if constexpr (DMA > 0) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
                     for (int u = 0; u < kUnroll; ++u) v[u] = s_rows[wid][u][lane];
                 }
+                // a pad slot's row is all ones: ANDed into k-mer CK-1 (its id bits), it changes nothing
+#pragma unroll
+                for (int u = 0; u < kUnroll; ++u)
+                    if (e[u] == kCobsPadEntry) v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
@@ -302,7 +318,8 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
                                                                        const uint32_t* __restrict__ blk_read,
                                                                        uint32_t* __restrict__ hits,
                                                                        uint64_t* __restrict__ partials, int pblocks,
-                                                                       uint64_t b_begin) {
+                                                                       uint64_t b_begin, uint64_t stride,
+                                                                       const uint16_t* __restrict__ tbm, uint32_t P1) {
     __shared__ uint32_t acc[4][CK];
     constexpr int kResolveThreads = resolve_threads<CK>();
     constexpr uint32_t kCntReads = cnt_reads<CK>();
@@ -331,8 +348,9 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
         for (uint32_t x = tid; x <= nr; x += kResolveThreads) s_kofs[x] = kofs[lo + x];
     }
     __syncthreads();
-    const uint64_t base = (B - b_begin) * CK * H;
-    const uint32_t tot = m * H;
+    const uint64_t base = (B - b_begin) * stride;
+    const uint32_t tot = tbm[(B - b_begin) * P1 + P1 - 1];  // m * H, plus the pad slots (all-ones rows)
+    (void)H;
     // kResolveUnroll rows in flight per lane, then their LDS ANDs
     for (uint32_t e0 = tid; e0 < tot; e0 += kResolveThreads * kResolveUnroll) {
         uint4 v[kResolveUnroll];
@@ -476,7 +494,11 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     // The bucket blocks run in ranges that reuse one workspace of at most
     // XSPECT2_AMD_CP_WS_MB MiB of entries + rows (default kCobsPartWsMiB), so
     // any batch size fits.
-    const uint64_t per_block = (uint64_t)ck * bv.h * (sizeof(uint32_t) + sizeof(uint4));
+    // runs padded to 4 entries (64-B row pieces: 4.37 -> 3.51 ms for the lookup's
+    // write stream alone, tools/runwrite.hip); XSPECT2_AMD_CP_PAD=1 turns it off
+    const uint32_t pad = (P <= kCobsPadParts && env_int("XSPECT2_AMD_CP_PAD", 4) != 1) ? 4 : 1;
+    const uint64_t stride = ((uint64_t)ck * bv.h + (pad - 1) * P + 7) / 8 * 8;
+    const uint64_t per_block = stride * (sizeof(uint32_t) + sizeof(uint4));
     const uint64_t cap = (uint64_t)std::max(1, env_int("XSPECT2_AMD_CP_WS_MB", (int)kCobsPartWsMiB)) << 20;
     const uint64_t rblk = std::max<uint64_t>(1, std::min<uint64_t>(nblk, cap / per_block));
     plan->ck = ck;
@@ -485,7 +507,9 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     plan->nblk = nblk;
     plan->rblk = rblk;
     plan->kbound = kbound;
-    plan->entry_bytes = rblk * per_block;                            // a range's entries, then their rows
+    plan->pad = pad;
+    plan->stride = stride;
+    plan->entry_bytes = rblk * per_block + 128;                      // a range's entries, then their rows (128-B aligned)
     plan->tbl_bytes = 2 * (P + 1) * rblk * sizeof(uint16_t);         // partition- + block-major
     plan->aux_bytes = (nblk + 1 + kQStride) * sizeof(uint32_t) + (size_t)P * kQStride * sizeof(uint32_t);
     plan->nkc_bytes = (n + 1) * sizeof(uint64_t);
@@ -499,7 +523,7 @@ static int cobs_lookup_grid(int per_cu_want) {
     static std::atomic<int> cache{0};
     const int per_cu_res = cached_grid(cache, [] {
         int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, true, 1024, false>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, true, 1024, 0>, 256, 0) !=
                 hipSuccess || per_cu < 1)
             per_cu = 1;
         return per_cu;
@@ -511,7 +535,7 @@ static int cobs_lookup_grid(int per_cu_want) {
     return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
 }
 
-template <int U, int CK, bool DMA>
+template <int U, int CK, int DMA>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
                           uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
@@ -520,10 +544,10 @@ static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t
     const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
     if (emb)
         cobs_lookup_kernel<U, true, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                 ent, tbl, rowv, qctr, b0, b1, gb);
+                                                                 ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
     else
         cobs_lookup_kernel<U, false, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                  ent, tbl, rowv, qctr, b0, b1, gb);
+                                                                  ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
 }
 
 // Ranges of plan.rblk bucket blocks, one after the other on stream s, each
@@ -533,16 +557,17 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
                                      const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
                                      hipStream_t s) {
     hipError_t e;
-    const uint64_t ne = plan.rblk * CK * H;
+    const uint64_t ne = plan.rblk * plan.stride;
     uint32_t* ent = reinterpret_cast<uint32_t*>(ws.entries);
-    uint4* rowv = reinterpret_cast<uint4*>(ent + (ne + 3) / 4 * 4);
+    uint4* rowv = reinterpret_cast<uint4*>(ent + (ne + 31) / 32 * 32);
     uint32_t* blk_read = ws.aux;
     uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.rblk;  // block-major copy
     uint32_t* qctr = ws.aux + (plan.nblk + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
     const bool emb = pb.D <= emb_max_docs<CK>();
-    // lookup: 0 (default) LDS-DMA row gathers, 6 in flight per lane, 2 workgroups
-    // per CU; 1 register gathers, 8 in flight, 3 per CU (the first build).
+    // lookup: 0 (default) LDS-DMA row gathers of 6 entries per lane, one gather in
+    // flight per wave at a time, 2 workgroups per CU; 1 register gathers, 8 in
+    // flight, 3 per CU (the first build); 2 LDS-DMA with all 6 in flight.
     // XSPECT2_AMD_CP_PERCU overrides the workgroups per CU.
     const int var = env_int("XSPECT2_AMD_CP_LOOKUP", 0);
     const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", var == 1 ? 3 : 2));
@@ -551,23 +576,30 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
         const unsigned nb = (unsigned)(b1 - b0);
         if (rv.k == 21 && H == 7)
             cobs_bucket_kernel<21, 7, CK><<<nb, bucket_threads<CK>(), 0, s>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
-                                                                            ent, tbm, blk_read, b0);
+                                                                            ent, tbm, blk_read, b0, plan.stride,
+                                                                            plan.pad);
         else
             cobs_bucket_kernel<0, 0, CK><<<nb, bucket_threads<CK>(), 0, s>>>(rv, pb, H, ws.kofs, plan.shift, plan.P,
-                                                                           ent, tbm, blk_read, b0);
+                                                                           ent, tbm, blk_read, b0, plan.stride,
+                                                                           plan.pad);
         part_transpose_kernel<<<dim3((nb + 63) / 64, (plan.P + 1 + 63) / 64), 256, 0, s>>>(
             tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
         if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
         switch (var) {
-            case 1: lookup_launch<8, CK, false>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            default: lookup_launch<6, CK, true>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 1: lookup_launch<8, CK, 0>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 2: lookup_launch<6, CK, 2>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 3: lookup_launch<6, CK, 3>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 4: lookup_launch<6, CK, 4>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            default: lookup_launch<6, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
-                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0);
+                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0, plan.stride, tbm,
+                plan.P + 1);
         else
             cobs_resolve_kernel<false, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
-                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0);
+                rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0, plan.stride, tbm,
+                plan.P + 1);
     }
     return hipGetLastError();
 }
