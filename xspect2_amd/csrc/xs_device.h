@@ -31,7 +31,19 @@ constexpr uint32_t kS32_0 = 0x396cfeb8u, kS32_1 = 0xbe4ba423u;
 constexpr uint64_t kLcgMh = 0x2360ED051FC65DA4ull, kLcgMl = 0x4385DF649FCCF645ull;
 constexpr uint64_t kLcgCh = 0x5851F42D4C957F2Dull, kLcgCl = 0x14057B7EF767814Full;
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// 64-bit rotate as two v_alignbit_b32 (the shift/or form compiles to three
+// instructions, one of them a 64-bit shift); r is a constant at every call.
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (r & 32) {
+        const uint32_t t = lo;
+        lo = hi;
+        hi = t;
+    }
+    if ((r & 31) == 0) return ((uint64_t)hi << 32) | lo;
+    const uint32_t s = 32 - (r & 31);
+    return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, s) << 32) | __builtin_amdgcn_alignbit(lo, hi, s);
+}
 
 __device__ __forceinline__ uint64_t xxh64_round0(uint64_t in) {
     return rotl64(in * P64_2, 31) * P64_1;

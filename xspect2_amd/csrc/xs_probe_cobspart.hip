@@ -88,12 +88,34 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
     const uint64_t hi = g0 + CK < Nk ? blk_read[B + 1] : rv.n - 1;
     const uint64_t nr = hi - lo + 2;
     const bool staged = nr <= kStageReads;
-    if (staged)
+    // k-mer -> read (staged case): s_map[i] = the block-local read of k-mer g0 + i, from
+    // each read's first k-mer marked and a block-wide max-scan (s_ent is free until the
+    // entries are placed)
+    uint32_t* s_map = s_ent;
+    if (staged) {
         for (uint32_t x = tid; x < nr; x += BT) {
             s_kofs[x] = kofs[lo + x];
             s_offs[x] = rv.offs[lo + x];
         }
+        for (uint32_t i = tid; i < CK; i += BT) s_map[i] = 0;  // read 0 holds k-mer g0
+    }
     __syncthreads();
+    if (staged) {
+        // reads 1 .. nr-2 start inside the block or after it; empty reads share a start
+        // with the next read, and the max keeps the later one
+        for (uint32_t x = 1 + tid; x + 1 < nr; x += BT) {
+            const uint64_t st = s_kofs[x] - g0;
+            if (st < (uint64_t)CK) atomicMax(&s_map[st], x);
+        }
+        __syncthreads();
+        uint32_t mv[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) mv[q] = s_map[tid * PER + q];
+        Scan(scan_tmp).InclusiveScan(mv, mv, hipcub::Max());
+#pragma unroll
+        for (int q = 0; q < PER; ++q) s_map[tid * PER + q] = mv[q];
+        __syncthreads();
+    }
     Kmer c[PER];
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
@@ -102,12 +124,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
             const uint64_t g = g0 + i;
             uint64_t kr, o0, o1;
             if (staged) {
-                uint32_t a = 0, b = (uint32_t)(nr - 2);  // largest x with s_kofs[x] <= g
-                while (a < b) {
-                    const uint32_t mid = (a + b + 1) >> 1;
-                    if (s_kofs[mid] <= g) a = mid;
-                    else b = mid - 1;
-                }
+                const uint32_t a = s_map[i];  // largest x with s_kofs[x] <= g
                 kr = s_kofs[a];
                 o0 = s_offs[a];
                 o1 = s_offs[a + 1];
@@ -120,7 +137,8 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
             kmer_at<KT, kKmerCobs>(rv, o0, o1 - o0, (g - kr) * rv.step, k, c[q]);
         }
     }
-    uint32_t row[PER][NH];  // the h rows of this thread's k-mers stay in registers
+    uint32_t row[PER][NH];  // the h rows of this thread's k-mers stay in registers,
+    uint32_t rk[PER][NH];   // with each row's rank in its partition (one LDS atomic per row)
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid + q * BT;
@@ -131,7 +149,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
             for (int j = 0; j < NH; ++j) {
                 if ((uint32_t)j < H) {
                     row[q][j] = fastmod_small(xxh64_seed<KT>(c[q], pre, k, (uint64_t)j), (uint32_t)pb.sig, pb.magic);
-                    atomicAdd(&cur[row[q][j] >> shift], 1u);
+                    rk[q][j] = atomicAdd(&cur[row[q][j] >> shift], 1u);
                 }
             }
         }
@@ -166,8 +184,7 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
 #pragma unroll
             for (int j = 0; j < NH; ++j) {
                 if ((uint32_t)j < H) {
-                    const uint32_t pos = atomicAdd(&cur[row[q][j] >> shift], 1u);
-                    s_ent[pos] = ((row[q][j] & omask) << IDB) | i;
+                    s_ent[cur[row[q][j] >> shift] + rk[q][j]] = ((row[q][j] & omask) << IDB) | i;
                 }
             }
         }
@@ -279,10 +296,15 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
 #pragma unroll
                     for (int u = 0; u < kUnroll; ++u) v[u] = s_rows[wid][u][lane];
                 }
-                // a pad slot's row is all ones: ANDed into k-mer CK-1 (its id bits), it changes nothing
+                // a pad slot's row is all ones, so ANDing it into any k-mer changes nothing; its id
+                // bits name the k-mer of its slot's position, spreading the pad rows' LDS ANDs in
+                // the resolve pass over the block instead of one address
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    if (e[u] == kCobsPadEntry) v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                    if (e[u] == kCobsPadEntry) {
+                        v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                        e[u] = (uint32_t)pos[u] & (CK - 1);
+                    }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
                     if (i0 + u * 64 + lane < total) {
@@ -360,7 +382,10 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
             const uint32_t e = e0 + u * kResolveThreads;
             if (e < tot) {
                 v[u] = load_nt(rowv + base + e);
-                if (!EMB) id[u] = __builtin_nontemporal_load(ent + base + e) & (CK - 1);
+                if (!EMB) {  // a pad slot's (all-ones) row goes to the k-mer of its position
+                    const uint32_t ev = __builtin_nontemporal_load(ent + base + e);
+                    id[u] = (ev == kCobsPadEntry ? e : ev) & (CK - 1);
+                }
             }
         }
 #pragma unroll
