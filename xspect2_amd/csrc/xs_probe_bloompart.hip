@@ -69,12 +69,31 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
     const uint64_t hi = g0 + kTK < Nk ? blk_read[blockIdx.x + 1] : rv.n - 1;
     const uint64_t nr = hi - lo + 2;  // kofs/offs entries lo .. hi+1
     const bool staged = nr <= kStageReads;
-    if (staged)
+    // k-mer -> read (staged case) by a block-wide max-scan of the reads' first k-mers, as in
+    // the COBS bucket pass (xs_probe_cobspart.hip); s_off is free until the entries are placed
+    uint32_t* s_map = s_off;
+    if (staged) {
         for (uint32_t x = tid; x < nr; x += kBucketThreads) {
             s_kofs[x] = kofs[lo + x];
             s_offs[x] = rv.offs[lo + x];
         }
+        for (uint32_t i = tid; i < kTK; i += kBucketThreads) s_map[i] = 0;  // read 0 holds k-mer g0
+    }
     __syncthreads();
+    if (staged) {
+        for (uint32_t x = 1 + tid; x + 1 < nr; x += kBucketThreads) {
+            const uint64_t st = s_kofs[x] - g0;
+            if (st < (uint64_t)kTK) atomicMax(&s_map[st], x);
+        }
+        __syncthreads();
+        uint32_t mv[PER];
+#pragma unroll
+        for (int q = 0; q < PER; ++q) mv[q] = s_map[tid * PER + q];
+        Scan(scan_tmp).InclusiveScan(mv, mv, hipcub::Max());
+#pragma unroll
+        for (int q = 0; q < PER; ++q) s_map[tid * PER + q] = mv[q];
+        __syncthreads();
+    }
     const uint64_t omask = (1ull << shift) - 1;
     Kmer c[PER];
 #pragma unroll
@@ -84,12 +103,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
             const uint64_t g = g0 + i;
             uint64_t r, o0, o1, kr;
             if (staged) {
-                uint32_t a = 0, b = (uint32_t)(nr - 2);  // largest x with s_kofs[x] <= g
-                while (a < b) {
-                    const uint32_t mid = (a + b + 1) >> 1;
-                    if (s_kofs[mid] <= g) a = mid;
-                    else b = mid - 1;
-                }
+                const uint32_t a = s_map[i];  // largest x with s_kofs[x] <= g
                 kr = s_kofs[a];
                 o0 = s_offs[a];
                 o1 = s_offs[a + 1];
@@ -102,7 +116,8 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
             kmer_at<KT, kKmerBio>(rv, o0, o1 - o0, (g - kr) * rv.step, k, c[q]);
         }
     }
-    uint64_t idx[PER][NK];  // the K bit indices of this thread's k-mers stay in registers
+    uint64_t idx[PER][NK];  // the K bit indices of this thread's k-mers stay in registers,
+    uint32_t rk[PER][NK];   // with each one's rank in its partition (one LDS atomic per index)
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid + q * kBucketThreads;
@@ -113,7 +128,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
                 if ((uint32_t)j < K) {
                     lcg_step(sl, sh);
                     idx[q][j] = fastmod(sh, bv.mbits, bv.magic);
-                    atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
+                    rk[q][j] = atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
                 }
             }
         }
@@ -141,7 +156,7 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
 #pragma unroll
             for (int j = 0; j < NK; ++j) {
                 if ((uint32_t)j < K) {
-                    const uint32_t pos = atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
+                    const uint32_t pos = cur[(uint32_t)(idx[q][j] >> shift)] + rk[q][j];
                     s_off[pos] = (uint32_t)(idx[q][j] & omask);
                     s_id[pos] = (uint16_t)i;
                 }
