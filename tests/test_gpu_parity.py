@@ -137,18 +137,37 @@ def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
     gb.close()
 
 
-@pytest.mark.parametrize("case", ["all_short", "one_read", "one_long_read", "empty_only"])
+@pytest.mark.parametrize("case", ["all_short", "one_read", "one_long_read", "empty_only", "tiny_reads",
+                                  "empty_between"])
 def test_partitioned_degenerate_batches(xs, oracle_mod, monkeypatch, case):
     """Forced partitioned COBS probe on batches with no k-mers at all, a single
-    read, a single read spanning many bucket blocks, and only empty reads:
-    hits, counts and totals equal the oracle's (zeros where no k-mer)."""
+    read, a single read spanning many bucket blocks, only empty reads, reads
+    of 1-3 k-mers (a bucket block spans more reads than it stages in LDS) and
+    reads with runs of empty and short reads between them (reads sharing a
+    first k-mer in the block's k-mer -> read map): hits, counts and totals
+    equal the oracle's (zeros where no k-mer)."""
     monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=12)
     rng = np.random.default_rng(5)
+    genome = b"".join(seqs)
+
+    def cut(n, lo, hi):
+        out = []
+        for _ in range(n):
+            L = int(rng.integers(lo, hi + 1))
+            o = int(rng.integers(0, len(genome) - L))
+            out.append(genome[o:o + L])
+        return out
+
+    mixed = []
+    for r in cut(400, 60, 300):
+        mixed += [b""] * int(rng.integers(0, 4)) + [b"ACGT"[: int(rng.integers(0, 4))]] + [r]
     reads = {"all_short": _reads(rng, 500, 21, min_len=0, max_len=21),
              "one_read": [seqs[0][:150]],
              "one_long_read": [b"".join(seqs[:4])[:20_000]],
-             "empty_only": [b""] * 7}[case]
+             "empty_only": [b""] * 7,
+             "tiny_reads": cut(6000, 21, 23),
+             "empty_between": mixed}[case]
     for step in (1, 2):
         want_h, want_n = ob.query(reads, step=step)
         got_h, got_n = gb.query(reads, step=step)
@@ -446,6 +465,32 @@ def test_bloom_partitioned_many_short_reads(xs, oracle_mod, monkeypatch, step):
         st = int(rng.integers(0, 19_000))
         reads.append(genome[0][st:st + L] if rng.random() < 0.6 else acgt[rng.integers(0, 4, L)].tobytes())
     reads[100:140] = [b""] * 40
+    want_h, want_n = bf.query(reads, step=step)
+    got_h, got_n = gb.query(reads, step=step)
+    assert np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)
+    assert gb.probe_path() == 1
+    gb.close()
+
+
+@pytest.mark.parametrize("step", [1, 3])
+def test_bloom_partitioned_empty_reads_between(xs, oracle_mod, monkeypatch, step):
+    """Reads of 60-300 bytes with runs of empty and sub-k reads between them:
+    the bucket block stages its reads in LDS and several share a first k-mer
+    in its k-mer -> read map (the later, non-empty one holds it)."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
+    rng = np.random.default_rng(77 + step)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genome = acgt[rng.integers(0, 4, 50_000)].tobytes()
+    bf = oracle_mod.BloomFilter(np.zeros(300_007, dtype=np.uint8), 7, 21)
+    bf.build([genome])
+    gb = xs.Bank.create_bloom(21, 300_007, 7)
+    gb.upload(bf.bits)
+    reads = []
+    for _ in range(800):
+        reads += [b""] * int(rng.integers(0, 4)) + [genome[:int(rng.integers(0, 21))]]
+        L = int(rng.integers(60, 301))
+        st = int(rng.integers(0, len(genome) - L))
+        reads.append(genome[st:st + L] if rng.random() < 0.7 else acgt[rng.integers(0, 4, L)].tobytes())
     want_h, want_n = bf.query(reads, step=step)
     got_h, got_n = gb.query(reads, step=step)
     assert np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)

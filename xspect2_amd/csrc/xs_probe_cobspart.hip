@@ -8,16 +8,19 @@
 // probe is (xs_probe_bloompart.hip):
 //
 //   counts  : per read k-mer count, exclusive scan -> global k-mer id g
-//   bucket  : one block per 1024 k-mers: canonical k-mer, the h XXH64 rows
-//             (exactly as the direct probe), each binned by bank partition
-//             (2 MiB of rows) with LDS counters, a block scan and LDS-sorted
-//             placement; one u32 entry per row = (row in partition << 10 |
-//             k-mer in block), copied out partition-ordered per block, plus
+//   bucket  : one block per CK (default 2048) k-mers: canonical k-mer, the h
+//             XXH64 rows (exactly as the direct probe), each binned by bank
+//             partition (2 MiB of rows) with one LDS atomic (its rank), a
+//             block scan and LDS-sorted placement; one u32 entry per row =
+//             (row in partition << 11 | k-mer in block), copied out
+//             partition-ordered per block in runs padded to 4 entries, plus
 //             one u16 start per partition into a partition-major table.
 //   lookup  : the workgroups of one XCD work through one partition at a time
 //             from a per-partition queue, so its 2 MiB of rows stay in that
-//             XCD's 4 MiB L2 while the entries stream past; each entry's
-//             16-B row is written back in entry order (coalesced).
+//             XCD's 4 MiB L2 while the entries stream past; rows are gathered
+//             by LDS-DMA, one gather instruction in flight per wave, and each
+//             entry's 16-B row is written back in entry order (runs start on
+//             64-B boundaries).
 //   resolve : per bucket block: AND the h rows of each of its k-mers in LDS,
 //             then count per (read, doc) with the column-popcount transpose
 //             of the direct probe; reads inside the block are stored, reads
