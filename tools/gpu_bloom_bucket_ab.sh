@@ -1,9 +1,9 @@
-# rbloom bucket pass (k-mer -> read map, one LDS atomic per index) against the previous
+# rbloom bucket pass changes (k-mer -> read map and one LDS atomic per index; then the closed-form LCG) against the previous
 # commit's library (head), genus bench, interleaved, one box; rbloom parity subset first.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-F=gpurun_out/r02bb; mkdir -p $F
+F=gpurun_out/r02bb2; mkdir -p $F
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   -k "bloom or genus or single_filter or rbloom" > $F/tests.log 2>&1 || { tail -40 $F/tests.log; exit 12; }
 tail -2 $F/tests.log

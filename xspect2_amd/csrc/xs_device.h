@@ -93,6 +93,51 @@ __device__ __forceinline__ void lcg_step(uint64_t& sl, uint64_t& sh) {
     sl = nl;
 }
 
+// The LCG's j-th state from a 64-bit start h (high word 0, as every rbloom index
+// sequence starts): state_j = A_j * h + B_j mod 2^128 with A_j = M^j and
+// B_j = C (M^(j-1) + ... + 1), constants folded at compile time.  Only the high
+// word is needed; each j is independent of the others (no chain), and the
+// product has a 64-bit factor: 7 multiplies instead of lcg_step's 10.
+struct LcgJump {
+    uint64_t ah, al, bh, bl;
+};
+constexpr LcgJump lcg_jump(int j) {
+    unsigned __int128 m = ((unsigned __int128)kLcgMh << 64) | kLcgMl;
+    unsigned __int128 c = ((unsigned __int128)kLcgCh << 64) | kLcgCl;
+    unsigned __int128 a = 1, b = 0;
+    for (int i = 0; i < j; ++i) {
+        a = a * m;
+        b = b * m + c;
+    }
+    return LcgJump{(uint64_t)(a >> 64), (uint64_t)a, (uint64_t)(b >> 64), (uint64_t)b};
+}
+template <int J>
+__device__ __forceinline__ uint64_t lcg_high(uint64_t h) {
+    constexpr LcgJump t = lcg_jump(J);
+    constexpr uint64_t a0 = (uint32_t)t.al, a1 = t.al >> 32;
+    const uint64_t h0 = (uint32_t)h, h1 = h >> 32;
+    // al * h, full 128 bits, from four 32 x 32 partial products
+    const uint64_t ll = a0 * h0, lh = a0 * h1, hl = a1 * h0, hh = a1 * h1;
+    const uint64_t mid = (ll >> 32) + (uint32_t)lh + (uint32_t)hl;  // < 3 * 2^32
+    const uint64_t plo = (mid << 32) | (uint32_t)ll;
+    const uint64_t phi = hh + (lh >> 32) + (hl >> 32) + (mid >> 32);
+    const uint64_t lo = plo + t.bl;
+    return phi + t.ah * h + t.bh + (lo < plo);
+}
+// j = 1 .. 8 (a constant once the caller's loop is unrolled)
+__device__ __forceinline__ uint64_t lcg_high_n(uint64_t h, int j) {
+    switch (j) {
+        case 1: return lcg_high<1>(h);
+        case 2: return lcg_high<2>(h);
+        case 3: return lcg_high<3>(h);
+        case 4: return lcg_high<4>(h);
+        case 5: return lcg_high<5>(h);
+        case 6: return lcg_high<6>(h);
+        case 7: return lcg_high<7>(h);
+        default: return lcg_high<8>(h);
+    }
+}
+
 // Canonical k-mer, held as 8 little-endian dwords (bytes >= k are zero) + a
 // zero guard word.
 struct Kmer {

@@ -122,12 +122,12 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
     for (int q = 0; q < PER; ++q) {
         const uint32_t i = tid + q * kBucketThreads;
         if (i < m) {
-            uint64_t sl = xxh3_kmer<KT>(c[q], k), sh = 0;
+            const uint64_t h = xxh3_kmer<KT>(c[q], k);
+            static_assert(NK <= 8, "lcg_high_n covers 8 states");
 #pragma unroll
             for (int j = 0; j < NK; ++j) {
                 if ((uint32_t)j < K) {
-                    lcg_step(sl, sh);
-                    idx[q][j] = fastmod(sh, bv.mbits, bv.magic);
+                    idx[q][j] = fastmod(lcg_high_n(h, j + 1), bv.mbits, bv.magic);
                     rk[q][j] = atomicAdd(&cur[(uint32_t)(idx[q][j] >> shift)], 1u);
                 }
             }
