@@ -53,6 +53,36 @@ __global__ void __launch_bounds__(256) runs(const uint32_t* __restrict__ start, 
     }
 }
 
+// The resolve's side of a partition-major layout: workgroup b reads block b's P runs, each
+// stored at its partition's region (run (b, p) at pstart[p] + prefix over blocks < b).
+__global__ void __launch_bounds__(256) runs_read(const uint32_t* __restrict__ cnt,   // [NB][P] run lengths
+                                                 const uint64_t* __restrict__ at,    // [NB][P] run starts
+                                                 uint32_t NB, uint32_t P, const u32x4* __restrict__ in,
+                                                 uint32_t* __restrict__ sink) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t acc = 0;
+    for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
+        for (uint32_t p = wave; p < P; p += 4) {
+            const uint32_t c = cnt[(uint64_t)b * P + p];
+            const uint64_t a = at[(uint64_t)b * P + p];
+            for (uint32_t e = lane; e < c; e += 64) {
+                const u32x4 v = __builtin_nontemporal_load(in + a + e);
+                acc += v[0] ^ v[3];
+            }
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+__global__ void __launch_bounds__(256) seq_read(uint64_t n, const u32x4* __restrict__ in, uint32_t* __restrict__ sink) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const u32x4 v = __builtin_nontemporal_load(in + i);
+        acc += v[0] ^ v[3];
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 __global__ void __launch_bounds__(256) seq(uint64_t n, u32x4* __restrict__ out) {
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const u32x4 v = {(uint32_t)i, 1, 2, 3};
@@ -131,6 +161,49 @@ int main(int argc, char** argv) {
         best = ms < best ? ms : best;
     }
     printf("sequential: %.3f ms, %.2f GB, %.0f GB/s\n", best, n * 16e-9, n * 16e-9 / (best * 1e-3));
+    {
+        // partition-major layout: run (b, p) at pbase[p] + sum of cnt[b' < b][p]
+        std::vector<uint64_t> at((size_t)NB * P);
+        uint64_t o = 0;
+        for (uint32_t p = 0; p < P; ++p)
+            for (uint32_t b = 0; b < NB; ++b) {
+                at[(size_t)b * P + p] = o;
+                o += cnt[(size_t)b * P + p];
+            }
+        uint32_t* d_cnt = nullptr;
+        uint64_t* d_at = nullptr;
+        uint32_t* sink = nullptr;
+        CHK(hipMalloc(&d_cnt, cnt.size() * 4));
+        CHK(hipMalloc(&d_at, at.size() * 8));
+        CHK(hipMalloc(&sink, 4));
+        CHK(hipMemcpy(d_cnt, cnt.data(), cnt.size() * 4, hipMemcpyHostToDevice));
+        CHK(hipMemcpy(d_at, at.data(), at.size() * 8, hipMemcpyHostToDevice));
+        for (int per : {2, 3, 4}) {
+            float bt = 1e30f;
+            for (int rep = 0; rep < 3; ++rep) {
+                CHK(hipEventRecord(e0));
+                runs_read<<<cus * per, 256>>>(d_cnt, d_at, NB, P, out, sink);
+                CHK(hipEventRecord(e1));
+                CHK(hipEventSynchronize(e1));
+                float ms = 0;
+                CHK(hipEventElapsedTime(&ms, e0, e1));
+                bt = ms < bt ? ms : bt;
+            }
+            printf("partition-major runs read block by block (%d workgroups/CU): %.3f ms, %.0f GB/s\n", per, bt,
+                   o * 16e-9 / (bt * 1e-3));
+        }
+        float bt = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+            CHK(hipEventRecord(e0));
+            seq_read<<<cus * 8, 256>>>(o, out, sink);
+            CHK(hipEventRecord(e1));
+            CHK(hipEventSynchronize(e1));
+            float ms = 0;
+            CHK(hipEventElapsedTime(&ms, e0, e1));
+            bt = ms < bt ? ms : bt;
+        }
+        printf("sequential read: %.3f ms, %.0f GB/s\n", bt, o * 16e-9 / (bt * 1e-3));
+    }
     CHK(hipFree(out));
     return 0;
 }
