@@ -350,6 +350,7 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
     constexpr uint32_t kCntReads = cnt_reads<CK>();
     __shared__ uint32_t cnt[kCntReads][128];
     __shared__ uint64_t s_kofs[kCntReads + 1];
+    __shared__ uint32_t s_tot[128];  // the block's per-doc totals (<= CK each)
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint64_t n = rv.n;
     const uint64_t Nk = kofs[n];
@@ -362,6 +363,7 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
     // reads lo..hi hold the block's k-mers (empty reads between them hold none)
     const uint64_t nr = hi - lo + 1;
     const bool lds_cnt = nr <= kCntReads;
+    if (tid < 128) s_tot[tid] = 0;
     for (uint32_t i = tid; i < CK; i += kResolveThreads) {
         acc[0][i] = ~0u;
         acc[1][i] = ~0u;
@@ -450,19 +452,23 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
             }
         }
     }
-    // per-doc totals of the block (lanes < 32 of each wave) and its k-mer count
+    // per-doc totals of the block and its k-mer count: the waves' sums meet in LDS, then one
+    // global atomic per doc instead of one per doc and wave
     if (partials) {
-        uint64_t* out = partials + (B % (uint32_t)pblocks) * (D + 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const uint32_t d = q * 32 + (uint32_t)lane;
-            if (lane < 32 && d < D && doc_tot[q])
-                atomicAdd(reinterpret_cast<unsigned long long*>(out + d), (unsigned long long)doc_tot[q]);
+            if (lane < 32 && d < D && doc_tot[q]) atomicAdd(&s_tot[d], (uint32_t)doc_tot[q]);
         }
+    }
+    __syncthreads();
+    if (partials) {
+        uint64_t* out = partials + (B % (uint32_t)pblocks) * (D + 1);
+        if ((uint32_t)tid < D && s_tot[tid])
+            atomicAdd(reinterpret_cast<unsigned long long*>(out + tid), (unsigned long long)s_tot[tid]);
         if (tid == 0) atomicAdd(reinterpret_cast<unsigned long long*>(out + D), (unsigned long long)m);
     }
     if (!hits || !lds_cnt) return;
-    __syncthreads();
     // reads wholly inside the block: stored; the edge reads: added
     for (uint32_t x = tid; x < nr * D; x += kResolveThreads) {
         const uint32_t ri = x / D, d = x - ri * D;
