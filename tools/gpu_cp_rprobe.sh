@@ -1,4 +1,5 @@
-# Timing probes of the resolve (results wrong on purpose; bench without the CPU parity sample):
+# Timing probes of the resolve (a temporary build with XSPECT2_AMD_CP_RPROBE = 1: no counting phase,
+# 2: no LDS ANDs; results wrong on purpose; not in the committed source; A/B item 28).
 # default, without the counting phase (1), without the LDS ANDs (2); kernel traces of each.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
