@@ -1,9 +1,9 @@
-# Resolve: per-doc block totals summed in LDS before one global atomic per doc (was one per doc and wave).
+# Resolve: the read search of the count phase moved into the first load pass (overlaps the rows in flight).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 R="$GRAFT_REPO_ROOT"
-F=gpurun_out/r02cnt16; rm -rf $F; mkdir -p $F
+F=gpurun_out/r02rsearch; rm -rf $F; mkdir -p $F
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   -k "partitioned or mixed_streams or over_mall or degenerate or species_model_same" > $F/tests.log 2>&1 || { tail -40 $F/tests.log; exit 12; }
 tail -2 $F/tests.log
