@@ -371,8 +371,8 @@ def main():
         wl.roofline_note = ("achieved = SURVEY.md §8(d)'s algorithmic bytes (h x 64 B per k-mer + reads, hits, "
                             "metadata) over the whole probe (HIP events around the pipeline); traffic = PMC HBM "
                             "bytes of the pipeline per step, below the algorithmic figure: rows come from "
-                            "L2-resident partitions, not random HBM lines.  Per-kernel bounds: bucket = integer "
-                            "multiplies (XXH64 x h + Barrett), lookup = vector-L1 miss path to L2 (TCP pending "
+                            "L2-resident partitions, not random HBM lines.  Per-kernel bounds: bucket = VALU issue "
+                            "(XXH64 x h + Barrett), lookup = vector-L1 miss path to L2 (TCP pending "
                             "stalls), resolve = HBM streaming; see DESIGN.md")
     elif wl.partitioned:
         wl.kernel = ("rbloom partitioned: bloom_bucket (hash, bin by 2 MiB filter partition) -> "
