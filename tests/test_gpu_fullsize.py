@@ -1,0 +1,145 @@
+"""BASELINE.json's config 2 at full size on the GPU (1 M x 150 bp reads, a
+100-species COBS classic bank of 0.61 GB built on the device from 100 x 4 Mbp
+genomes, seed 42: bench.py's species workload), and the genus rbloom filter
+over the same genomes (479 MB).
+
+The oracle cannot probe 1.3e10 k-mer x doc pairs in a test's time, so the full
+batch is checked through properties that do not depend on its size
+(SURVEY.md §8(c)):
+* the two independent device probe paths (direct gathers and the partitioned
+  bucket -> lookup -> resolve pipeline; for rbloom, gather and partitioned)
+  give the same hit matrix, bit for bit;
+* per-doc totals equal the hit matrix's column sums and the k-mer total is
+  n * 130; every read has 130 k-mers (probabilistic_filter_model.py:462);
+* a filter has no false negatives: error-free 150 bp windows of genome d hit
+  doc d (species) / the filter (genus) with all 130 k-mers, which pins the
+  device-built bank at full size;
+* 3,000 reads (the first, the last and a seeded random 1,000) match the C
+  oracle probing the downloaded bank image.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+D, GLEN, N, L, K = 100, 4_000_000, 1_000_000, 150, 21
+NK = L - K + 1
+
+
+@pytest.fixture(scope="module")
+def data():
+    from xspect2_amd.synth import make_genomes, make_reads
+    genomes = make_genomes(D, GLEN, seed=42)
+    reads, _ = make_reads(genomes, N, L, seed=42)
+    return genomes, reads
+
+
+@pytest.fixture(scope="module")
+def dev_inputs(data):
+    torch = pytest.importorskip("torch")
+    genomes, reads = data
+    dev = torch.device("cuda", 0)
+    g = torch.from_numpy(genomes.reshape(-1)).to(dev)
+    g_offs = torch.arange(D + 1, dtype=torch.int64, device=dev) * GLEN
+    r = torch.from_numpy(reads.reshape(-1)).to(dev)
+    r_offs = torch.arange(N + 1, dtype=torch.int64, device=dev) * L
+    return torch, dev, g, g_offs, r, r_offs
+
+
+def _sample_ids():
+    rng = np.random.default_rng(7)
+    return np.unique(np.concatenate([np.arange(1000), np.arange(N - 1000, N), rng.integers(0, N, 1000)]))
+
+
+def _windows(genomes, per_doc=20, seed=11):
+    """Error-free 150 bp windows, per_doc from each genome, and their doc ids."""
+    rng = np.random.default_rng(seed)
+    seqs, docs = [], []
+    for d in range(D):
+        for st in rng.integers(0, GLEN - L + 1, per_doc):
+            seqs.append(genomes[d, st:st + L].tobytes())
+            docs.append(d)
+    return seqs, np.asarray(docs)
+
+
+def _query(bank, torch, dev, r, r_offs, cols):
+    hits = torch.empty((N, cols), dtype=torch.int32, device=dev)
+    nk = torch.empty(N, dtype=torch.int64, device=dev)
+    tot = torch.zeros(cols + 1, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    bank.query_device(r, N * L, r_offs, N, 1, hits, nk, tot, stream=s.cuda_stream)
+    torch.cuda.synchronize(dev)
+    return (hits.cpu().numpy().view(np.uint32), nk.cpu().numpy().view(np.uint64),
+            tot.cpu().numpy().view(np.uint64), bank.probe_path())
+
+
+def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
+    from xspect2_amd import _lib
+    from xspect2_amd.bank import Bank, cobs_signature_size
+    genomes, reads = data
+    torch, dev, g, g_offs, r, r_offs = dev_inputs
+    h = 7
+    sig = cobs_signature_size(GLEN - K + 1, h, 0.01)
+    bank = Bank.create_cobs(K, h, [sig], D, [f"s{i}" for i in range(D)], device=0)
+    bank.build_device(g, genomes.size, g_offs, D, torch.arange(D, dtype=torch.int32, device=dev),
+                      stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+    assert bank.info.device_bytes > 256 << 20  # larger than the Infinity Cache
+
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    h0, n0, t0, p0 = _query(bank, torch, dev, r, r_offs, D)
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "1")
+    h1, n1, t1, p1 = _query(bank, torch, dev, r, r_offs, D)
+    assert p0 == _lib.XS_PATH_GATHER and p1 == _lib.XS_PATH_PARTITIONED
+    assert np.array_equal(h0, h1), int((h0 != h1).sum())
+    assert np.array_equal(n0, n1) and (n1 == NK).all()
+    for t in (t0, t1):
+        assert np.array_equal(t[:D], h1.sum(axis=0, dtype=np.uint64)) and int(t[D]) == N * NK
+    assert int(h1.max()) <= NK
+
+    # no false negatives at full size: error-free windows of genome d hit doc d with every k-mer
+    seqs, docs = _windows(genomes)
+    wh, wn = bank.query(seqs)
+    assert (wn == NK).all() and (wh[np.arange(len(seqs)), docs] == NK).all()
+
+    # the C oracle on the downloaded bank image, for a sample of the batch
+    ob = oracle_mod.CobsBank(bank.download(), [sig], (D + 7) // 8, D, h, K)
+    ids = _sample_ids()
+    want_h, want_n = ob.query([reads[i].tobytes() for i in ids])
+    assert np.array_equal(h1[ids], want_h) and np.array_equal(n1[ids], want_n)
+    wo, _ = ob.query(seqs)
+    assert np.array_equal(wo, wh)
+    bank.close()
+
+
+def test_genus_rbloom_full_size(data, dev_inputs, oracle_mod, monkeypatch):
+    from xspect2_amd import _lib
+    from xspect2_amd.bank import Bank, bloom_parameters
+    genomes, reads = data
+    torch, dev, g, g_offs, r, r_offs = dev_inputs
+    nbytes, nh = bloom_parameters(genomes.size - K + 1, 0.01)  # Bloom(total_length - k + 1, fpr)
+    bank = Bank.create_bloom(K, nbytes, nh, device=0)
+    bank.build_device(g, genomes.size, g_offs, D, None, stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.synchronize(dev)
+
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "0")
+    h0, n0, t0, p0 = _query(bank, torch, dev, r, r_offs, 1)
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    h1, n1, t1, p1 = _query(bank, torch, dev, r, r_offs, 1)
+    assert p0 == _lib.XS_PATH_GATHER and p1 == _lib.XS_PATH_PARTITIONED
+    assert np.array_equal(h0, h1), int((h0 != h1).sum())
+    assert np.array_equal(n0, n1) and (n1 == NK).all()
+    for t in (t0, t1):
+        assert int(t[0]) == int(h1.sum(dtype=np.uint64)) and int(t[1]) == N * NK
+
+    seqs, _ = _windows(genomes)
+    wh, wn = bank.query(seqs)
+    assert (wn == NK).all() and (wh[:, 0] == NK).all()
+
+    ob = oracle_mod.BloomFilter(bank.download(), nh, K)
+    ids = _sample_ids()
+    want_h, want_n = ob.query([reads[i].tobytes() for i in ids])
+    assert np.array_equal(h1[ids, 0], want_h) and np.array_equal(n1[ids], want_n)
+    bank.close()
