@@ -143,3 +143,70 @@ def test_genus_rbloom_full_size(data, dev_inputs, oracle_mod, monkeypatch):
     want_h, want_n = ob.query([reads[i].tobytes() for i in ids])
     assert np.array_equal(h1[ids, 0], want_h) and np.array_equal(n1[ids], want_n)
     bank.close()
+
+
+def test_config4_mlst_full_size(oracle_mod):
+    """Config 4 at full size: 7 loci x 1430 alleles (COBS compact, k = 31,
+    h = 1, fpr 0.001, pages of 64 bytes: 3 doc groups per locus, bench.py's
+    generator), 1 M error-free 150 bp allele windows.  Per locus, on the
+    device: totals = column sums of the 1 M x 1430 hit matrix, 120 k-mers per
+    read, and every read taken from allele a of this locus hits allele a with
+    all 120 k-mers (no false negatives); 3,000 sampled reads equal the C
+    oracle on the downloaded compact bank."""
+    torch = pytest.importorskip("torch")
+    from xspect2_amd.bank import Bank, cobs_signature_size
+    k, loci, n_alleles, page = 31, 7, 1430, 64
+    nk = L - k + 1
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    rng = np.random.default_rng(4242)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    li = rng.integers(0, loci, N)
+    ai = rng.integers(0, n_alleles, N)
+    reads = np.empty((N, L), dtype=np.uint8)
+    r = torch.empty(N * L, dtype=torch.uint8, device=dev)
+    r_offs = torch.arange(N + 1, dtype=torch.int64, device=dev) * L
+    hits = torch.empty((N, n_alleles), dtype=torch.int32, device=dev)
+    d_nk = torch.empty(N, dtype=torch.int64, device=dev)
+    tot = torch.empty(n_alleles + 1, dtype=torch.int64, device=dev)
+    all_alleles, banks = [], []
+    for _ in range(loci):
+        base = acgt[rng.integers(0, 4, 620)]
+        alleles = []
+        for _ in range(n_alleles):
+            a = base[:int(rng.integers(400, 601))].copy()
+            pos = rng.integers(0, a.size, int(rng.integers(0, 12)))
+            a[pos] = acgt[(np.searchsorted(acgt, a[pos]) + 1) % 4]
+            alleles.append(a)
+        alleles.sort(key=lambda a: a.size)  # COBS compact: docs sorted by size
+        per = 8 * page
+        sig = [cobs_signature_size(max(a.size for a in alleles[g:g + per]) - k + 1, 1, 0.001)
+               for g in range(0, n_alleles, per)]
+        bank = Bank.create_cobs(k, 1, sig, n_alleles, [f"Allele_ID_{i}" for i in range(n_alleles)],
+                                page_size=page, compact=True, device=0)
+        buf = np.concatenate(alleles)
+        offs = np.zeros(n_alleles + 1, dtype=np.int64)
+        offs[1:] = np.cumsum([a.size for a in alleles])
+        bank.build_device(torch.from_numpy(buf).to(dev), buf.size, torch.from_numpy(offs).to(dev), n_alleles,
+                          torch.arange(n_alleles, dtype=torch.int32, device=dev), stream=s)
+        all_alleles.append(alleles)
+        banks.append((bank, sig))
+    for i in range(N):
+        a = all_alleles[li[i]][ai[i]]
+        st = int(rng.integers(0, a.size - L + 1))
+        reads[i] = a[st:st + L]
+    r.copy_(torch.from_numpy(reads.reshape(-1)))
+    ids = _sample_ids()
+    for locus, (bank, sig) in enumerate(banks):
+        bank.query_device(r, N * L, r_offs, N, 1, hits, d_nk, tot, stream=s)
+        torch.cuda.synchronize(dev)
+        assert bool((d_nk == nk).all())
+        assert torch.equal(tot[:n_alleles], hits.sum(dim=0, dtype=torch.int64)) and int(tot[n_alleles]) == N * nk
+        mine = torch.from_numpy(np.nonzero(li == locus)[0]).to(dev)
+        own = hits[mine, torch.from_numpy(ai[li == locus]).to(dev)]
+        assert bool((own == nk).all()), int((own != nk).sum())
+        ob = oracle_mod.CobsBank(bank.download(), sig, page, n_alleles, 1, k)
+        want_h, want_n = ob.query([reads[i].tobytes() for i in ids])
+        got = hits[torch.from_numpy(ids).to(dev)].cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want_h) and np.array_equal(want_n, np.full(ids.size, nk, np.uint64))
+        bank.close()
