@@ -398,7 +398,7 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu_pmc_traffic_part.sh, gpu_cp_pmc2.sh)
+    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu/gpu_pmc_traffic_part.sh, gpu_cp_pmc2.sh)
         traffic = None
         try:
             key = "species_partitioned" if wl.partitioned == "cobs" else "genus_partitioned"

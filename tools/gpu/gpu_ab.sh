@@ -1,4 +1,4 @@
-# A/B of an env knob over the default bench:  bash tools/gpu_ab.sh VAR v1 v2 ...
+# A/B of an env knob over the default bench:  bash tools/gpu/gpu_ab.sh VAR v1 v2 ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

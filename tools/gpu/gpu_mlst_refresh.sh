@@ -4,6 +4,6 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/gpu_mlst.sh || exit $?
-WORKLOADS=mlst bash tools/gpu_pmc_traffic.sh > gpurun_out/pmct_mlst.log 2>&1 || { tail -20 gpurun_out/pmct_mlst.log; exit 20; }
+bash tools/gpu/gpu_mlst.sh || exit $?
+WORKLOADS=mlst bash tools/gpu/gpu_pmc_traffic.sh > gpurun_out/pmct_mlst.log 2>&1 || { tail -20 gpurun_out/pmct_mlst.log; exit 20; }
 tail -20 gpurun_out/pmct_mlst.log

@@ -1,4 +1,4 @@
-# A/B of XSPECT2_AMD_WIDE_P on wide classic banks:  bash tools/gpu_wide_ab.sh "1000 300" "1 2 4"
+# A/B of XSPECT2_AMD_WIDE_P on wide classic banks:  bash tools/gpu/gpu_wide_ab.sh "1000 300" "1 2 4"
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp

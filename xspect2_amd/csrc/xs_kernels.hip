@@ -55,7 +55,7 @@ __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
 
 // ------------------------------------------------------------------ rbloom probe
 // Filter bits tested before the rest: 2 measured fastest for member-heavy
-// and foreign-heavy reads alike (tools/gpu_bloom_ab.sh).
+// and foreign-heavy reads alike (tools/gpu/gpu_bloom_ab.sh).
 constexpr int kBloomSplitDefault = 2;
 // All K bit indices first, then all K dword loads in flight at once (the
 // reference stops at the first zero bit; the answer is the same).
