@@ -56,13 +56,16 @@ __global__ void __launch_bounds__(256) gather(const uint32_t* __restrict__ base,
 }
 
 // The lookup's mix: per gathered 16-B row also one 4-B streaming entry load and one 16-B
-// streaming row store (HBM), both contiguous per wave, as in cobs_lookup.
-template <int U>
+// streaming row store (HBM), both contiguous per wave, as in cobs_lookup.  SL < 64: only
+// lanes < SL store, contiguously per wave (the store stream of rows packed to 16 * SL / 64
+// bytes, without the packing itself).
+template <int U, int SL = 64>
 __global__ void __launch_bounds__(256) gather_mix(const uint32_t* __restrict__ base, uint32_t iters,
                                                   const uint32_t* __restrict__ ent, uint4* __restrict__ out,
                                                   uint32_t* __restrict__ sink) {
     const uint32_t* reg = base + (size_t)xcc_id() * kRegionWords;
     const size_t t = blockIdx.x * 256 + threadIdx.x, nt = (size_t)gridDim.x * 256;
+    const size_t lane = t & 63, wv = t >> 6, nw = nt >> 6;
     uint32_t acc = 0;
     for (uint32_t it = 0; it < iters; ++it) {
         uint32_t e[U];
@@ -79,14 +82,18 @@ __global__ void __launch_bounds__(256) gather_mix(const uint32_t* __restrict__ b
         for (int u = 0; u < U; ++u) {
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             const u32x4 q = {v[u].x + e[u], v[u].y, v[u].z, v[u].w};
-            __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + ((size_t)(it * U + u) * nt + t)));
+            if (SL == 64)
+                __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + ((size_t)(it * U + u) * nt + t)));
+            else if (lane < SL)
+                __builtin_nontemporal_store(
+                    q, reinterpret_cast<u32x4*>(out + (((size_t)(it * U + u) * nw + wv) * SL + lane)));
             acc += v[u].x;
         }
     }
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
-template <int U>
+template <int U, int SL = 64>
 static void run_mix(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hipEvent_t e0, hipEvent_t e1) {
     const int grid = cus * per_cu;
     const uint32_t iters = 2048 / U;
@@ -99,16 +106,16 @@ static void run_mix(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hipE
     float best = 1e30f;
     for (int r = 0; r < 3; ++r) {
         CHK(hipEventRecord(e0));
-        gather_mix<U><<<grid, 256>>>(d, iters, ent, out, sink);
+        gather_mix<U, SL><<<grid, 256>>>(d, iters, ent, out, sink);
         CHK(hipEventRecord(e1));
         CHK(hipEventSynchronize(e1));
         float ms = 0;
         CHK(hipEventElapsedTime(&ms, e0, e1));
         best = ms < best ? ms : best;
     }
-    printf("16-B gathers + 4-B entry load + 16-B row store each, %d in flight, %d workgroups/CU: %.3f ms, "
-           "%.1f G gathers/s, %.0f GB/s HBM streams\n", U, per_cu, best, n / (best * 1e-3) / 1e9,
-           n * 20.0 / (best * 1e-3) / 1e9);
+    printf("16-B gathers + 4-B entry load + %.0f-B row store each, %d in flight, %d workgroups/CU: %.3f ms, "
+           "%.1f G gathers/s, %.0f GB/s HBM streams\n", 16.0 * SL / 64, U, per_cu, best, n / (best * 1e-3) / 1e9,
+           n * (4.0 + 16.0 * SL / 64) / (best * 1e-3) / 1e9);
     CHK(hipFree(ent));
     CHK(hipFree(out));
 }
@@ -134,7 +141,8 @@ static void run(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hipEvent
            per_cu, best, req / (best * 1e-3) / 1e9);
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool packed = argc > 1 && argv[1][0] == 'p';  // store-stream width sweep only
     int cus = 0;
     CHK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     uint32_t* d = nullptr;
@@ -145,6 +153,14 @@ int main() {
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
+    if (packed) {  // rows packed to 14 / 12 B (D + 11 id bits in 112 / 96 bits), interleaved
+        for (int r = 0; r < 3; ++r) {
+            run_mix<8, 64>(d, sink, cus, 2, e0, e1);
+            run_mix<8, 56>(d, sink, cus, 2, e0, e1);
+            run_mix<8, 48>(d, sink, cus, 2, e0, e1);
+        }
+        return 0;
+    }
     for (int c : {2, 4}) {
         run_mix<4>(d, sink, cus, c, e0, e1);
         run_mix<8>(d, sink, cus, c, e0, e1);
