@@ -93,6 +93,92 @@ __global__ void __launch_bounds__(256) gather_mix(const uint32_t* __restrict__ b
     if (acc == 0x12345678u) sink[0] = acc;
 }
 
+// Parts of the mix: MODE 1 = gathers + row stores (addresses hashed from the index, no
+// entry loads); 2 = entry loads + gathers (no stores); 3 = entry loads one iteration
+// ahead of their gathers (software-prefetched), + stores.
+template <int U, int MODE>
+__global__ void __launch_bounds__(256) gather_part(const uint32_t* __restrict__ base, uint32_t iters,
+                                                   const uint32_t* __restrict__ ent, uint4* __restrict__ out,
+                                                   uint32_t* __restrict__ sink) {
+    const uint32_t* reg = base + (size_t)xcc_id() * kRegionWords;
+    const size_t t = blockIdx.x * 256 + threadIdx.x, nt = (size_t)gridDim.x * 256;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t acc = 0;
+    uint32_t en[U];
+    if (MODE == 3) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) en[u] = __builtin_nontemporal_load(ent + ((size_t)u * nt + t));
+    }
+    for (uint32_t it = 0; it < iters; ++it) {
+        uint32_t e[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const size_t i = (size_t)(it * U + u) * nt + t;
+            if (MODE == 1) e[u] = (uint32_t)i * 0x9E3779B1u;
+            else if (MODE == 2) e[u] = __builtin_nontemporal_load(ent + i);
+            else if (MODE == 4) e[u] = __builtin_nontemporal_load(ent + (i & ((256u << 10) - 1)));  // L2 hits
+            else if (MODE == 5) e[u] = (xcc_id() & 1) ? (uint32_t)i * 0x9E3779B1u : __builtin_nontemporal_load(ent + i);
+            else e[u] = en[u];
+        }
+        uint4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t h = (e[u] ^ (uint32_t)((it * U + u) * nt + t)) * 2654435761u;
+            const uint32_t o = ((h ^ (h >> 15)) * 2246822519u >> 8) % (kRegionWords / 4) * 4;
+            v[u] = *reinterpret_cast<const uint4*>(reg + o);
+        }
+        // the next iteration's entries are issued after this iteration's gathers, so that
+        // waiting for the gathers (vmcnt counts in issue order) does not wait for them
+        if (MODE == 3) __builtin_amdgcn_sched_barrier(0);  // gathers stay before the prefetches
+        if (MODE == 3) {  // unconditional (the last iteration reloads its own entries), so that the
+                          // compiler's vmcnt counts before the stores stay exact
+            const uint32_t nx = it + 1 < iters ? it + 1 : it;
+#pragma unroll
+            for (int u = 0; u < U; ++u) en[u] = __builtin_nontemporal_load(ent + ((size_t)(nx * U + u) * nt + t));
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (MODE != 2 && (MODE != 5 || (xcc_id() & 1))) {  // (the row alone: e[u]'s registers are the next prefetch's in MODE 3)
+                const u32x4 q = {v[u].x, v[u].y, v[u].z, v[u].w};
+                __builtin_nontemporal_store(q, reinterpret_cast<u32x4*>(out + ((size_t)(it * U + u) * nt + t)));
+            }
+            acc += v[u].x;
+        }
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+template <int U, int MODE>
+static void run_part(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hipEvent_t e0, hipEvent_t e1) {
+    const int grid = cus * per_cu;
+    const uint32_t iters = 2048 / U;
+    const size_t n = (size_t)grid * 256 * iters * U;
+    uint32_t* ent = nullptr;
+    uint4* out = nullptr;
+    CHK(hipMalloc(&ent, n * 4));
+    CHK(hipMalloc(&out, n * 16));
+    CHK(hipMemset(ent, 7, n * 4));
+    float best = 1e30f;
+    for (int r = 0; r < 3; ++r) {
+        CHK(hipEventRecord(e0));
+        gather_part<U, MODE><<<grid, 256>>>(d, iters, ent, out, sink);
+        CHK(hipEventRecord(e1));
+        CHK(hipEventSynchronize(e1));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+    }
+    const char* what[] = {"", "gathers + 16-B row stores (no entry loads)", "4-B entry loads + gathers (no stores)",
+                          "4-B entry loads one iteration ahead + gathers + 16-B row stores",
+                          "4-B entry loads that hit L2 (a 1 MiB array) + gathers + 16-B row stores",
+                          "XCDs split: even XCDs entry loads + gathers, odd XCDs gathers + row stores"};
+    printf("%s, %d in flight, %d workgroups/CU: %.3f ms, %.1f G gathers/s\n", what[MODE], U, per_cu, best,
+           n / (best * 1e-3) / 1e9);
+    CHK(hipFree(ent));
+    CHK(hipFree(out));
+}
+
 template <int U, int SL = 64>
 static void run_mix(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hipEvent_t e0, hipEvent_t e1) {
     const int grid = cus * per_cu;
@@ -153,6 +239,18 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CHK(hipEventCreate(&e0));
     CHK(hipEventCreate(&e1));
+    if (argc > 1 && argv[1][0] == 'm') {  // which part of the mix costs the rate
+        for (int r = 0; r < 2; ++r) {
+            run_mix<8, 64>(d, sink, cus, 2, e0, e1);
+            run_part<8, 1>(d, sink, cus, 2, e0, e1);
+            run_part<8, 2>(d, sink, cus, 2, e0, e1);
+            run_part<8, 3>(d, sink, cus, 2, e0, e1);
+            run_part<8, 4>(d, sink, cus, 2, e0, e1);
+            run_part<8, 5>(d, sink, cus, 2, e0, e1);
+            run<8, 4>(d, sink, cus, 2, e0, e1);
+        }
+        return 0;
+    }
     if (packed) {  // rows packed to 14 / 12 B (D + 11 id bits in 112 / 96 bits), interleaved
         for (int r = 0; r < 3; ++r) {
             run_mix<8, 64>(d, sink, cus, 2, e0, e1);
