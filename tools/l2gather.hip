@@ -118,6 +118,7 @@ __global__ void __launch_bounds__(256) gather_part(const uint32_t* __restrict__ 
             else if (MODE == 2) e[u] = __builtin_nontemporal_load(ent + i);
             else if (MODE == 4) e[u] = __builtin_nontemporal_load(ent + (i & ((256u << 10) - 1)));  // L2 hits
             else if (MODE == 5) e[u] = (xcc_id() & 1) ? (uint32_t)i * 0x9E3779B1u : __builtin_nontemporal_load(ent + i);
+            else if (MODE == 6) e[u] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t*>(ent) + i);  // 2-B entries
             else e[u] = en[u];
         }
         uint4 v[U];
@@ -172,7 +173,8 @@ static void run_part(const uint32_t* d, uint32_t* sink, int cus, int per_cu, hip
     const char* what[] = {"", "gathers + 16-B row stores (no entry loads)", "4-B entry loads + gathers (no stores)",
                           "4-B entry loads one iteration ahead + gathers + 16-B row stores",
                           "4-B entry loads that hit L2 (a 1 MiB array) + gathers + 16-B row stores",
-                          "XCDs split: even XCDs entry loads + gathers, odd XCDs gathers + row stores"};
+                          "XCDs split: even XCDs entry loads + gathers, odd XCDs gathers + row stores",
+                          "2-B entry loads + gathers + 16-B row stores"};
     printf("%s, %d in flight, %d workgroups/CU: %.3f ms, %.1f G gathers/s\n", what[MODE], U, per_cu, best,
            n / (best * 1e-3) / 1e9);
     CHK(hipFree(ent));
@@ -247,6 +249,7 @@ int main(int argc, char** argv) {
             run_part<8, 3>(d, sink, cus, 2, e0, e1);
             run_part<8, 4>(d, sink, cus, 2, e0, e1);
             run_part<8, 5>(d, sink, cus, 2, e0, e1);
+            run_part<8, 6>(d, sink, cus, 2, e0, e1);
             run<8, 4>(d, sink, cus, 2, e0, e1);
         }
         return 0;
