@@ -9,6 +9,7 @@ Tested by tests/test_integration_stub.py.
 """
 import ctypes as C
 import os
+from collections import namedtuple
 import numpy as np
 
 _lib = C.CDLL(os.environ.get("XSPECT_HIP_LIB", "libxspect_hip.so"))  # path or LD_LIBRARY_PATH
@@ -30,6 +31,9 @@ class XsBankInfo(C.Structure):
 _lib.xs_bank_info.argtypes = [C.c_void_p, C.POINTER(XsBankInfo)]
 
 COBS_CLASSIC, COBS_COMPACT, RBLOOM = 0, 1, 2
+# cobs_index.SearchResult: the consumers read .doc_name and .score
+# (probabilistic_filter_model.py:406-409, probabilistic_filter_mlst_model.py:377-380)
+SearchResult = namedtuple("SearchResult", ["doc_name", "score"])
 
 def _check(rc):
     if rc != 0:
@@ -63,10 +67,11 @@ class GpuSearch:
         return hits, nk
 
     def search(self, seq, step=1):
-        """cobs_index.Search.search() shape: [(score, doc_name)], score desc."""
+        """cobs_index.Search.search(): every doc as SearchResult(doc_name, score),
+        score descending (ties by doc index; COBS's own tie order is unpinned)."""
         row = self.search_batch([seq], step)[0][0]
         order = sorted(range(self.D), key=lambda d: (-int(row[d]), d))
-        return [(int(row[d]), self.names[d]) for d in order]
+        return [SearchResult(self.names[d], int(row[d])) for d in order]
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -41,7 +41,8 @@ def species_dir(tmp_path, genomes):
 
 
 def _oracle_species(oracle_mod, species_dir, k=K, h=7, fpr=0.01):
-    files = sorted(species_dir.iterdir())
+    from xspect2_amd.probabilistic_filter_model import training_files
+    files = training_files(species_dir)  # the reference's iterdir order (doc order of the bank)
     seqs, docs = [], []
     for d, f in enumerate(files):
         for r in get_record_iterator(f):

@@ -116,6 +116,20 @@ def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, shift, D):
     _classic_case(xs, oracle_mod, D, 21, 7, [1_000_003], want_path=1)
 
 
+@pytest.mark.parametrize("shift,ck,want_path", [("20", "2048", 1), ("21", "2048", 0), ("20", "4096", 0),
+                                                ("21", "1024", 1)])
+def test_partition_entry_width_limit(xs, oracle_mod, monkeypatch, shift, ck, want_path):
+    """Entries are (row in partition << log2(CK)) | k-mer in block: a plan whose
+    entry would fill all 32 bits (shift + log2(CK) == 32) could produce the
+    all-ones pad sentinel for a real entry, so it falls back to the direct
+    probe; one bit less takes the partitioned path.  Bank of 2^22 + 15 rows
+    (more than one 2^21-row partition); same hits as the oracle either way."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
+    monkeypatch.setenv("XSPECT2_AMD_CP_SHIFT", shift)
+    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
+    _classic_case(xs, oracle_mod, 100, 21, 7, [(1 << 22) + 15], want_path=want_path)
+
+
 def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D * 31 + k)
     rng = np.random.default_rng(D + k + h)
@@ -205,7 +219,12 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     for step in (1, 3):
         want_h, want_n = ob.query(reads, step=step)
         want[step] = (want_h, want_n)
-        got_h, got_n = gb.query(reads, step=step)  # host batches: the first 8 MiB chunk takes the path
+        # host batches go in 8/32 MiB chunks, some under the default's k-mer
+        # threshold (step 3 always): force the path so every chunk takes it
+        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
+        got_h, got_n = gb.query(reads, step=step)
+        assert gb.probe_path() == _lib.XS_PATH_PARTITIONED
+        monkeypatch.delenv("XSPECT2_AMD_COBS_PART")
         assert np.array_equal(got_n, want_n)
         assert np.array_equal(got_h, want_h), int((got_h != want_h).sum())
         tot, nk = gb.query_totals(reads, step=step)

@@ -157,6 +157,46 @@ def test_prepare_input_output_paths(tmp_path):
         prepare_input_output_paths(tmp_path / "nope")
 
 
+def test_directory_walk_orders_are_the_references(tmp_path):
+    """Directory walks happen in the reference's order (iterdir / glob, not
+    sorted): species training files (probabilistic_filter_model.py:170-179),
+    SVM training genomes (probabilistic_filter_svm_model.py:147-152), the
+    MLST locus size (next(glob("*.fasta")), probabilistic_filter_mlst_model.py:
+    127-130) and classify inputs (file_io.py:218-221).  The names are chosen
+    so that directory order and name order are unlikely to agree."""
+    import os
+    from xspect2_amd.probabilistic_filter_mlst_model import first_allele_length
+    from xspect2_amd.probabilistic_filter_model import training_files
+    from xspect2_amd.probabilistic_filter_svm_model import svm_training_files
+
+    rng = np.random.default_rng(3)
+    sp = tmp_path / "species"
+    sp.mkdir()
+    names = [f"{int(x)}.fasta" for x in rng.permutation(40) + 1000] + ["skip.txt", "x.fq"]
+    for n in names:
+        (sp / n).write_text(">a\nACGT\n")
+    (sp / "sub.fasta").mkdir()  # a directory is not a training file
+    want = [sp / n for n in os.listdir(sp) if (sp / n).is_file() and n.split(".")[-1] in ("fasta", "fq")]
+    assert training_files(sp) == want and len(want) == 41
+    svm = tmp_path / "svm"
+    for lab in ("470", "28901", "48296"):
+        for acc in rng.permutation(6):
+            (svm / lab).mkdir(parents=True, exist_ok=True)
+            (svm / lab / f"GCF_{acc}.fna").write_text(">a\nACGT\n")
+    (svm / "notes.txt").write_text("")
+    want = [(svm / lab, svm / lab / f) for lab in os.listdir(svm) if (svm / lab).is_dir()
+            for f in os.listdir(svm / lab)]
+    assert svm_training_files(svm) == want
+    locus = tmp_path / "Oxf_cpn60"
+    locus.mkdir()
+    for i in rng.permutation(30):
+        (locus / f"Allele_ID_{i}.fasta").write_text(f">Oxf_cpn60_{i}\n{'A' * (400 + int(i))}\n>x\nAC\n")
+    first = next(n for n in os.listdir(locus) if n.endswith(".fasta"))
+    assert first_allele_length(locus) == 400 + int(first.split("_")[-1].split(".")[0])
+    ins, _ = prepare_input_output_paths(sp)
+    assert ins == [sp / n for e in ("fasta", "fq") for n in os.listdir(sp) if n.endswith("." + e)]
+
+
 def test_bank_parameter_formulas(oracle_mod):
     for n, h, f in [(4_000_000, 7, 0.01), (600, 1, 0.001)]:
         assert cobs_signature_size(n, h, f) == oracle_mod.signature_size(n, h, f)

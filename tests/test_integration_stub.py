@@ -31,6 +31,28 @@ def _load_stub():
     return mod
 
 
+def _convert_cobs_result_to_dict(cobs_result) -> dict:
+    """Restated consumer: ProbabilisticFilterModel._convert_cobs_result_to_dict
+    (src/xspect/models/probabilistic_filter_model.py:393-409)."""
+    return {individual_result.doc_name: individual_result.score for individual_result in cobs_result}
+
+
+def get_cobs_result(cobs_result, kmer_threshold: bool) -> dict:
+    """Restated consumer: ProbabilisticFilterMlstSchemeModel.get_cobs_result
+    (src/xspect/models/probabilistic_filter_mlst_model.py:362-380)."""
+    hits = [result for result in cobs_result if not kmer_threshold or result.score > 50]
+    return {result.doc_name: result.score for result in hits}
+
+
+def test_stub_search_result_shape():
+    """search() yields cobs_index.SearchResult-like objects (.doc_name, .score)."""
+    mod = _load_stub()
+    r = mod.SearchResult("sp3", 60)
+    assert (r.doc_name, r.score) == ("sp3", 60)
+    assert _convert_cobs_result_to_dict([r, mod.SearchResult("sp1", 0)]) == {"sp3": 60, "sp1": 0}
+    assert get_cobs_result([mod.SearchResult("a", 51), mod.SearchResult("b", 50)], True) == {"a": 51}
+
+
 def test_stub_binds_declared_symbols():
     mod = _load_stub()
     header = (ROOT / "include" / "xspect_hip.h").read_text()
@@ -76,8 +98,17 @@ def test_stub_search_matches_oracle(oracle_mod, tmp_path):
         want, want_n = ob.query([r.encode() for r in reads], step=step)
         assert np.array_equal(got, want.reshape(got.shape)) and np.array_equal(nk, want_n)
     res = s.search(reads[0])
-    assert [n for _, n in res][0] == "sp0" and res[0][0] == 130
-    assert [sc for sc, _ in res] == sorted((sc for sc, _ in res), reverse=True)
+    assert res[0].doc_name == "sp0" and res[0].score == 130
+    assert [r.score for r in res] == sorted((r.score for r in res), reverse=True)
+    # the reference's consumers of cobs_index.SearchResult run unchanged on it
+    for q in reads[:6]:
+        res = s.search(q)
+        row = ob.query([q.encode()])[0][0]
+        conv = _convert_cobs_result_to_dict(res)
+        assert list(conv) == [f"sp{d}" for d in sorted(range(D), key=lambda d: (-int(row[d]), d))]
+        assert conv == {f"sp{d}": int(row[d]) for d in range(D)}
+        assert get_cobs_result(res, False) == conv
+        assert get_cobs_result(res, True) == {n: v for n, v in conv.items() if v > 50}
     del s
 
     nbytes, K = oracle_mod.BloomFilter.params(20_000, 0.01)

@@ -65,12 +65,22 @@ constexpr uint64_t kPad = 64;  // spare bytes after staged host reads
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    // Workspace buffers of a bank handle: every enqueue that touches them ends
+    // with a record of the handle's ws_ev (ws_leave), so waiting for that event
+    // is enough before freeing the old buffer on growth.  Buffers without a
+    // guard wait for the device.
+    const hipEvent_t* guard_ev = nullptr;
+    const bool* guard_used = nullptr;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return XS_OK;
         if (p) {
             // Growth only: work queued earlier on any stream (a device query on
             // the caller's stream) may still read the old buffer.
-            (void)hipDeviceSynchronize();
+            if (guard_ev) {
+                if (*guard_used) (void)hipEventSynchronize(*guard_ev);
+            } else {
+                (void)hipDeviceSynchronize();
+            }
             (void)hipFree(p);
         }
         p = nullptr;
@@ -170,6 +180,15 @@ struct xs_bank {
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
+
+    xs_bank() {
+        for (DevBuf* d : {&seqs, &offs, &nseg, &unit_ofs, &unit_read, &n_units, &scan_tmp, &nk, &hits, &partials,
+                          &totals, &tmp, &best, &rows_read, &pk_nkc, &pk_kofs, &pk_scan, &pk_entries, &pk_tbl,
+                          &pk_miss, &pk_aux, &bloom_tot}) {
+            d->guard_ev = &ws_ev;
+            d->guard_used = &ws_used;
+        }
+    }
 
     uint64_t sig_total() const {
         uint64_t s = 0;

@@ -514,11 +514,15 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     // 2^17 rows (2 MiB) per partition, fewer rows while that leaves under 64
     // partitions (8 per XCD), more while over kPartMax
     const uint32_t floor_shift = mode >= 3 ? 10 : 13;
+    // (an explicit XSPECT2_AMD_CP_SHIFT is kept as given, up to the kPartMax bound)
+    const bool shift_set = getenv("XSPECT2_AMD_CP_SHIFT") != nullptr;
     uint32_t shift = (uint32_t)std::min(std::max(env_int("XSPECT2_AMD_CP_SHIFT", 17), 10), 21);
     auto parts = [sig](uint32_t s) { return (sig + (1ull << s) - 1) >> s; };
-    while (shift > floor_shift && parts(shift) < 64) --shift;
+    while (!shift_set && shift > floor_shift && parts(shift) < 64) --shift;
     while (parts(shift) > kPartMax) ++shift;
-    if (shift + idb > 32) return false;
+    // entry = (row in partition << idb) | k-mer in block: at shift + idb == 32 the
+    // last row's last k-mer would encode to kCobsPadEntry (0xFFFFFFFF)
+    if (shift + idb >= 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
     // small batches: the direct probe is faster below ~60-100 k reads of 150 bp
     // (profiles/r02_cobspart_small.txt)

@@ -229,13 +229,14 @@ def prepare_input_output_paths(input_path: Path):
     """Input files + output-path factory (mirror of file_io.py:194-234).
 
     A directory yields its files grouped by ending in the order of
-    FASTA_ENDINGS + FASTQ_ENDINGS (sorted within an ending, where the reference
-    keeps glob order) and suffixes every output name with _<idx+1>.
+    FASTA_ENDINGS + FASTQ_ENDINGS, each group in ``glob`` (directory) order
+    as the reference's (file_io.py:218-221), and suffixes every output name
+    with _<idx+1>, so output file i belongs to the same input as there.
     """
     input_path = Path(input_path)
     input_is_dir = input_path.is_dir()
     if input_is_dir:
-        inputs = [p for e in FASTA_ENDINGS + FASTQ_ENDINGS for p in sorted(input_path.glob(f"*.{e}"))]
+        inputs = [p for e in FASTA_ENDINGS + FASTQ_ENDINGS for p in input_path.glob(f"*.{e}")]
     elif input_path.is_file():
         inputs = [input_path]
     else:

@@ -43,6 +43,17 @@ def _default_resolver(flattened: dict, scheme_url: str):
     return PubMLSTHandler().get_strain_type_name(flattened, scheme_url)
 
 
+def first_allele_length(locus_path: Path) -> int:
+    """Length of the first record of the first ``*.fasta`` file that
+    ``locus_path.glob`` yields (directory order, not sorted), which the
+    reference stores as the locus' "average" size (:126-130).  It sets the
+    splitter's chunk width and ``has_sufficient_score``'s threshold."""
+    fasta_file_path = next(locus_path.glob("*.fasta"), None)
+    if fasta_file_path is None:
+        raise ValueError(f"No allele FASTA files in {locus_path}")
+    return len(next(get_record_iterator(fasta_file_path)).seq)
+
+
 class ProbabilisticFilterMlstSchemeModel(ProbabilisticFilterModel):
     """One compact bank per locus of an MLST scheme."""
 
@@ -85,8 +96,7 @@ class ProbabilisticFilterMlstSchemeModel(ProbabilisticFilterModel):
             locus = locus_path.name
             alleles = sorted(p for p in locus_path.iterdir() if p.suffix == ".fasta")
             self.loci[locus] = len(alleles)
-            first = next(get_record_iterator(alleles[0]))
-            self.avg_locus_bp_size.append(len(first.seq))
+            self.avg_locus_bp_size.append(first_allele_length(locus_path))
             docs = []
             for p in alleles:
                 seqs = [seq_text(r.seq) for r in get_record_iterator(p)]

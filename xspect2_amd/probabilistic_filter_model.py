@@ -30,6 +30,12 @@ MAX_BATCH_BYTES = 1 << 30
 MAX_BATCH_READS = 1 << 24
 
 
+def training_files(dir_path: Path) -> list[Path]:
+    """Training FASTA/FASTQ files of a species directory in ``iterdir()`` order
+    (reference probabilistic_filter_model.py:170-171)."""
+    return [f for f in dir_path.iterdir() if f.is_file() and f.suffix[1:] in FASTA_ENDINGS + FASTQ_ENDINGS]
+
+
 def _records(sequence_input) -> list | None:
     """Materialise a record list / iterator; None if the input is neither."""
     if isinstance(sequence_input, (list, tuple)):
@@ -118,7 +124,11 @@ class ProbabilisticFilterModel:
     def fit(self, dir_path: Path, display_names: dict | None = None,
             training_accessions: dict[str, list[str]] | None = None) -> None:
         """Build the COBS classic bank from one FASTA/FASTQ file per species
-        (reference :131-194).  Files are taken in name order; the doc name is the
+        (reference :131-194).  Files are taken in ``dir_path.iterdir()`` order,
+        as the reference adds them to its DocumentList (:170-179), so
+        ``display_names`` keeps the reference's key order (which ``_get_svm``'s
+        column indices follow); docs are in the same order (COBS keeping its
+        list order is unverified offline).  The doc name is the
         file name up to its first '.' (as COBS does)."""
         display_names = display_names or {}
         if not isinstance(dir_path, Path):
@@ -128,15 +138,15 @@ class ProbabilisticFilterModel:
         if not dir_path.is_dir():
             raise ValueError("Directory path must be a directory")
         self.training_accessions = training_accessions
-        files = sorted(f for f in dir_path.iterdir()
-                       if f.is_file() and f.suffix[1:] in FASTA_ENDINGS + FASTQ_ENDINGS)
+        files = training_files(dir_path)
+        for f in files:
+            if f.stem in display_names:
+                self.display_names[f.stem.split(".")[0]] = display_names[f.stem]
+            else:
+                self.display_names[f.stem.split(".")[0]] = f.stem
         if not files:
             raise ValueError("No valid files found in directory. Must be fasta or fastq")
-        names = []
-        for f in files:
-            doc = f.stem.split(".")[0]
-            self.display_names[doc] = display_names.get(f.stem, f.stem)
-            names.append(doc)
+        names = [f.stem.split(".")[0] for f in files]
         # signature size from the largest document's term count
         terms = [sum(int(np.maximum(b.lengths().astype(np.int64) - self.k + 1, 0).sum())
                      for b in read_batches(f)) for f in files]

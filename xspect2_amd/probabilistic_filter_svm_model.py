@@ -20,6 +20,22 @@ from .probabilistic_filter_model import ProbabilisticFilterModel
 from .result import MatrixResult, ModelResult
 
 
+def svm_training_files(svm_path: Path) -> list[tuple[Path, Path]]:
+    """(species folder, genome file) pairs in the reference's walk order:
+    ``svm_path.iterdir()`` then each folder's ``iterdir()``, unsorted
+    (probabilistic_filter_svm_model.py:147-152), so scores.csv rows come out
+    in the reference's order."""
+    out = []
+    for species_folder in svm_path.iterdir():
+        if not species_folder.is_dir():
+            continue
+        for file in species_folder.iterdir():
+            if file.suffix[1:] not in FASTA_ENDINGS + FASTQ_ENDINGS:
+                continue
+            out.append((species_folder, file))
+    return out
+
+
 class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
     """COBS species bank on the GPU + scikit-learn SVC on the score vector."""
 
@@ -55,14 +71,11 @@ class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
         super().fit(dir_path, display_names=display_names, training_accessions=training_accessions)
         self.svm_accessions = svm_accessions
         rows = []
-        for species_folder in sorted(p for p in svm_path.iterdir() if p.is_dir()):
-            for file in sorted(species_folder.iterdir()):
-                if file.suffix[1:] not in FASTA_ENDINGS + FASTQ_ENDINGS:
-                    continue
-                print(f"Calculating {file.name} scores for SVM training...")
-                totals = ProbabilisticFilterModel.predict_columnar(self, file, step=svm_step).get_total_scores()
-                values = ",".join(str(v) for _, v in sorted(totals.items()))
-                rows.append(f"{file.stem},{values},{species_folder.name}")
+        for species_folder, file in svm_training_files(svm_path):
+            print(f"Calculating {file.name} scores for SVM training...")
+            totals = ProbabilisticFilterModel.predict_columnar(self, file, step=svm_step).get_total_scores()
+            values = ",".join(str(v) for _, v in sorted(totals.items()))
+            rows.append(f"{file.stem},{values},{species_folder.name}")
         header = f"file,{','.join(sorted(self.display_names))},label_id"
         self.scores_csv_path().parent.mkdir(parents=True, exist_ok=True)
         self.scores_csv_path().write_text("\n".join([header] + rows), encoding="utf-8")
