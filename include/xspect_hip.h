@@ -202,12 +202,18 @@ void xs_bank_close(xs_bank* bank);
 /* ---- Result output (src/xspect/models/result.py:151-202, json.dumps(indent=4)).
  * Appends the "hits", "scores" (with "total") and "num_kmers" sections of a
  * ModelResult JSON for an n x num_docs hit matrix to `path`; the caller writes
- * the fields before and after.  ids_json / labels_json: packed JSON string
- * literals (quotes included) with n+1 / num_docs+1 offsets; doc_mask
- * (num_docs bytes, 1 = keep) may be NULL.  threads <= 0: 16. */
-int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, const uint32_t* hits,
+ * the fields before and after.  hits: counts of hit_bytes = 1, 2 or 4 bytes
+ * (uint8/uint16/uint32: a matrix narrowed on the device stays narrow).
+ * ids_json / labels_json: packed JSON string literals (quotes included) with
+ * n+1 / num_docs+1 offsets; doc_mask (num_docs bytes, 1 = keep) may be NULL.
+ * total_hits (num_docs sums), total_kmers and total_order_row (a hit row
+ * whose COBS order orders the "total" labels): the whole job's totals for one
+ * shard of a read-sharded job (n may then be 0); NULL: computed from this
+ * matrix and its first row.  threads <= 0: 16. */
+int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, const void* hits, int hit_bytes,
                              const uint64_t* num_kmers, const char* ids_json, const uint64_t* ids_off,
                              const char* labels_json, const uint64_t* labels_off, const uint8_t* doc_mask,
+                             const uint64_t* total_hits, uint64_t total_kmers, const uint32_t* total_order_row,
                              int threads);
 
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
@@ -227,14 +233,23 @@ typedef struct xs_fastx_batch {
     const uint64_t* offsets;     /* n+1 entries, offsets[0] = 0 */
     const char* ids;             /* record ids (first header token), packed */
     const uint64_t* id_offsets;  /* n+1 entries */
-    uint64_t text_offset;        /* file bytes consumed so far */
-    uint64_t text_bytes;         /* file size */
+    uint64_t text_offset;        /* file offset parsed up to */
+    uint64_t text_bytes;         /* end offset of the reader's text (file size, or its part's end) */
     const char* descs;           /* record titles (header line minus '>'/'@', right-stripped) */
     const uint64_t* desc_offsets;/* n+1 entries */
 } xs_fastx_batch;
 
 /* threads <= 0: up to 16.  The file is memory-mapped until xs_fastx_close. */
 int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx** out);
+/* Part `part` of `parts` of the file, for one rank of a read-sharded job
+ * (the reference reads the whole file in one
+ * process, file_io.py:47-79): the reader yields only the records whose first
+ * byte lies in [cut(part), cut(part+1)), cut(i) being the first record start at
+ * or after file_size*i/parts.  The parts' records, concatenated in part order,
+ * are exactly the file's records.  Each rank maps the file and parses its own
+ * slice only.  xs_fastx_open(...) = xs_fastx_open_range(..., 0, 1, ...). */
+int xs_fastx_open_range(const char* path, int format, int threads, int flags, uint32_t part, uint32_t parts,
+                        xs_fastx** out);
 /* Parse the next batch: about max_text_bytes of file text, cut at a record
  * start (one record at least).  The batch's buffers stay valid until the
  * SECOND following call, so batch i can be probed while batch i+1 is parsed.

@@ -1,0 +1,192 @@
+"""Config 3 and config 5 end to end over gloo on CPU (world 2 and 3).
+
+* Config 3: ``distributed.classify_species_sharded`` — every rank parses only
+  its byte range of one FASTQ file, probes it, the D+1 totals are
+  all-reduced, rank 0 forms the SVM label, every rank writes a JSON shard.
+  The merged shards must equal the single-process result of the same model
+  (``predict_columnar`` + ``save``, the reference's classify_species flow,
+  src/xspect/classify.py:43-92), for plain and SVM models, exclusions,
+  display names, steps, and more ranks than the file has reads.
+* Config 5: a multi-genus set of 120 documents sharded over the ranks (one
+  bank of 40-50 docs each): the gathered hit matrix equals the bank-by-bank
+  concatenation.
+
+The per-rank probe is the CPU oracle behind the model's index interface
+(test infrastructure); on MI355X the same functions run on the HIP banks
+with RCCL (tests/test_gpu_distributed.py, tools/gpu/gpu_r03_sharded.sh).
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+K = 21
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class _Info:
+    device = 0
+
+
+class OracleIndex:
+    """The Bank interface predict_columnar uses, answered by the CPU oracle."""
+
+    def __init__(self, ob, names):
+        self.ob, self.doc_names, self.num_docs, self.info = ob, list(names), len(names), _Info()
+
+    def query(self, packed, step=1):
+        return self.ob.query_packed(np.ascontiguousarray(packed.buf), np.ascontiguousarray(packed.offsets),
+                                    step=step, threads=1)
+
+
+def _setup(tmp: Path, n_reads: int, svm: bool):
+    """A species model over 6 synthetic genomes (oracle bank), its reads as a FASTQ file."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+
+    rng = np.random.default_rng(7)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    genomes = [acgt[rng.integers(0, 4, 3000)].tobytes() for _ in range(6)]
+    names = [f"GCF_{470 + 13 * d:09d}" for d in range(6)]
+    ob = oracle.CobsBank.empty([oracle.signature_size(3000, 7, 0.01)], 1, 6, 7, K)
+    ob.build(genomes, list(range(6)))
+    base = tmp / "models"
+    if svm:
+        model = ProbabilisticFilterSVMModel(K, "Acinetobacter", None, None, "Species", base, "rbf", 1.0)
+        (base / model.slug()).mkdir(parents=True, exist_ok=True)
+        rows = ["file," + ",".join(sorted(names)) + ",label_id"]
+        for j, lab in enumerate(sorted(names)):
+            for rep in range(3):
+                v = [round(0.05 + 0.02 * rep, 2)] * 6
+                v[j] = 1.0 - 0.1 * rep
+                rows.append(f"acc{j}{rep}," + ",".join(str(x) for x in v) + f",{lab}")
+        (base / model.slug() / "scores.csv").write_text("\n".join(rows))
+    else:
+        model = ProbabilisticFilterModel(K, "Acinetobacter", None, None, "Species", base)
+    model.display_names = {n: f"Acinetobacter sp{d}" for d, n in enumerate(names)}
+    model.index = OracleIndex(ob, names)
+    reads = []
+    for i in range(n_reads):
+        g = genomes[i % 6] if i % 7 else acgt[rng.integers(0, 4, 3000)].tobytes()
+        L = int(rng.integers(K + 1, 200))
+        s = int(rng.integers(0, len(g) - L))
+        reads.append((f"read_{i}", g[s:s + L].decode()))
+    fq = tmp / "reads.fq"
+    fq.write_text("".join(f"@{rid} x\n{s}\n+\n{'I' * len(s)}\n" for rid, s in reads))
+    return model, fq
+
+
+CASES = [dict(step=1), dict(step=3, display_name=True), dict(step=1, exclude_ids=["GCF_000000483"])]
+
+
+def _worker(rank: int, world: int, port: int, tmp: str, n_reads: int, svm: bool):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model, fq = _setup(Path(tmp), n_reads, svm)
+        for i, kw in enumerate(CASES):
+            distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / f"case{i}.json", **kw)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_reads,svm", [(2, 600, False), (3, 600, True), (3, 2, True)])
+def test_classify_species_sharded_equals_single_process(tmp_path, world, n_reads, svm):
+    import torch.multiprocessing as mp
+    from xspect2_amd import distributed
+
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_reads, svm), nprocs=world, join=True)
+    model, fq = _setup(tmp_path, n_reads, svm)
+    for i, kw in enumerate(CASES):
+        res = model.predict_columnar(fq, **kw)
+        res.input_source = fq.name
+        res.save(tmp_path / f"single{i}.json")
+        want = json.loads((tmp_path / f"single{i}.json").read_text())
+        shards = [distributed.shard_path(tmp_path / "out" / f"case{i}.json", r, world) for r in range(world)]
+        assert all(p.exists() for p in shards)
+        got = distributed.merge_result_shards(shards)
+        assert got == want
+        assert list(got["hits"]) == list(want["hits"])
+        if svm:
+            assert got["prediction"] == want["prediction"]
+        per_shard = [len(json.loads(p.read_text())["hits"]) for p in shards]
+        assert sum(per_shard) == n_reads
+        if n_reads >= 600:
+            assert min(per_shard) > n_reads / world / 2  # byte ranges balance the reads
+
+
+def _gather_worker(rank: int, world: int, port: int, tmp: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    import torch
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+    from xspect2_amd.packing import pack_sequences
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        banks, reads = _genera(oracle, world)
+        pr = pack_sequences(reads)
+        ob = banks[rank]
+        hits, nk = distributed.docs_sharded_hits(
+            pr, 1, lambda sl, st: ob.query_packed(sl.buf, sl.offsets, step=st, threads=1))
+        # the tensor-level gather the device path uses, from a CPU tensor
+        h, _ = ob.query_packed(pr.buf, pr.offsets, step=2, threads=1)
+        t = distributed.gather_doc_shards(torch.from_numpy(h.view(np.int32)), 130)
+        np.savez(Path(tmp) / f"g{rank}.npz", hits=hits, nk=nk, step2=t.numpy().view(np.uint32))
+    finally:
+        dist.destroy_process_group()
+
+
+def _genera(oracle, world):
+    """`world` genus banks of 40-50 species (> 100 docs in all), reads from all of them."""
+    rng = np.random.default_rng(5)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    banks, reads = [], []
+    for g in range(world):
+        D = 40 + 5 * g
+        docs = [acgt[rng.integers(0, 4, 800)].tobytes() for _ in range(D)]
+        ob = oracle.CobsBank.empty([oracle.signature_size(800, 7, 0.01)], (D + 7) // 8, D, 7, K)
+        ob.build(docs, list(range(D)))
+        banks.append(ob)
+        reads += [d[o:o + 150] for d in docs[::3] for o in (0, 500)]
+    reads += [acgt[rng.integers(0, 4, 150)].tobytes() for _ in range(30)]
+    return banks, reads
+
+
+@pytest.mark.parametrize("world", [3])
+def test_multigenus_docs_sharded_over_100_docs(tmp_path, world):
+    import torch.multiprocessing as mp
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+
+    mp.spawn(_gather_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    banks, reads = _genera(oracle, world)
+    assert sum(b.D for b in banks) > 100
+    want1 = np.concatenate([b.query(reads)[0] for b in banks], axis=1)
+    want2 = np.concatenate([b.query(reads, step=2)[0] for b in banks], axis=1)
+    assert int(want1.sum()) > 0
+    for r in range(world):
+        o = np.load(tmp_path / f"g{r}.npz")
+        assert np.array_equal(o["hits"], want1)
+        assert np.array_equal(o["step2"], want2)

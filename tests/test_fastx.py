@@ -186,3 +186,48 @@ def test_get_record_iterator_contract(tmp_path):
     ok = tmp_path / "x.fna"
     ok.write_text(">a b\nAC\nGT\n>c\nT\n")
     assert [(r.id, r.seq) for r in get_record_iterator(ok)] == [("a", "ACGT"), ("c", "T")]
+
+
+def _native_part(path, part, parts, max_bytes=1 << 30, threads=0):
+    got = []
+    with FastxReader(path, threads=threads, part=part, parts=parts) as rd:
+        for b in rd.batches(max_bytes):
+            got += _rows(b)
+    return got
+
+
+@pytest.mark.parametrize("kind", ["fasta", "fasta_crlf", "fastq", "fastq_blank", "fastq_wrapped", "tiny"])
+def test_byte_range_parts_stitch_to_the_whole_file(tmp_path, kind):
+    """xs_fastx_open_range: each rank of a read-sharded job parses only its
+    part of the file; the parts, concatenated in part order, are exactly the
+    whole file's records (ids and sequences), for 1-9 parts, more parts than
+    records, every batch size and thread count."""
+    rng = np.random.default_rng(len(kind))
+    text = {"fasta": lambda: _fasta_text(rng, 3000),
+            "fasta_crlf": lambda: _fasta_text(rng, 2000, crlf=True),
+            "fastq": lambda: _fastq_text(rng, 3000),
+            "fastq_blank": lambda: _fastq_text(rng, 3000, crlf=True, blank=True),
+            "fastq_wrapped": lambda: _wrapped_fastq(rng, 3000),
+            "tiny": lambda: b">a\nACGT\n>b\nGG\n"}[kind]()
+    p = tmp_path / ("x.fq" if "fastq" in kind else "x.fasta")
+    p.write_bytes(text)
+    want = ofx.parse_file(p)
+    for parts in (1, 2, 3, 5, 9):
+        got = [_native_part(p, i, parts, mb, th) for i in range(parts)
+               for mb, th in [((1 << 30) if i % 2 else 7000, 1 + i % 3)]]
+        assert [r for g in got for r in g] == want, parts
+        if len(want) >= 100 and parts > 1:
+            sizes = [len(g) for g in got]
+            assert min(sizes) > 0 and max(sizes) <= 2 * len(want) / parts + 10  # balanced by bytes
+    with pytest.raises(ValueError):
+        FastxReader(p, part=3, parts=3)
+
+
+def test_byte_range_parts_of_a_large_file(tmp_path):
+    """Parts larger than 1 MiB are themselves parsed by several threads."""
+    rng = np.random.default_rng(17)
+    p = tmp_path / "big.fastq"
+    p.write_bytes(_fastq_text(rng, 60_000))
+    want = ofx.parse_file(p)
+    got = [r for i in range(3) for r in _native_part(p, i, 3, 3 << 20, 8)]
+    assert got == want

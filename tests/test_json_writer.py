@@ -118,3 +118,51 @@ def test_empty_result_raises_like_reference(tmp_path):
         res.save(tmp_path / "e.json")
     with pytest.raises(ValueError, match="reserved"):
         MatrixResult("m", ["total"], ["a"], np.zeros((1, 1), np.uint32), np.ones(1, np.uint64))
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.uint16])
+def test_narrow_hit_matrices_write_the_same_bytes(tmp_path, dtype):
+    """A hit matrix narrowed to uint8/uint16 (counts <= k-mers per read) is
+    written, summed and converted exactly as the uint32 one."""
+    rng = np.random.default_rng(int(np.dtype(dtype).itemsize))
+    top = 130 if dtype == np.uint8 else 9000
+    nk = rng.integers(top // 2, top + 1, 400).astype(np.uint64)
+    hits = np.minimum(rng.integers(0, top + 1, (400, 30)), nk[:, None]).astype(np.uint32)
+    ids, labels = [f"r{i}" for i in range(400)], [f"d{j}" for j in range(30)]
+    wide = MatrixResult("m", ids, labels, hits, nk, 1, "470", "x.fq")
+    narrow = MatrixResult("m", ids, labels, hits.astype(dtype), nk, 1, "470", "x.fq")
+    assert narrow.hits.dtype == dtype
+    wide.save(tmp_path / "w.json")
+    narrow.save(tmp_path / "n.json")
+    assert (tmp_path / "n.json").read_bytes() == (tmp_path / "w.json").read_bytes()
+    assert narrow.get_total_hits() == wide.get_total_hits()
+    assert narrow.to_model_result().to_dict() == wide.to_model_result().to_dict()
+
+
+@pytest.mark.parametrize("cut", [[0, 37, 120, 200], [0, 0, 150, 200], [0, 200, 200, 200]])
+def test_sharded_results_stitch_to_the_whole(tmp_path, cut):
+    """Shards of a read-sharded job (set_job_totals: the job's sums, k-mer
+    count and first row) write per-read sections for their own reads and the
+    job's "total"; merged, they are the whole result's JSON.  A shard without
+    reads writes empty sections, as json.dumps does."""
+    import json
+    from xspect2_amd.distributed import merge_result_shards
+
+    rng = np.random.default_rng(sum(cut))
+    n, D = 200, 9
+    nk = rng.integers(60, 131, n).astype(np.uint64)
+    hits = np.minimum(rng.integers(0, 131, (n, D)), nk[:, None]).astype(np.uint8)
+    ids, labels = [f"read_{i}" for i in range(n)], [f"sp{j}" for j in range(D)]
+    mask = np.ones(D, np.uint8)
+    mask[4] = 0
+    whole = MatrixResult("m", ids, labels, hits, nk, 2, "470", "in.fq", mask)
+    whole.save(tmp_path / "whole.json")
+    paths = []
+    for p, (lo, hi) in enumerate(zip(cut, cut[1:])):
+        sh = MatrixResult("m", ids[lo:hi], labels, hits[lo:hi], nk[lo:hi], 2, "470", "in.fq", mask)
+        sh.set_job_totals(hits.sum(axis=0, dtype=np.uint64), int(nk.sum()), hits[0])
+        assert sh.get_total_scores() == whole.get_total_scores()
+        sh.save(tmp_path / f"s{p}.json")
+        json.loads((tmp_path / f"s{p}.json").read_text())  # every shard is valid JSON
+        paths.append(tmp_path / f"s{p}.json")
+    assert merge_result_shards(paths) == json.loads((tmp_path / "whole.json").read_text())

@@ -149,8 +149,9 @@ int main() {
         for (auto& m : mask) m = rng() % 3 != 0;
         FILE* f = fopen("/tmp/xs_asan_out.json", "wb");
         fclose(f);
-        if (xs_write_result_sections("/tmp/xs_asan_out.json", n, D, hits.data(), nk.data(), ids.c_str(), io.data(),
-                                     labels.c_str(), lo.data(), trial % 2 ? mask.data() : nullptr, 1 + trial % 8))
+        if (xs_write_result_sections("/tmp/xs_asan_out.json", n, D, hits.data(), 4, nk.data(), ids.c_str(), io.data(),
+                                     labels.c_str(), lo.data(), trial % 2 ? mask.data() : nullptr, nullptr, 0,
+                                     nullptr, 1 + trial % 8))
             ++errors;
     }
     printf("host sanitizer run: %d input files x 15 reader configurations, 20 JSON matrices; "

@@ -305,6 +305,42 @@ bool fastq_wrapped(const char* p, const char* end) {
     return false;
 }
 
+// Wrapped FASTQ cannot be cut by pattern: the first record start at or after
+// `pos`, found by walking the records from the start of the text (the same
+// line rules as parse_fastq, nothing copied).  A malformed record ends the
+// walk there; the part that holds it reports the error when parsed.
+const char* fastq_boundary_sequential(const char* lo, const char* pos, const char* end) {
+    const char *b, *le;
+    const char* q = lo;
+    for (;;) {
+        const char* rec_start = q;
+        bool got = false;
+        while (next_line(q, end, b, le)) {
+            if (rstrip(b, le) == b) {
+                rec_start = q;
+                continue;
+            }
+            got = true;
+            break;
+        }
+        if (!got) return end;
+        if (rec_start >= pos) return rec_start;
+        if (*b != '@') return rec_start;
+        size_t slen = 0;
+        bool plus = false;
+        while (next_line(q, end, b, le)) {
+            if (le > b && *b == '+') {
+                plus = true;
+                break;
+            }
+            slen += (size_t)(rstrip(b, le) - b);
+        }
+        if (!plus) return rec_start;
+        size_t qlen = 0;
+        while (qlen < slen && next_line(q, end, b, le)) qlen += (size_t)(rstrip(b, le) - b);
+    }
+}
+
 struct Batch {
     HostBuf seqs, offs, ids, id_offs, descs, desc_offs;
     uint64_t n = 0, seq_bytes = 0;
@@ -318,7 +354,8 @@ struct xs_fastx {
     bool wrapped = false;
     int fd = -1;
     const char* base = nullptr;
-    size_t size = 0;
+    size_t size = 0;   // mapped bytes
+    size_t stop = 0;   // end of this reader's text (the file, or its part)
     size_t cur = 0;
     uint64_t records = 0;
     Batch batch[2];
@@ -333,7 +370,13 @@ struct xs_fastx {
 extern "C" {
 
 int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx** out) {
+    return xs_fastx_open_range(path, format, threads, flags, 0, 1, out);
+}
+
+int xs_fastx_open_range(const char* path, int format, int threads, int flags, uint32_t part, uint32_t parts,
+                        xs_fastx** out) {
     if (!path || !out) return xs::set_error(XS_ERR_ARG, "null argument");
+    if (parts == 0 || part >= parts) return xs::set_error(XS_ERR_ARG, "part must be < parts");
     if (format != XS_FASTX_FASTA && format != XS_FASTX_FASTQ)
         return xs::set_error(XS_ERR_ARG, "format must be XS_FASTX_FASTA or XS_FASTX_FASTQ");
     *out = nullptr;
@@ -362,6 +405,25 @@ int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx
     int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     r->threads = std::min(t, 64);
     if (format == XS_FASTX_FASTQ && r->size) r->wrapped = fastq_wrapped(r->base, r->base + r->size);
+    // Part p of P: the records whose first byte lies in [cut(p), cut(p+1)), cut(i)
+    // = the first record start at or after size*i/P (cut(0) = 0, cut(P) = size).
+    // Every record belongs to exactly one part, in file order.
+    r->stop = r->size;
+    if (parts > 1 && r->size) {
+        const char* lo = r->base;
+        const char* end = r->base + r->size;
+        auto cut = [&](uint64_t i) -> size_t {
+            if (i == 0) return 0;
+            if (i >= parts) return r->size;
+            const char* pos = lo + (size_t)((unsigned __int128)r->size * i / parts);
+            const char* c = format == XS_FASTX_FASTA ? fasta_boundary(lo, pos, end)
+                            : r->wrapped             ? fastq_boundary_sequential(lo, pos, end)
+                                                     : fastq_boundary(lo, pos, end);
+            return (size_t)(c - lo);
+        };
+        r->cur = cut(part);
+        r->stop = std::max(r->cur, cut((uint64_t)part + 1));
+    }
     for (auto& b : r->batch) {
         const bool pinned = (flags & XS_FASTX_PINNED) != 0;
         b.seqs.pinned = b.offs.pinned = pinned;
@@ -377,7 +439,7 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     Batch& bt = r->batch[r->flip];
     r->flip ^= 1;
     bt.n = bt.seq_bytes = 0;
-    const char* end = r->base + r->size;
+    const char* end = r->base + r->stop;
     const size_t budget = std::max<uint64_t>(max_text_bytes, 1);
     int nparts = 0;
     // a window can hold no record (text before the first one): go on until
@@ -426,7 +488,7 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     if (nparts) r->cur = (size_t)(r->parts[nparts - 1].stop - r->base);
     size_t got = 0;
     for (int i = 0; i < nparts; ++i) got += r->parts[i].lens.size();
-    if (got || r->cur >= r->size || !nparts) break;
+    if (got || r->cur >= r->stop || !nparts) break;
     }
     // pack the parts
     uint64_t n = 0, sbytes = 0, ibytes = 0, dbytes = 0;
@@ -487,7 +549,7 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     out->ids = bt.ids.p;
     out->id_offsets = ioffs;
     out->text_offset = r->cur;
-    out->text_bytes = r->size;
+    out->text_bytes = r->stop;
     out->descs = bt.descs.p;
     out->desc_offsets = doffs;
     return XS_OK;

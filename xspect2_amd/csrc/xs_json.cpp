@@ -56,9 +56,10 @@ struct ScoreCache {  // per thread: score strings of h = 0..n for the last n see
     }
 };
 
+template <class T>
 struct Ctx {
     uint64_t n, D;
-    const uint32_t* hits;
+    const T* hits;  // n x D counts (uint8, uint16 or uint32)
     const uint64_t* nk;
     const char* ids;
     const uint64_t* ids_off;
@@ -67,10 +68,10 @@ struct Ctx {
     std::vector<uint32_t> docs;  // emitted docs (doc_mask), ascending
 };
 
-// Docs of read r in COBS result order: count descending, ties by doc index.
-void order_of(const Ctx& c, uint64_t r, std::vector<uint32_t>& ord) {
-    ord = c.docs;
-    const uint32_t* row = c.hits + r * c.D;
+// Docs of one hit row in COBS result order: count descending, ties by doc index.
+template <class T>
+void order_of(const std::vector<uint32_t>& docs, const T* row, std::vector<uint32_t>& ord) {
+    ord = docs;
     std::stable_sort(ord.begin(), ord.end(), [row](uint32_t a, uint32_t b) { return row[a] > row[b]; });
 }
 
@@ -79,7 +80,8 @@ inline void put_key(std::string& o, const char* base, const uint64_t* off, uint6
 }
 
 // section 0: hits, 1: scores, 2: num_kmers — entries of reads [lo, hi)
-void format_block(const Ctx& c, int section, uint64_t lo, uint64_t hi, std::string& o) {
+template <class T>
+void format_block(const Ctx<T>& c, int section, uint64_t lo, uint64_t hi, std::string& o) {
     std::vector<uint32_t> ord;
     ScoreCache cache;
     char num[32];
@@ -97,15 +99,15 @@ void format_block(const Ctx& c, int section, uint64_t lo, uint64_t hi, std::stri
             continue;
         }
         o += ": {\n";
-        order_of(c, r, ord);
-        const uint32_t* row = c.hits + r * c.D;
+        const T* row = c.hits + r * c.D;
+        order_of(c.docs, row, ord);
         for (size_t j = 0; j < ord.size(); ++j) {
             if (j) o += ",\n";
             o += "            ";
             put_key(o, c.labels, c.labels_off, ord[j]);
             o += ": ";
             if (section == 0) {
-                int k = snprintf(num, sizeof(num), "%u", row[ord[j]]);
+                int k = snprintf(num, sizeof(num), "%u", (unsigned)row[ord[j]]);
                 o.append(num, (size_t)k);
             } else {
                 o += cache.get(row[ord[j]], c.nk[r]);
@@ -115,56 +117,52 @@ void format_block(const Ctx& c, int section, uint64_t lo, uint64_t hi, std::stri
     }
 }
 
-}  // namespace
-
-extern "C" {
-
-int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, const uint32_t* hits,
-                             const uint64_t* num_kmers, const char* ids_json, const uint64_t* ids_off,
-                             const char* labels_json, const uint64_t* labels_off, const uint8_t* doc_mask,
-                             int threads) {
-    if (!path || (n && (!hits || !num_kmers || !ids_json || !ids_off)) || !labels_json || !labels_off)
-        return xs::set_error(XS_ERR_ARG, "null argument");
-    if (n == 0) return xs::set_error(XS_ERR_ARG, "a result needs at least one read");
-    Ctx c{n, num_docs, hits, num_kmers, ids_json, ids_off, labels_json, labels_off, {}};
-    for (uint64_t d = 0; d < num_docs; ++d)
-        if (!doc_mask || doc_mask[d]) c.docs.push_back((uint32_t)d);
-    for (uint64_t r = 0; r < n; ++r)
-        if (num_kmers[r] == 0) return xs::set_error(XS_ERR_ARG, "a read has no k-mers (scores divide by zero)");
-
+template <class T>
+int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits, uint64_t total_kmers_in,
+                   const uint32_t* total_order_row, int threads) {
+    const uint64_t n = c.n, num_docs = c.D;
     FILE* f = fopen(path, "ab");
     if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
-    const int T = std::max(1, std::min(threads > 0 ? threads : 16, 64));
+    const int NT = std::max(1, std::min(threads > 0 ? threads : 16, 64));
     const uint64_t block = 1 << 16;  // reads per formatting round
-    std::vector<std::string> out((size_t)T);
+    std::vector<std::string> out((size_t)NT);
     bool ok = true;
-    const char* heads[3] = {"\"hits\": {\n", "\"scores\": {\n", "\"num_kmers\": {\n"};
+    const char* heads[3] = {"\"hits\": ", "\"scores\": ", "\"num_kmers\": "};
     for (int section = 0; section < 3 && ok; ++section) {
-        ok = fputs(heads[section], f) >= 0;
+        // an empty section is "{}" as json.dumps writes it (a shard without reads)
+        const bool empty = n == 0 && section != 1;
+        ok = fputs(heads[section], f) >= 0 && fputs(empty ? "{}" : "{\n", f) >= 0;
         for (uint64_t b0 = 0; b0 < n && ok; b0 += block) {
             const uint64_t b1 = std::min(n, b0 + block);
-            const uint64_t per = (b1 - b0 + T - 1) / T;
+            const uint64_t per = (b1 - b0 + NT - 1) / NT;
             std::vector<std::thread> th;
             auto work = [&](int t) {
                 out[t].clear();
                 const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
                 if (lo < hi) format_block(c, section, lo, hi, out[t]);
             };
-            for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+            for (int t = 1; t < NT; ++t) th.emplace_back(work, t);
             work(0);
             for (auto& x : th) x.join();
-            for (int t = 0; t < T && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
+            for (int t = 0; t < NT && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
         }
         if (!ok) break;
         if (section == 1) {
-            // "total": labels in the first read's order, round(sum hits / sum num_kmers, 2)
+            // "total": labels in the first read's order, round(sum hits / sum num_kmers, 2);
+            // a shard of a read-sharded job passes the whole job's sums and first row
             std::vector<uint64_t> tot(num_docs, 0);
-            for (uint64_t r = 0; r < n; ++r)
-                for (uint64_t d = 0; d < num_docs; ++d) tot[d] += hits[r * num_docs + d];
-            const uint64_t total_kmers = std::accumulate(num_kmers, num_kmers + n, (uint64_t)0);
+            uint64_t total_kmers = total_kmers_in;
+            if (total_hits) {
+                std::copy(total_hits, total_hits + num_docs, tot.begin());
+            } else {
+                for (uint64_t r = 0; r < n; ++r)
+                    for (uint64_t d = 0; d < num_docs; ++d) tot[d] += c.hits[r * num_docs + d];
+                total_kmers = std::accumulate(c.nk, c.nk + n, (uint64_t)0);
+            }
             std::vector<uint32_t> ord;
-            order_of(c, 0, ord);
-            std::string o = ",\n        \"total\": ";
+            if (total_order_row) order_of(c.docs, total_order_row, ord);
+            else order_of(c.docs, c.hits, ord);
+            std::string o = n ? ",\n        \"total\": " : "        \"total\": ";
             if (ord.empty()) {
                 o += "{}";
             } else {
@@ -172,18 +170,55 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
                 for (size_t j = 0; j < ord.size(); ++j) {
                     if (j) o += ",\n";
                     o += "            ";
-                    put_key(o, labels_json, labels_off, ord[j]);
+                    put_key(o, c.labels, c.labels_off, ord[j]);
                     o += ": " + score_text(tot[ord[j]], total_kmers);
                 }
                 o += "\n        }";
             }
             ok = fwrite(o.data(), 1, o.size(), f) == o.size();
         }
-        if (ok) ok = fputs(section < 2 ? "\n    },\n    " : "\n    },\n", f) >= 0;
+        if (ok)
+            ok = fputs(empty ? (section < 2 ? ",\n    " : ",\n") : (section < 2 ? "\n    },\n    " : "\n    },\n"), f) >= 0;
     }
     if (fclose(f) != 0) ok = false;
     if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
     return XS_OK;
+}
+
+template <class T>
+int write_typed(const char* path, uint64_t n, uint64_t num_docs, const void* hits, const uint64_t* num_kmers,
+                const char* ids_json, const uint64_t* ids_off, const char* labels_json, const uint64_t* labels_off,
+                const uint8_t* doc_mask, const uint64_t* total_hits, uint64_t total_kmers,
+                const uint32_t* total_order_row, int threads) {
+    Ctx<T> c{n, num_docs, static_cast<const T*>(hits), num_kmers, ids_json, ids_off, labels_json, labels_off, {}};
+    for (uint64_t d = 0; d < num_docs; ++d)
+        if (!doc_mask || doc_mask[d]) c.docs.push_back((uint32_t)d);
+    return write_sections(path, c, total_hits, total_kmers, total_order_row, threads);
+}
+
+}  // namespace
+
+extern "C" {
+
+int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, const void* hits, int hit_bytes,
+                             const uint64_t* num_kmers, const char* ids_json, const uint64_t* ids_off,
+                             const char* labels_json, const uint64_t* labels_off, const uint8_t* doc_mask,
+                             const uint64_t* total_hits, uint64_t total_kmers, const uint32_t* total_order_row,
+                             int threads) {
+    if (!path || (n && (!hits || !num_kmers || !ids_json || !ids_off)) || !labels_json || !labels_off)
+        return xs::set_error(XS_ERR_ARG, "null argument");
+    if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return xs::set_error(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
+    if (total_hits) {
+        if (!total_order_row) return xs::set_error(XS_ERR_ARG, "total_hits needs total_order_row");
+        if (total_kmers == 0) return xs::set_error(XS_ERR_ARG, "total_kmers must be > 0 (scores divide by it)");
+    } else if (n == 0) {
+        return xs::set_error(XS_ERR_ARG, "a result needs at least one read");
+    }
+    for (uint64_t r = 0; r < n; ++r)
+        if (num_kmers[r] == 0) return xs::set_error(XS_ERR_ARG, "a read has no k-mers (scores divide by zero)");
+    auto w = hit_bytes == 1 ? write_typed<uint8_t> : hit_bytes == 2 ? write_typed<uint16_t> : write_typed<uint32_t>;
+    return w(path, n, num_docs, hits, num_kmers, ids_json, ids_off, labels_json, labels_off, doc_mask, total_hits,
+             total_kmers, total_order_row, threads);
 }
 
 }  // extern "C"

@@ -2,20 +2,30 @@
 
 Two partitionings:
 
-* **reads sharded, bank replicated** (config 3) — each rank probes a
-  contiguous slice of the reads against its own replica of the bank; the only
-  exchange is one all-reduce (sum) of D+1 uint64 counters (per-doc totals and
+* **reads sharded, bank replicated** (config 3) — each rank classifies a
+  contiguous share of the reads against its own replica of the bank; the
+  only exchange is one all-reduce (sum) of D+1 counters (per-doc totals and
   the k-mer total), the inputs of ``ModelResult.get_scores()["total"]`` and
   the SVM vector.  Per-read hit rows stay on the rank that computed them.
+  ``classify_species_sharded`` is the whole flow for one input file: every
+  rank parses only its byte range of the file (xs_fastx_open_range), the
+  totals are all-reduced on a device tensor, rank 0 forms the SVM vector and
+  label, and every rank writes its own JSON shard.
 * **docs sharded** (config 5) — each rank holds a different bank (e.g. one
   genus of a multi-genus collection) and probes all reads; per-read hit
-  vectors are all-gathered along the doc axis.
+  vectors are all-gathered along the doc axis, in the narrowest integer type
+  that carries them (``docs_sharded_hits_device`` stays on the device from
+  the probe to the gathered matrix).
 
-The per-rank compute is a callable so the collectives can be exercised with
-``gloo`` on CPU (tests) and with the HIP banks + RCCL on MI355X.
+The collectives run on CUDA tensors when the process group is RCCL
+(``nccl``) and on CPU tensors under ``gloo`` (CPU tests, and the one-GPU
+rehearsal where several ranks share a device).  The per-rank compute of the
+host-level helpers is a callable so they can be exercised with the CPU oracle.
 """
 from __future__ import annotations
 
+import json
+from pathlib import Path
 from typing import Callable
 
 import numpy as np
@@ -42,14 +52,40 @@ def _dist():
     return dist
 
 
+def collective_device():
+    """Where collective tensors live: the current GPU under RCCL, else the CPU."""
+    import torch
+    dist = _dist()
+    if dist.get_backend() == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
+def _on_wire(t):
+    """`t` moved to the collective device (a no-op when it is already there)."""
+    dev = collective_device()
+    return t if t.device == dev else t.to(dev)
+
+
+def allreduce_(t, op=None):
+    """In-place all-reduce of a tensor on any device (RCCL on the device, or
+    gloo through a host copy)."""
+    dist = _dist()
+    op = dist.ReduceOp.SUM if op is None else op
+    w = _on_wire(t)
+    dist.all_reduce(w, op=op)
+    if w is not t:
+        t.copy_(w)
+    return t
+
+
 def allreduce_totals(totals: np.ndarray, total_kmers: int, device=None) -> tuple[np.ndarray, int]:
     """Sum of (per-doc totals, k-mer total) over all ranks (one collective)."""
     import torch
-    dist = _dist()
     t = torch.from_numpy(np.concatenate([totals.astype(np.int64), [np.int64(total_kmers)]]))
     if device is not None:
         t = t.to(device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    allreduce_(t)
     out = t.cpu().numpy().view(np.uint64)
     return out[:-1].copy(), int(out[-1])
 
@@ -92,41 +128,71 @@ def transport_dtype(max_count: int):
     return torch.int32
 
 
-def docs_sharded_hits(reads: PackedReads, step: int,
-                      local_query: Callable[[PackedReads, int], tuple[np.ndarray, np.ndarray]],
-                      device=None) -> tuple[np.ndarray, np.ndarray]:
-    """Config 5: each rank's bank covers its own docs; gather [n, sum(D_r)] in rank order.
+def gather_doc_shards(hits, max_count: int):
+    """All-gather per-rank hit columns [n, D_r] (any integer tensor, any
+    device) into [n, sum(D_r)] int32 in rank order, on the tensor's device.
 
-    The hit rows travel in the narrowest integer type that holds the largest
-    k-mer count of any read on any rank (agreed by one all-reduce), and are
-    widened back to uint32 on arrival."""
+    The rows travel in ``transport_dtype`` of the largest per-read k-mer count
+    on any rank (one all-reduce agrees on it), padded to the widest D_r; the
+    narrowing and widening run where the tensor is (on the GPU for the
+    device-resident path)."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
-    hits, nk = local_query(reads, step)
     n, d_local = hits.shape
-    nk = np.asarray(nk)
-    meta = torch.tensor([d_local, int(nk.max()) if nk.size else 0], dtype=torch.int64)
-    dims = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    if device is not None:
-        dims = [x.to(device) for x in dims]
-        meta = meta.to(device)
-    dist.all_gather(dims, meta)
-    d_max = max(int(x[0].item()) for x in dims)
-    dt = transport_dtype(max(int(x[1].item()) for x in dims))
-    pad = torch.zeros((n, d_max), dtype=dt)
-    pad[:, :d_local] = torch.from_numpy(hits.astype(np.int64)).to(dt)
-    if device is not None:
-        pad = pad.to(device)
+    meta = torch.tensor([d_local, int(max_count)], dtype=torch.int64)
+    allmeta = [torch.zeros(2, dtype=torch.int64, device=collective_device()) for _ in range(world)]
+    dist.all_gather(allmeta, _on_wire(meta))
+    dims = [int(m[0].item()) for m in allmeta]
+    dt = transport_dtype(max(int(m[1].item()) for m in allmeta))
+    d_max = max(dims)
+    pad = torch.zeros((n, d_max), dtype=dt, device=hits.device)
+    pad[:, :d_local] = hits.to(dt)  # lossless: counts <= k-mers per read <= max_count
     # gloo and RCCL gather no int16: 2-byte rows travel as float16 bit patterns
     # (an all-gather copies bits, it does no arithmetic)
-    wire = pad.view(torch.float16) if dt == torch.int16 else pad
+    wire = _on_wire(pad.view(torch.float16) if dt == torch.int16 else pad)
     parts = [torch.empty_like(wire) for _ in range(world)]
     dist.all_gather(parts, wire)
-    if dt == torch.int16:
-        parts = [p.view(torch.int16) for p in parts]
-    cols = [p.cpu().to(torch.int64).numpy()[:, :int(d[0].item())] for p, d in zip(parts, dims)]
-    return np.concatenate(cols, axis=1).astype(np.uint32), nk
+    cols = []
+    for p, d in zip(parts, dims):
+        if dt == torch.int16:
+            p = p.view(torch.int16)
+        cols.append(p.to(hits.device)[:, :d].to(torch.int32))
+    return torch.cat(cols, dim=1)
+
+
+def docs_sharded_hits(reads: PackedReads, step: int,
+                      local_query: Callable[[PackedReads, int], tuple[np.ndarray, np.ndarray]],
+                      device=None) -> tuple[np.ndarray, np.ndarray]:
+    """Config 5 from host reads: each rank's bank covers its own docs; the
+    hit columns of all ranks [n, sum(D_r)] in rank order (host uint32)."""
+    import torch
+    hits, nk = local_query(reads, step)
+    nk = np.asarray(nk)
+    t = torch.from_numpy(np.ascontiguousarray(hits).view(np.int32))
+    if device is not None:
+        t = t.to(device)
+    out = gather_doc_shards(t, int(nk.max()) if nk.size else 0)
+    return out.cpu().numpy().view(np.uint32), nk
+
+
+def docs_sharded_hits_device(bank, d_seqs, seq_bytes: int, d_offsets, n: int, step: int = 1, stream=None):
+    """Config 5 on the device: probe device-resident reads against this rank's
+    bank (xs_query_device), then all-gather the hit columns of every rank over
+    RCCL, narrowed to the smallest exact type on the device and widened back
+    there.  Returns (hits [n, sum(D_r)] int32, num_kmers [n] int64), both on
+    the bank's device; nothing crosses to the host but two 16-byte metadata
+    exchanges."""
+    import torch
+    dev = torch.device("cuda", bank.info.device)
+    d_hits = torch.empty((n, bank.num_docs), dtype=torch.int32, device=dev)
+    d_nk = torch.empty(n, dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev) if stream is None else stream
+    bank.query_device(d_seqs, seq_bytes, d_offsets, n, step, d_hits, d_nk, None, stream=s.cuda_stream)
+    with torch.cuda.stream(s):
+        mx = d_nk.max().reshape(1) if n else torch.zeros(1, dtype=torch.int64, device=dev)
+        allreduce_(mx, _dist().ReduceOp.MAX)
+        return gather_doc_shards(d_hits, int(mx.item())), d_nk
 
 
 def svm_vector(labels: list[str], totals, total_kmers: int) -> list[float]:
@@ -149,3 +215,106 @@ def reads_sharded_svm_predict(reads: PackedReads, step: int, labels: list[str],
         out[0] = str(classify([svm_vector(labels, tot, nk)]))
     dist.broadcast_object_list(out, src=0)
     return out[0]
+
+
+# ---------------------------------------------------------------- config 3: sharded classify
+def shard_path(output_path: Path, rank: int, world: int) -> Path:
+    """JSON shard of one rank: <stem>.part<rank+1>-of-<world><suffix>."""
+    output_path = Path(output_path)
+    return output_path.with_name(f"{output_path.stem}.part{rank + 1}-of-{world}{output_path.suffix}")
+
+
+def _job_first_row(res, D: int) -> np.ndarray:
+    """Hit row of the job's first read (first read of the lowest rank that has
+    one), which orders the labels of the job's "total" scores as the
+    reference's get_total_hits does (result.py:84-90)."""
+    import torch
+    dist = _dist()
+    world = dist.get_world_size()
+    flags = [torch.zeros(1, dtype=torch.int64, device=collective_device()) for _ in range(world)]
+    dist.all_gather(flags, _on_wire(torch.tensor([len(res.ids)], dtype=torch.int64)))
+    owners = [r for r, f in enumerate(flags) if int(f.item()) > 0]
+    if not owners:
+        raise IndexError("list index out of range")  # get_total_hits on no reads, as the reference
+    row = torch.zeros(D, dtype=torch.int64)
+    if dist.get_rank() == owners[0]:
+        row = torch.from_numpy(res.hits[0].astype(np.int64))
+    row = _on_wire(row)
+    dist.broadcast(row, src=owners[0])
+    return row.cpu().numpy().astype(np.uint32)
+
+
+def classify_species_sharded(model, input_file: Path, output_path: Path, step: int = 1,
+                             display_name: bool = False, exclude_ids: list[str] | None = None):
+    """Config 3 (reads sharded over the ranks of the process group), for one
+    FASTA/FASTQ file and a loaded species model (the reference's
+    ``classify_species``, src/xspect/classify.py:43-92, and
+    ``ProbabilisticFilterSVMModel.predict``, probabilistic_filter_svm_model.py:
+    175-223, spread over ranks):
+
+    1. rank r parses only part r of the file (record-aligned byte ranges) and
+       probes it against its bank replica (``predict_columnar``);
+    2. the D+1 counters (per-doc totals, k-mer total) are all-reduced as one
+       int64 tensor on the device (RCCL);
+    3. rank 0 forms the SVM vector from the job's total scores and predicts
+       the label (SVM models), which is broadcast;
+    4. every rank writes its JSON shard (``shard_path``): its own reads' hits,
+       scores and k-mer counts, the job's "total" and prediction.
+
+    ``merge_result_shards`` of the shards equals the single-process JSON.
+    Returns this rank's MatrixResult (a shard)."""
+    import torch
+    from .file_io import FileShard
+    from .probabilistic_filter_model import ProbabilisticFilterModel
+
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    input_file = Path(input_file)
+    res = ProbabilisticFilterModel.predict_columnar(model, FileShard(input_file, rank, world), exclude_ids, step,
+                                                    display_name)
+    D = len(res.labels)
+    local = np.zeros(D + 1, dtype=np.int64)
+    if res.ids:
+        local[:D] = res.hits.sum(axis=0, dtype=np.uint64).astype(np.int64)
+        local[D] = int(res.num_kmers.sum())
+    dev = torch.device("cuda", model.index.info.device) if collective_device().type == "cuda" else None
+    t = torch.from_numpy(local)
+    if dev is not None:
+        t = t.to(dev)
+    allreduce_(t)  # RCCL over xGMI: per-doc totals + k-mer total, one collective
+    tot = t.cpu().numpy()
+    first = _job_first_row(res, D)
+    res.set_job_totals(tot[:D].astype(np.uint64), int(tot[D]), first)
+    if hasattr(model, "_get_svm"):  # ProbabilisticFilterSVMModel: label from the job's totals
+        out = [None]
+        if rank == 0:
+            features = [[v for _, v in sorted(res.get_total_scores().items())]]
+            out[0] = str(model._get_svm(exclude_ids).predict(features)[0])
+        dist.broadcast_object_list(out, src=0)
+        res.prediction = out[0]
+    res.input_source = input_file.name
+    res.save(shard_path(output_path, rank, world))
+    return res
+
+
+def merge_result_shards(paths) -> dict:
+    """The single-process result dict from the JSON shards of a sharded job
+    (in part order): per-read sections concatenated, the job's "total",
+    prediction and fields from the shards (they agree).  Duplicate read ids
+    across shards keep their first position and the last values, as the
+    reference's dictionaries do."""
+    out = None
+    for p in paths:
+        d = json.loads(Path(p).read_text(encoding="utf-8"))
+        if out is None:
+            out = {k: v for k, v in d.items()}
+            out["hits"], out["num_kmers"] = {}, {}
+            out["scores"] = {}
+        total = d["scores"].pop("total")
+        out["hits"].update(d["hits"])
+        out["scores"].update(d["scores"])
+        out["num_kmers"].update(d["num_kmers"])
+        out["scores"]["total"] = total
+    if out is not None:  # "total" is the last key of "scores", as get_scores() builds it
+        out["scores"]["total"] = out["scores"].pop("total")
+    return out

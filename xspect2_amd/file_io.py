@@ -123,15 +123,21 @@ def fastx_format(path: Path) -> int:
 
 
 class FastxReader:
-    """Native multithreaded FASTA/FASTQ reader (xs_fastx_* in xspect_hip.h)."""
+    """Native multithreaded FASTA/FASTQ reader (xs_fastx_* in xspect_hip.h).
 
-    def __init__(self, path: Path, threads: int = 0, pinned: bool = False):
+    ``part``/``parts``: read only part ``part`` of ``parts`` byte ranges of the
+    file, cut at record starts (xs_fastx_open_range): one rank's share of a
+    read-sharded job.  The parts' records in part order are the file's."""
+
+    def __init__(self, path: Path, threads: int = 0, pinned: bool = False, part: int = 0, parts: int = 1):
         self.path = Path(path)
         fmt = fastx_format(self.path)
+        if not 0 <= part < parts:
+            raise ValueError("part must be in [0, parts)")
         self._lib = load()
         h = ctypes.c_void_p()
-        check(self._lib.xs_fastx_open(str(self.path).encode(), fmt, threads,
-                                      XS_FASTX_PINNED if pinned else 0, ctypes.byref(h)))
+        check(self._lib.xs_fastx_open_range(str(self.path).encode(), fmt, threads,
+                                            XS_FASTX_PINNED if pinned else 0, part, parts, ctypes.byref(h)))
         self._h = h
 
     def next_batch(self, max_bytes: int = DEFAULT_BATCH_TEXT) -> SeqBatch:
@@ -169,16 +175,17 @@ class FastxReader:
 
 
 def read_batches(path: Path, max_bytes: int | None = None, threads: int = 0,
-                 pinned: bool = False) -> Iterator[SeqBatch]:
-    """Batches of a FASTA/FASTQ file, parsing batch i+1 while the caller works on
-    batch i (the native reader releases the GIL).  A yielded batch's buffers
-    stay valid until the generator is advanced again.  max_bytes: file text
-    per batch (None: DEFAULT_BATCH_TEXT)."""
+                 pinned: bool = False, part: int = 0, parts: int = 1) -> Iterator[SeqBatch]:
+    """Batches of a FASTA/FASTQ file (or of its part ``part`` of ``parts``),
+    parsing batch i+1 while the caller works on batch i (the native reader
+    releases the GIL).  A yielded batch's buffers stay valid until the
+    generator is advanced again.  max_bytes: file text per batch (None:
+    DEFAULT_BATCH_TEXT)."""
     from concurrent.futures import ThreadPoolExecutor
 
     max_bytes = DEFAULT_BATCH_TEXT if max_bytes is None else max_bytes
 
-    with FastxReader(path, threads, pinned) as rd, ThreadPoolExecutor(1) as pool:
+    with FastxReader(path, threads, pinned, part, parts) as rd, ThreadPoolExecutor(1) as pool:
         fut = pool.submit(rd.next_batch, max_bytes)
         while True:
             b = fut.result()
@@ -187,6 +194,19 @@ def read_batches(path: Path, max_bytes: int | None = None, threads: int = 0,
             # the reader double-buffers: parsing i+1 leaves batch i intact
             fut = pool.submit(rd.next_batch, max_bytes)
             yield b
+
+
+@dataclass(frozen=True)
+class FileShard:
+    """Part ``part`` of ``parts`` of a FASTA/FASTQ file (record-aligned byte
+    ranges): what one rank of a read-sharded job classifies.  Accepted by the
+    models' ``predict_columnar`` / ``predict_matrix`` like a Path."""
+    path: Path
+    part: int = 0
+    parts: int = 1
+
+    def batches(self, max_bytes: int | None = None) -> Iterator[SeqBatch]:
+        return read_batches(self.path, max_bytes, part=self.part, parts=self.parts)
 
 
 def _native_records(path: Path) -> Iterator[Record]:

@@ -19,8 +19,8 @@ import numpy as np
 
 from .bank import Bank, cobs_signature_size
 from ._lib import XS_BANK_COBS_CLASSIC
-from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, check_input_path, get_record_iterator, is_record,
-                      read_batches, seq_text)
+from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, FileShard, check_input_path, get_record_iterator,
+                      is_record, read_batches, seq_text)
 from .packing import PackedReads, pack_sequences
 from .result import MatrixResult, ModelResult
 from .util import default_device, slugify
@@ -197,6 +197,8 @@ class ProbabilisticFilterModel:
             raise ValueError("step must be >= 1")
         if isinstance(sequence_input, Path):
             return self._matrix_file(sequence_input, step)
+        if isinstance(sequence_input, FileShard):
+            return self._matrix_file(sequence_input.path, step, sequence_input.part, sequence_input.parts)
         records = self._collect(sequence_input)
         ids = [r.id for r in records]
         texts = [seq_text(r.seq) for r in records]
@@ -214,16 +216,17 @@ class ProbabilisticFilterModel:
             nk[lo:hi] = n
         return ids, lens, hits, nk
 
-    def _matrix_file(self, path: Path, step: int):
-        """A FASTA/FASTQ file streamed through the native reader: batch i+1 is
-        parsed while batch i is probed, and no per-record objects are built
-        (the reference iterates Bio.SeqIO records, :316-330)."""
+    def _matrix_file(self, path: Path, step: int, part: int = 0, parts: int = 1):
+        """A FASTA/FASTQ file (or its part ``part`` of ``parts``, FileShard)
+        streamed through the native reader: batch i+1 is parsed while batch i
+        is probed, and no per-record objects are built (the reference iterates
+        Bio.SeqIO records, :316-330)."""
         check_input_path(path)
         if self.index is None:
             raise ValueError("The model has not been trained yet")
         ids: list[str] = []
         lens, hits, nks = [], [], []
-        for batch in read_batches(path):
+        for batch in read_batches(path, part=part, parts=parts):
             L = batch.lengths()
             if (L <= self.k).any():
                 raise ValueError("Invalid sequence, must be longer than k")

@@ -120,6 +120,12 @@ class MatrixResult:
     index); ``doc_mask`` drops excluded docs (predict's exclude_ids).
     Duplicate read ids collapse as they do in the reference's dictionaries:
     the first position, the last record's values.
+
+    ``hits`` may be uint8 / uint16 / uint32: a matrix narrowed on the device
+    (counts never exceed a read's k-mer count) is kept narrow, and widened
+    only where a caller reads values.  ``set_job_totals`` makes the result one
+    shard of a read-sharded job: its "total" scores (and get_total_hits) are
+    the whole job's, all-reduced over the ranks (xspect2_amd.distributed).
     """
 
     def __init__(self, model_slug: str, ids: list[str], labels: list[str], hits: np.ndarray,
@@ -127,7 +133,9 @@ class MatrixResult:
                  input_source: str | None = None, doc_mask: np.ndarray | None = None):
         if "total" in ids:
             raise ValueError("'total' is a reserved key and cannot be used as a subsequence")
-        hits = np.ascontiguousarray(hits, dtype=np.uint32)
+        hits = np.ascontiguousarray(hits)
+        if hits.dtype not in (np.uint8, np.uint16, np.uint32):
+            hits = hits.astype(np.uint32)
         num_kmers = np.ascontiguousarray(num_kmers, dtype=np.uint64)
         if hits.ndim != 2 or hits.shape[0] != len(ids) or hits.shape[1] != len(labels) or \
                 num_kmers.shape != (len(ids),):
@@ -147,6 +155,17 @@ class MatrixResult:
         self.input_source = input_source
         self.doc_mask = None if doc_mask is None else np.ascontiguousarray(doc_mask, dtype=np.uint8)
         self.misclassified = None
+        self.job_total_hits: np.ndarray | None = None    # whole-job sums (a shard of a sharded job)
+        self.job_total_kmers: int | None = None
+        self.job_order_row: np.ndarray | None = None     # the job's first hit row (orders "total")
+
+    def set_job_totals(self, total_hits: np.ndarray, total_kmers: int, order_row: np.ndarray) -> None:
+        """Make this result one shard of a read-sharded job: "total" covers the
+        job (per-doc sums and k-mer count over every rank, labels in the COBS
+        order of the job's first read), the per-read sections this shard's reads."""
+        self.job_total_hits = np.ascontiguousarray(total_hits, dtype=np.uint64)
+        self.job_total_kmers = int(total_kmers)
+        self.job_order_row = np.ascontiguousarray(order_row, dtype=np.uint32)
 
     @property
     def docs(self) -> np.ndarray:
@@ -170,14 +189,17 @@ class MatrixResult:
                            self.input_source)
 
     def get_total_hits(self) -> dict[str, int]:
-        if not self.ids:
+        if self.job_total_hits is not None:
+            tot, first = self.job_total_hits, self.job_order_row
+        elif not self.ids:
             raise IndexError("list index out of range")
-        tot = self.hits.sum(axis=0, dtype=np.uint64)
-        return {self.labels[d]: int(tot[d]) for d in cobs_order(self.hits[0], self.docs).tolist()}
+        else:
+            tot, first = self.hits.sum(axis=0, dtype=np.uint64), self.hits[0]
+        return {self.labels[d]: int(tot[d]) for d in cobs_order(first, self.docs).tolist()}
 
     def get_total_scores(self) -> dict[str, float]:
         """get_scores()["total"] without the per-read part."""
-        n_all = int(self.num_kmers.sum())
+        n_all = self.job_total_kmers if self.job_total_hits is not None else int(self.num_kmers.sum())
         return {label: round(v / n_all, 2) for label, v in self.get_total_hits().items()}
 
     def best(self) -> tuple[np.ndarray, np.ndarray]:
@@ -193,9 +215,17 @@ class MatrixResult:
     def save(self, path: Path) -> None:
         """Write the JSON ModelResult.save writes (byte-identical)."""
         path = Path(path)
+        shard = self.job_total_hits is not None
         if self._needs_dicts():
-            return self.to_model_result().save(path)
-        if not self.ids:
+            mr = self.to_model_result()
+            if not shard:
+                return mr.save(path)
+            d = mr.to_dict()
+            d["scores"]["total"] = self.get_total_scores()
+            path.parent.mkdir(exist_ok=True, parents=True)
+            path.write_text(dumps(d, indent=4), encoding="utf-8")
+            return None
+        if not self.ids and not shard:
             raise IndexError("list index out of range")  # get_total_hits on no reads, as the reference
         from ._lib import check, load
         path.parent.mkdir(exist_ok=True, parents=True)
@@ -208,9 +238,11 @@ class MatrixResult:
         mask = self.doc_mask
         vp = ctypes.c_void_p
         check(load().xs_write_result_sections(
-            str(path).encode(), len(self.ids), len(self.labels), vp(self.hits.ctypes.data),
+            str(path).encode(), len(self.ids), len(self.labels), vp(self.hits.ctypes.data), self.hits.itemsize,
             vp(self.num_kmers.ctypes.data), ids_b, vp(ids_off.ctypes.data), lab_b, vp(lab_off.ctypes.data),
-            vp(mask.ctypes.data) if mask is not None else None, 0))
+            vp(mask.ctypes.data) if mask is not None else None,
+            vp(self.job_total_hits.ctypes.data) if shard else None, self.job_total_kmers if shard else 0,
+            vp(self.job_order_row.ctypes.data) if shard else None, 0))
         tail = [("misclassified", self.misclassified), ("input_source", self.input_source)]
         if self.prediction is not None:
             tail.append(("prediction", self.prediction))
