@@ -48,6 +48,12 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBS = 8000.0
+# Infinity-Cache (MALL) ceiling for random row gathers: /opt/skills/guides/MI355X_MICROARCH.md
+# "Indexed rows: gather into LDS", 38 MB table of uniformly random rows: 8.6 TB/s chip-wide
+MALL_PEAK_GBS = 8600.0
+# L2 request ceiling of one XCD's gathers from an L2-resident table, all 8 XCDs:
+# 268 G requests/s whatever the size (4 or 16 B), depth or occupancy (profiles/r02_l2gather.txt)
+L2_GATHER_PEAK_REQ = 268e9
 # BASELINE.json "metric", verbatim (the line reports one N of the 1/2/4/8 curve)
 METRIC = "k-mer\u00d7filter probes/s (150bp reads, ~100-species Bloom bank) at 1/2/4/8 GPUs"
 # Bytes one random row (or filter dword) costs: the gfx950 L2 fills a whole
@@ -61,28 +67,6 @@ SURVEY_ROW_BYTES = 64
 # Rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo
 # collectives through host copies (RCCL does not share a device between ranks).
 SHARE_GPU = os.environ.get("XSPECT_BENCH_SHARE_GPU") == "1"
-
-
-def all_reduce(t, op=None):
-    import torch.distributed as dist
-    op = dist.ReduceOp.SUM if op is None else op
-    if SHARE_GPU:
-        c = t.cpu()
-        dist.all_reduce(c, op=op)
-        t.copy_(c)
-    else:
-        dist.all_reduce(t, op=op)
-
-
-def all_gather(outs, t):
-    import torch.distributed as dist
-    if SHARE_GPU:
-        cs = [o.cpu() for o in outs]
-        dist.all_gather(cs, t.cpu())
-        for o, c in zip(outs, cs):
-            o.copy_(c)
-    else:
-        dist.all_gather(outs, t)
 
 
 def parse():
@@ -191,15 +175,14 @@ class Workload:
         self.nk_read = (args.read_len - self.k + args.step) // args.step
         self.kmers = self.n * self.nk_read
         if w == "multigenus" and world > 1:
-            # hit rows travel in the narrowest type that holds a read's k-mer count
-            # (1 byte for 150 bp reads; distributed.transport_dtype)
-            from xspect2_amd.distributed import transport_dtype
-            self.wire_dtype = transport_dtype(self.nk_read)
-            self.d_narrow = torch.empty((self.n, self.docs[0]), dtype=self.wire_dtype, device=dev)
-            wire = self.d_narrow.view(torch.float16) if self.wire_dtype == torch.int16 else self.d_narrow
-            self.wire = wire
-            self.gathered = [torch.empty_like(wire) for _ in range(world)]
-            self.config["gather_dtype"] = str(self.wire_dtype).replace("torch.", "")
+            # the library's docs-sharded gather (xspect2_amd.distributed): hit rows
+            # travel in the narrowest type that holds a read's k-mer count (1 byte
+            # for 150 bp reads), narrowed and widened on the device; the layout
+            # (docs per rank, wire type) is agreed once, as a serving loop would
+            from xspect2_amd.distributed import doc_shard_layout
+            self.layout = doc_shard_layout(self.docs[0], self.nk_read)
+            self.config["gather_dtype"] = str(self.layout[1]).replace("torch.", "")
+            self.config["gathered_docs"] = sum(self.layout[0])
 
     def _mlst(self, args, dev, s):
         import torch
@@ -250,8 +233,10 @@ class Workload:
         # a locus bank (~97 MB) stays in the 256 MB Infinity Cache: count the
         # row itself (page bytes), not an HBM line fill
         self.row_bytes = page
-        self.roofline_note = ("locus banks (~97 MB each) are Infinity-Cache resident: rows arrive as 128-B "
-                              "line fills from the MALL, not HBM; achieved counts the 64-B rows themselves")
+        self.roofline_note = ("bound = mall: locus banks (~97 MB each) are Infinity-Cache resident, rows arrive "
+                              "as 128-B line fills from the MALL (or hit L2), not HBM; achieved counts the 64-B rows "
+                              "themselves; peak = the guide's random-row gather rate from a 38 MB (Infinity-Cache) "
+                              "table, 8.6 TB/s")
         return reads, {"alleles_per_locus": n_alleles, "page_size": page, "k": self.k,
                        "foreign_read_frac": args.mlst_foreign,
                        "num_hashes": 1, "fpr": 0.001,
@@ -262,12 +247,13 @@ class Workload:
             b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step,
                            None if self.args.totals_only else h, self.d_nk, t, stream=self.stream)
         if self.world > 1:
+            from xspect2_amd import distributed
             if self.args.workload == "multigenus":
-                self.d_narrow.copy_(self.d_hits[0])      # counts <= k-mers per read: lossless
-                all_gather(self.gathered, self.wire)     # docs sharded: hit vectors over xGMI
+                # docs sharded: hit vectors of every rank's bank over xGMI -> [n, sum D_r]
+                self.gathered = distributed.gather_doc_shards(self.d_hits[0], layout=self.layout)
             else:
                 for t in self.d_tot:
-                    all_reduce(t)  # per-doc totals + k-mer total over all ranks
+                    distributed.allreduce_(t)  # per-doc totals + k-mer total over all ranks
 
     def probes_per_step(self):
         per_rank = self.kmers * sum(self.docs)
@@ -325,6 +311,7 @@ def main():
         b.set_profiling(True)
         b.probe_stats()  # reset
         b.probe_rows()
+        b.pass_stats()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -337,8 +324,12 @@ def main():
     elapsed = time.perf_counter() - t0
     launches, probe_ms_total, probe_ms_max = 0, 0.0, 0.0
     rows_read = 0
+    passes = {}
     for b in wl.banks:
         rows_read += b.probe_rows()
+        for name, (ms, cnt) in b.pass_stats().items():
+            t, c = passes.get(name, (0.0, 0))
+            passes[name] = (t + ms, c + cnt)
         b.set_profiling(False)
         n_l, tot_ms, mx = b.probe_stats()
         launches += n_l
@@ -346,8 +337,9 @@ def main():
         probe_ms_max = max(probe_ms_max, mx)
     probe_ms = probe_ms_total / max(1, launches)
     if world > 1:
+        from xspect2_amd.distributed import allreduce_
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        all_reduce(t, op=dist.ReduceOp.MAX)
+        allreduce_(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
     # sanity of the last step: whole-job k-mer totals
@@ -386,6 +378,8 @@ def main():
         wl.rows_per_kmer = rows_read / max(1, launches) / wl.kmers
     algo_bytes = wl.algo_bytes_per_launch()
     achieved = algo_bytes / (probe_ms * 1e-3) / 1e9
+    # MLST locus banks (~97 MB) are Infinity-Cache resident
+    peak = MALL_PEAK_GBS if args.workload == "mlst" else HBM_PEAK_GBS
     traffic = None
     tj = Path(args.traffic_json)
     if tj.exists():
@@ -407,6 +401,23 @@ def main():
                 traffic = tp.get("hbm_bytes_per_step")
         except Exception:
             traffic = None
+    pass_ms = {name: ms / max(1, launches) for name, (ms, cnt) in passes.items() if cnt}
+    lookup_l2 = None
+    if wl.partitioned == "cobs" and "lookup" in pass_ms:
+        # the dominant pass against its own ceiling: L2 requests per launch (PMC,
+        # scaled to this call's k-mers) over the lookup's live HIP-event time
+        try:
+            pmc = json.loads((ROOT / "profiles" / "r02_pmc_cobspart.json").read_text())["kernels"]
+            key = next(k for k in pmc if k.startswith("xs::cobs_lookup_kernel"))
+            req = pmc[key]["TCC_REQ_sum"] * wl.kmers / (1_000_000 * 130)
+            ach = req / (pass_ms["lookup"] * 1e-3)
+            lookup_l2 = {"kernel": key, "bound": "l2_requests", "achieved": ach, "peak": L2_GATHER_PEAK_REQ,
+                         "unit": "req/s", "frac": ach / L2_GATHER_PEAK_REQ, "requests_per_launch": req,
+                         "lookup_ms_avg": pass_ms["lookup"],
+                         "source": "TCC_REQ_sum per dispatch from profiles/r02_pmc_cobspart.json (1 M reads; "
+                                   "scaled by k-mers); peak = pure L2 gathers, profiles/r02_l2gather.txt"}
+        except Exception:
+            lookup_l2 = None
     host = None if args.no_host_path else host_path(wl, args)
 
     cpu = None
@@ -442,9 +453,12 @@ def main():
             "kmers_per_gpu": wl.kmers, "parallelism": par[args.workload], **wl.config,
         },
         "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": wl.kernel,
+            "bound": "mall" if args.workload == "mlst" else "hbm", "achieved": achieved, "peak": peak,
+            "unit": "GB/s", "frac": achieved / peak, "traffic": traffic,
+            "traffic_frac": (traffic / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "kernel": wl.kernel,
             "probe_ms_avg": probe_ms, "probe_ms_max": probe_ms_max, "probe_launches": launches,
+            "pass_ms_avg": pass_ms or None, "lookup_l2": lookup_l2,
             "algo_bytes_per_launch": algo_bytes, "row_bytes": wl.row_bytes, "rows_per_kmer": wl.rows_per_kmer,
             **({"note": wl.roofline_note} if wl.roofline_note else {}),
         },
@@ -465,7 +479,8 @@ def cpu_baseline(wl, args):
     import oracle  # checker + CPU baseline only
     from xspect2_amd.packing import pack_fixed
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    cpus = host_cpus()
+    threads = cpus["share"]
     obanks = []
     for b in wl.banks:
         inf = b.info
@@ -500,12 +515,35 @@ def cpu_baseline(wl, args):
         mism += int(np.count_nonzero(gpu != hits.reshape(gpu.shape)))
         probes += int(nk.sum()) * gpu.shape[1] * passes
     return {
-        "value": probes / dt, "unit": "probes/s", "cores": threads, "kind": "port",
+        "value": probes / dt, "unit": "probes/s", "cores": threads, "kind": "port", "host_cpus": cpus,
         "sample": f"{passes} pass(es) over {m2} of the benchmark reads x {len(obanks)} bank(s) "
-                  f"({probes} probes) in {dt:.1f}s with the C oracle (OpenMP, {threads} threads)",
+                  f"({probes} probes) in {dt:.1f}s with the C oracle (OpenMP, {threads} threads = every CPU "
+                  f"this process may run on: affinity {cpus['affinity']}, cgroup quota {cpus['cgroup_quota']}; "
+                  f"os.cpu_count() {cpus['os_cpu_count']})",
         "parity_sample_mismatches": mism,
         "reference_style": ref_style,
     }
+
+
+def host_cpus() -> dict:
+    """The host CPUs this process can use: os.cpu_count() (the machine),
+    sched_getaffinity (nproc) and the cgroup v2 CPU quota (cpu.max), whose
+    minimum is the share the CPU baseline runs on."""
+    import math
+    total = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except Exception:
+        aff = total
+    quota = None
+    try:
+        q, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = int(q) / int(period)
+    except Exception:
+        quota = None
+    share = min(aff, max(1, math.floor(quota))) if quota else aff
+    return {"os_cpu_count": total, "affinity": aff, "cgroup_quota": quota, "share": share}
 
 
 def host_path(wl, args, reps=3):
@@ -513,11 +551,17 @@ def host_path(wl, args, reps=3):
     in pageable host memory -> H2D -> kernels -> D2H of the n x D hit matrix
     (xs_query), and of the totals only (xs_query_totals).  PCIe-inclusive;
     never the headline value, which starts with the reads in HBM."""
+    from xspect2_amd.bank import max_kmers, narrowest_count_dtype, pinned_empty
     from xspect2_amd.packing import pack_fixed
 
     pr = pack_fixed(wl.reads)
     out = {}
-    for name, fn in (("hits", lambda b: b.query(pr, step=args.step)),
+    # hit matrix in the narrowest exact type (narrowed on the device), into a
+    # pinned output reused call after call, as a serving loop holds it
+    dt = narrowest_count_dtype(max_kmers(pr, wl.k, args.step))
+    outs = {id(b): pinned_empty((pr.n, b.num_docs), dt) for b in wl.banks}
+    for name, fn in (("hits", lambda b: b.query(pr, step=args.step, hit_dtype=dt, out=outs[id(b)])),
+                     ("hits_u32_pageable", lambda b: b.query(pr, step=args.step)),
                      ("totals", lambda b: b.query_totals(pr, step=args.step))):
         for b in wl.banks:  # warm
             fn(b)
@@ -527,8 +571,11 @@ def host_path(wl, args, reps=3):
                 fn(b)
         dt = (time.perf_counter() - t) / reps
         out[name] = {"ms_per_step": dt * 1e3, "probes_per_s": wl.probes_per_step() / wl.world / dt}
-    out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H (hits: n x D uint32 matrix; "
-                   "totals: D+1 counters); the headline value starts with the reads in HBM")
+    out["hit_dtype"] = np.dtype(dt).name
+    out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H.  hits: the n x D matrix in "
+                   f"{np.dtype(dt).name} (narrowed on the device; counts <= k-mers per read) into a reused pinned "
+                   "buffer (xs_query_hits); hits_u32_pageable: xs_query's uint32 matrix into a fresh pageable "
+                   "array; totals: D+1 counters.  The headline value starts with the reads in HBM")
     return out
 
 

@@ -129,6 +129,19 @@ const char* xs_bank_doc_name(const xs_bank* bank, uint64_t i);
 int xs_query(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
              uint32_t* hits_out, uint64_t* num_kmers_out);
 
+/* xs_query with the hit matrix in hit_bytes = 1, 2 or 4 bytes per count
+ * (uint8 / uint16 / uint32).  A count never exceeds its read's sampled k-mers,
+ * so 150 bp reads (130 k-mers) come back in one byte: the matrix is narrowed
+ * on the device and a quarter of the bytes cross PCIe.  Fails with XS_ERR_ARG
+ * if some read has more k-mers than the width holds. */
+int xs_query_hits(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                  void* hits_out, int hit_bytes, uint64_t* num_kmers_out);
+
+/* Pinned (page-locked) host memory for outputs the caller reuses across calls:
+ * results land there by DMA, with no page faults on a fresh pageable buffer. */
+int xs_host_alloc(uint64_t bytes, void** out);
+void xs_host_free(void* p);
+
 /* totals_out[d] = sum over reads of hits[r][d] (D entries, uint64),
  * *total_kmers_out = sum of num_kmers.  No per-read matrix is materialised. */
 int xs_query_totals(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n,
@@ -170,6 +183,25 @@ int xs_gather_reads_device(const void* d_seqs, const uint64_t* d_offsets, const 
 int xs_mlst_sum(xs_bank* bank, const uint32_t* hits, const uint32_t* seq_of_chunk,
                 uint64_t n_chunks, uint64_t n_seqs, uint32_t threshold, uint64_t* scores);
 
+/* One MLST locus in one call (probabilistic_filter_mlst_model.py:192-303; the
+ * reference makes one cobs search per sequence, and per chunk of every
+ * sequence >= 10 kbp, :236-286).  Records [0, n_direct) of seqs/offsets are
+ * sequences probed whole: their hit rows come back in direct_hits
+ * (n_direct x D uint32).  Records [n_direct, n_direct + n_chunks) are the
+ * sequence_splitter chunks (:382-426) of the longer sequences, chunk c owned by
+ * sequence chunk_owner[c] (non-decreasing, < n_owners); their rows stay on
+ * the device, where per (owner, allele) the chunk scores > threshold
+ * (get_cobs_result :377-380) are summed into owner_scores (n_owners x D,
+ * :249-252), owner_first gets the first such chunk (index among the chunks,
+ * UINT32_MAX if none) and owner_first_score its score: the position at which
+ * the reference's all_counts dict first sees the allele, which orders ties of
+ * its stable sort by -score (:254-256).  offsets: n_direct + n_chunks + 1
+ * entries.  Every output may be NULL (owner_first_score needs owner_first). */
+int xs_mlst_query(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n_direct, uint64_t n_chunks,
+                  const uint32_t* chunk_owner, uint64_t n_owners, uint32_t step, uint32_t threshold,
+                  uint32_t* direct_hits, uint64_t* owner_scores, uint32_t* owner_first,
+                  uint32_t* owner_first_score);
+
 /* Record HIP events around the probe kernel of every query on this handle. */
 int xs_bank_set_profiling(xs_bank* bank, int on);
 /* Duration of the probe kernel of the last profiled query, milliseconds. */
@@ -177,6 +209,15 @@ int xs_bank_last_probe_ms(xs_bank* bank, float* ms);
 /* Count, summed and maximum duration of every probe kernel launched since
  * profiling was enabled or the last call of this function (then resets). */
 int xs_bank_probe_stats(xs_bank* bank, uint64_t* count, double* total_ms, float* max_ms);
+
+/* Partitioned probes (xs_bank_probe_path == XS_PATH_PARTITIONED), profiling
+ * on: time spent per pass since the last call (then resets), from HIP events
+ * on the launch stream at the pass boundaries.  ms[4], count[4] indexed by
+ * pass: 0 prep (k-mer counts, scan, block map), 1 bucket (hash, bin by bank
+ * partition, transpose), 2 lookup (per-XCD L2-resident partition gathers),
+ * 3 resolve (AND per k-mer and count; rbloom: resolve + count).  count =
+ * pass instances (one per workspace range). */
+int xs_bank_pass_stats(xs_bank* bank, double* ms, uint64_t* count);
 
 /* rbloom banks: filter words the probe kernels loaded since profiling was
  * enabled or the last call (then resets).  The probe tests 2 bits first and

@@ -46,9 +46,13 @@ class OracleIndex:
     def __init__(self, ob, names):
         self.ob, self.doc_names, self.num_docs, self.info = ob, list(names), len(names), _Info()
 
-    def query(self, packed, step=1):
-        return self.ob.query_packed(np.ascontiguousarray(packed.buf), np.ascontiguousarray(packed.offsets),
-                                    step=step, threads=1)
+    def query(self, packed, step=1, hit_dtype=np.uint32):
+        from xspect2_amd.bank import max_kmers, narrowest_count_dtype
+        h, nk = self.ob.query_packed(np.ascontiguousarray(packed.buf), np.ascontiguousarray(packed.offsets),
+                                     step=step, threads=1)
+        if hit_dtype == "auto":  # as Bank.query: the narrowest exact type
+            hit_dtype = narrowest_count_dtype(max_kmers(packed, self.ob.k, step))
+        return h.astype(hit_dtype), nk
 
 
 def _setup(tmp: Path, n_reads: int, svm: bool):

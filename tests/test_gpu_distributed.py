@@ -1,0 +1,105 @@
+"""The device-resident multi-GPU paths on one MI355X (GPU), in a world-1 RCCL
+process group: the collectives run on device tensors exactly as at N = 8,
+with one participant.  (Multi-rank equality is tested with gloo on the CPU,
+tests/test_distributed_sharded.py, and rehearsed with torchrun on the GPU box
+by tools/gpu/gpu_r03_sharded.sh.)
+
+* config 5: ``docs_sharded_hits_device`` — probe on the device, narrow, RCCL
+  all-gather, widen — equals the bank's hit matrix, for 1-byte and 2-byte
+  transport;
+* config 3: ``classify_species_sharded`` — the byte-range reader, the RCCL
+  all-reduce of D+1 totals on a device tensor, the SVM label — writes the
+  JSON the single-process ``classify_species`` writes.
+"""
+from __future__ import annotations
+
+import json
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+K = 21
+
+
+@pytest.fixture(scope="module")
+def pg():
+    import torch
+    import torch.distributed as dist
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl"
+    yield dist
+    dist.destroy_process_group()
+
+
+def _bank(oracle_mod, D=100, seed=0):
+    from xspect2_amd.bank import Bank
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    docs = [acgt[rng.integers(0, 4, 5000)].tobytes() for _ in range(D)]
+    sig = [oracle_mod.signature_size(5000, 7, 0.01)]
+    ob = oracle_mod.CobsBank.empty(sig, (D + 7) // 8, D, 7, K)
+    ob.build(docs, list(range(D)))
+    gb = Bank.create_cobs(K, 7, sig, D, [f"s{i}" for i in range(D)])
+    gb.upload(ob.rows)
+    return ob, gb, docs
+
+
+@pytest.mark.parametrize("read_len,wire", [(150, "uint8"), (2000, "int16")])
+def test_docs_sharded_gather_on_device(pg, oracle_mod, read_len, wire):
+    import torch
+    from xspect2_amd import distributed
+    from xspect2_amd.packing import pack_sequences
+    ob, gb, docs = _bank(oracle_mod)
+    rng = np.random.default_rng(read_len)
+    reads = [d[o:o + read_len] for d in docs[:60] for o in (0, 1000, 2500)]
+    reads += [np.frombuffer(b"ACGT", dtype=np.uint8)[rng.integers(0, 4, read_len)].tobytes() for _ in range(40)]
+    pr = pack_sequences(reads)
+    dev = torch.device("cuda", 0)
+    d_seq = torch.from_numpy(pr.buf.copy()).to(dev)
+    d_off = torch.from_numpy(pr.offsets.astype(np.int64)).to(dev)
+    hits, nk = distributed.docs_sharded_hits_device(gb, d_seq, pr.nbytes, d_off, pr.n, 1)
+    assert hits.is_cuda and hits.dtype == torch.int32 and tuple(hits.shape) == (pr.n, 100)
+    want, want_n = ob.query(reads)
+    assert np.array_equal(hits.cpu().numpy().view(np.uint32), want)
+    assert np.array_equal(nk.cpu().numpy().view(np.uint64), want_n)
+    dims, dt = distributed.doc_shard_layout(100, int(want_n.max()))
+    assert dims == [100] and str(dt) == f"torch.{wire}"
+    gb.close()
+
+
+def test_classify_species_sharded_world1_equals_classify_species(pg, tmp_path, monkeypatch):
+    from xspect2_amd import classify, distributed
+    from xspect2_amd.file_io import Record, write_fasta
+    from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+    from xspect2_amd.synth import make_genomes, make_reads
+
+    root = tmp_path / "xspect-data"
+    monkeypatch.setenv("XSPECT_DATA", str(root))
+    genomes = make_genomes(5, 40_000, seed=3)
+    for d in range(5):
+        g = genomes[d].tobytes().decode()
+        write_fasta([Record(f"c{d}", g[:30_000])], tmp_path / "sp" / f"GCF_{900 + d:09d}.1_x.fna")
+        for j in range(2):
+            write_fasta([Record("x", g[20_000 + 8000 * j:30_000 + 8000 * j])], tmp_path / "svm" / f"L{d}" / f"a{j}.fasta")
+    model = ProbabilisticFilterSVMModel(K, "Acinetobacter", None, None, "Species", root / "models", "rbf", 1.0)
+    model.fit(tmp_path / "sp", tmp_path / "svm", svm_step=10)
+    model.save()
+    reads, _ = make_reads(genomes, 3000, 150, seed=5)
+    fq = tmp_path / "reads.fq"
+    fq.write_text("".join(f"@r{i}\n{reads[i].tobytes().decode()}\n+\n{'I' * 150}\n" for i in range(3000)))
+    classify.classify_species("Acinetobacter", fq, tmp_path / "single.json", step=2)
+    outs = classify.classify_species_sharded("Acinetobacter", fq, tmp_path / "sharded.json", step=2)
+    assert outs == [tmp_path / "sharded.json"]
+    shard = distributed.shard_path(tmp_path / "sharded.json", 0, 1)
+    want = json.loads((tmp_path / "single.json").read_text())
+    assert distributed.merge_result_shards([shard]) == want
+    assert shard.read_bytes() == (tmp_path / "single.json").read_bytes()  # one shard = the whole file
+    assert want["prediction"].startswith("L")

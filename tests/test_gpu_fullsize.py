@@ -210,3 +210,137 @@ def test_config4_mlst_full_size(oracle_mod):
         got = hits[torch.from_numpy(ids).to(dev)].cpu().numpy().view(np.uint32)
         assert np.array_equal(got, want_h) and np.array_equal(want_n, np.full(ids.size, nk, np.uint64))
         bank.close()
+
+
+def test_config3_per_gpu_shard(data, dev_inputs, oracle_mod, monkeypatch):
+    """BASELINE config 3's per-GPU shard: 12.5 M x 150 bp reads (one eighth of
+    100 M; seed 42 + rank, here rank 0 -> seed 43) against the replicated
+    config-2 bank, in one device call.  The partitioned probe runs it in
+    workspace ranges (the bucket blocks of 1.6e9 k-mers reuse one bounded
+    workspace); the direct probe gives the same 12.5 M x 100 matrix bit for
+    bit, totals equal its column sums, every read has 130 k-mers, and 3,000
+    sampled reads equal the C oracle."""
+    from xspect2_amd import _lib
+    from xspect2_amd.bank import Bank, cobs_signature_size
+    from xspect2_amd.synth import make_reads
+    genomes, _ = data
+    torch, dev, g, g_offs, _, _ = dev_inputs
+    n = 12_500_000
+    reads, _ = make_reads(genomes, n, L, seed=43)
+    r = torch.from_numpy(reads.reshape(-1)).to(dev)
+    r_offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+    h = 7
+    sig = cobs_signature_size(GLEN - K + 1, h, 0.01)
+    bank = Bank.create_cobs(K, h, [sig], D, [f"s{i}" for i in range(D)], device=0)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    bank.build_device(g, genomes.size, g_offs, D, torch.arange(D, dtype=torch.int32, device=dev), stream=s)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+        hits = torch.empty((n, D), dtype=torch.int32, device=dev)
+        nk = torch.empty(n, dtype=torch.int64, device=dev)
+        tot = torch.zeros(D + 1, dtype=torch.int64, device=dev)
+        bank.query_device(r, n * L, r_offs, n, 1, hits, nk, tot, stream=s)
+        torch.cuda.synchronize(dev)
+        out[mode] = (hits, nk, tot, bank.probe_path())
+    (h0, n0, t0, p0), (h1, n1, t1, p1) = out["0"], out["1"]
+    assert p0 == _lib.XS_PATH_GATHER and p1 == _lib.XS_PATH_PARTITIONED
+    assert torch.equal(h0, h1), int((h0 != h1).sum())
+    del h0
+    assert torch.equal(n0, n1) and bool((n1 == NK).all())
+    col = h1.sum(dim=0, dtype=torch.int64)
+    for t in (t0, t1):
+        assert torch.equal(t[:D], col) and int(t[D]) == n * NK
+    assert int(h1.max()) <= NK
+    ob = oracle_mod.CobsBank(bank.download(), [sig], (D + 7) // 8, D, h, K)
+    rng = np.random.default_rng(8)
+    ids = np.unique(np.concatenate([np.arange(1000), np.arange(n - 1000, n), rng.integers(0, n, 1000)]))
+    want_h, want_n = ob.query([reads[i].tobytes() for i in ids])
+    got = h1[torch.from_numpy(ids).to(dev)].cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want_h) and np.array_equal(want_n, np.full(ids.size, NK, np.uint64))
+    bank.close()
+
+
+def _reference_long_path(model, ob_by_locus, text, limit=False):
+    """The reference's long-sequence loop (probabilistic_filter_mlst_model.py:
+    236-271), restated over the C oracle's chunk rows: split, keep scores > 50
+    per chunk in COBS order, add into an insertion-ordered dict, stable sort
+    by -score.  Returns {locus: sorted_counts}."""
+    from collections import defaultdict
+    out = {}
+    for li, (locus, (ob, names)) in enumerate(ob_by_locus.items()):
+        parts = model.sequence_splitter(text, model.avg_locus_bp_size[li])
+        rows, _ = ob.query([p.encode() for p in parts])
+        cobs_results = []
+        for row in rows:
+            keep = np.flatnonzero(row > 50)
+            if keep.size:
+                order = keep[np.argsort(-row[keep].astype(np.int64), kind="stable")]
+                cobs_results.append({names[d]: int(row[d]) for d in order})
+        all_counts = defaultdict(int)
+        for res in cobs_results:
+            for name, value in res.items():
+                all_counts[name] += value
+        out[locus] = dict(sorted(all_counts.items(), key=lambda item: -item[1]))
+    return out
+
+
+def test_config4_mlst_long_contigs(oracle_mod):
+    """Config 4's long-sequence branch at size: 200 contigs of 10-200 kbp
+    (random flanks around alleles of the 7 loci, 1430 alleles each, k = 31),
+    through the model's one-call-per-locus path (xs_mlst_query: every chunk
+    of every contig probed at once, the > 50 sums and the first passing chunk
+    per allele made on the device).  Every contig's per-locus sorted counts,
+    keys in order, equal the reference's loop restated over the C oracle's
+    chunk rows; the alleles share most k-mers, so equal sums (ties, broken by
+    first appearance) are frequent."""
+    torch = pytest.importorskip("torch")
+    from xspect2_amd.bank import Bank, cobs_signature_size
+    from xspect2_amd.probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
+    k, loci, n_alleles, page = 31, 7, 1430, 64
+    rng = np.random.default_rng(777)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    model = ProbabilisticFilterMlstSchemeModel(k, "MLST (Oxford)", __import__("pathlib").Path("."), "", "abaumannii")
+    oracles, all_alleles = {}, []
+    for li in range(loci):
+        base = acgt[rng.integers(0, 4, 620)]
+        alleles = []
+        for _ in range(n_alleles):
+            a = base[:int(rng.integers(400, 601))].copy()
+            pos = rng.integers(0, a.size, int(rng.integers(0, 12)))
+            a[pos] = acgt[(np.searchsorted(acgt, a[pos]) + 1) % 4]
+            alleles.append(a)
+        alleles.sort(key=lambda a: a.size)
+        per = 8 * page
+        sig = [cobs_signature_size(max(a.size for a in alleles[g:g + per]) - k + 1, 1, 0.001)
+               for g in range(0, n_alleles, per)]
+        names = [f"Allele_ID_{i}" for i in range(n_alleles)]
+        bank = Bank.create_cobs(k, 1, sig, n_alleles, names, page_size=page, compact=True, device=0)
+        bank.build([a.tobytes() for a in alleles], np.arange(n_alleles))
+        model.indices.append(bank)
+        model.loci[f"Oxf_L{li}"] = n_alleles
+        model.avg_locus_bp_size.append(int(alleles[int(rng.integers(0, n_alleles))].size))
+        oracles[f"Oxf_L{li}"] = (oracle_mod.CobsBank(bank.download(), sig, page, n_alleles, 1, k), names)
+        all_alleles.append(alleles)
+    contigs = []
+    for c in range(200):
+        L = int(rng.integers(10_000, 200_001))
+        seq = acgt[rng.integers(0, 4, L)]
+        for _ in range(int(rng.integers(0, 4))):  # alleles of random loci inside the flank
+            a = all_alleles[int(rng.integers(0, loci))][int(rng.integers(0, n_alleles))]
+            at = int(rng.integers(0, L - a.size))
+            seq[at:at + a.size] = a
+        contigs.append(seq.tobytes().decode())
+    rows = model._locus_rows(contigs, 1)
+    ties = 0
+    for i, text in enumerate(contigs):
+        want = _reference_long_path(model, oracles, text)
+        for li, locus in enumerate(model.loci):
+            got = model._summed_counts(model.indices[li], rows[li][1][i])
+            assert list(got.items()) == list(want[locus].items()), (i, locus)
+            vals = list(got.values())
+            ties += sum(1 for a, b in zip(vals, vals[1:]) if a == b)
+    assert ties > 0  # the tie order was exercised
+    assert sum(bool(model._summed_counts(model.indices[li], rows[li][1][i])) for i in range(200)
+               for li in range(loci)) > 100
+    model.close()

@@ -814,3 +814,57 @@ def test_host_batches_staged_in_chunks(xs, oracle_mod):
     tot, nk = gb.query_totals(seqs)
     assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
     gb.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "3"])
+def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, monkeypatch, mode):
+    """xs_query_hits: the hit matrix narrowed on the device to uint8 / uint16
+    ("auto" picks the narrowest that holds the batch's largest k-mer count)
+    equals xs_query's uint32 matrix, on both probe paths, into a fresh or a
+    reused pinned buffer (pinned_empty), over several host chunks; a width
+    too narrow for the reads is refused."""
+    from xspect2_amd import _lib
+    from xspect2_amd.bank import pinned_empty
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=4)
+    rng = np.random.default_rng(4)
+    genome = b"".join(seqs)
+    reads = [genome[o:o + 150] for o in rng.integers(0, len(genome) - 150, 60_000)] + [b"", b"ACGT"]
+    want, want_n = ob.query(reads)
+    for dt in (np.uint8, np.uint16, np.uint32, "auto"):
+        got, n = gb.query(reads, hit_dtype=dt)
+        assert got.dtype == (np.uint8 if dt == "auto" else dt)
+        assert np.array_equal(got.astype(np.uint32), want) and np.array_equal(n, want_n)
+    out = pinned_empty((len(reads), 100), np.uint8)
+    for _ in range(2):
+        out[:] = 0xAA
+        got, _ = gb.query(reads, hit_dtype=np.uint8, out=out)
+        assert got is out and np.array_equal(out.astype(np.uint32), want)
+    longr = [genome[:400]]
+    with pytest.raises(_lib.XsError):  # 380 k-mers: counts may not fit a byte
+        gb.query(longr, hit_dtype=np.uint8)
+    got, _ = gb.query(longr, hit_dtype="auto")
+    assert got.dtype == np.uint16 and np.array_equal(got, ob.query(longr)[0])
+    gb.close()
+
+
+def test_pass_stats_of_the_partitioned_probe(xs, oracle_mod, monkeypatch):
+    """xs_bank_pass_stats: with profiling on, the partitioned probe's passes
+    are timed on the launch stream; their sum is within the probe's own time."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
+    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "2")  # several workspace ranges
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)
+    reads = [s[:150] for s in seqs] * 200
+    gb.set_profiling(True)
+    gb.probe_stats()
+    gb.pass_stats()
+    got, _ = gb.query(reads)
+    assert np.array_equal(got, ob.query(reads)[0])
+    n, tot_ms, _ = gb.probe_stats()
+    st = gb.pass_stats()
+    assert set(st) == {"prep", "bucket", "lookup", "resolve"}
+    assert st["lookup"][1] == st["resolve"][1] == st["bucket"][1] >= 2 and st["prep"][1] >= 1
+    assert 0 < sum(ms for ms, _ in st.values()) <= tot_ms * 1.05 + 0.05
+    assert gb.pass_stats()["lookup"] == (0.0, 0)  # reset
+    gb.set_profiling(False)
+    gb.close()

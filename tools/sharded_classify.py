@@ -1,0 +1,100 @@
+"""Config 3 rehearsal: `classify species` sharded over ranks vs one process.
+
+    python tools/sharded_classify.py setup  --root DIR [--reads N]   # model (GPU fit) + reads.fq
+    python tools/sharded_classify.py single --root DIR               # classify_species -> single.json
+    torchrun --nproc-per-node N tools/sharded_classify.py shard --root DIR
+    python tools/sharded_classify.py check  --root DIR --world N     # merged shards == single.json
+
+`shard` runs xspect2_amd.classify.classify_species_sharded: each rank parses
+its byte range of reads.fq, the D+1 totals are all-reduced (RCCL, or gloo
+with XSPECT_SHARE_GPU=1 when the ranks share one GPU), rank 0 forms the SVM
+label, every rank writes its JSON shard.  Each step is its own process.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+GENUS = "Acinetobacter"
+
+
+def setup(root: Path, n_reads: int) -> None:
+    from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+    from xspect2_amd.synth import make_genomes, make_reads
+    from xspect2_amd.file_io import Record, write_fasta
+
+    os.environ["XSPECT_DATA"] = str(root / "xspect-data")
+    genomes = make_genomes(12, 200_000, seed=42)
+    sp = root / "species"
+    svm = root / "svm"
+    for d in range(12):
+        g = genomes[d].tobytes().decode()
+        write_fasta([Record(f"c{d}", g[:150_000])], sp / f"GCF_{470 + 31 * d:09d}.1_genomic.fna", width=80)
+        for j in range(2):
+            write_fasta([Record("x", g[100_000 + 40_000 * j:140_000 + 40_000 * j])],
+                        svm / f"label{d:02d}" / f"acc{d}{j}.fasta")
+    model = ProbabilisticFilterSVMModel(21, GENUS, None, None, "Species", root / "xspect-data" / "models", "rbf", 1.0)
+    model.fit(sp, svm, svm_step=50)
+    model.save()
+    reads, _ = make_reads(genomes, n_reads, 150, seed=43)
+    with open(root / "reads.fq", "w") as fh:
+        for i in range(n_reads):
+            s = reads[i].tobytes().decode()
+            fh.write(f"@read_{i} synthetic\n{s}\n+\n{'I' * len(s)}\n")
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["setup", "single", "shard", "check"])
+    ap.add_argument("--root", required=True)
+    ap.add_argument("--reads", type=int, default=200_000)
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--step", type=int, default=1)
+    a = ap.parse_args()
+    root = Path(a.root).resolve()
+    root.mkdir(parents=True, exist_ok=True)
+    os.environ["XSPECT_DATA"] = str(root / "xspect-data")
+    t0 = time.time()
+    if a.cmd == "setup":
+        setup(root, a.reads)
+    elif a.cmd == "single":
+        from xspect2_amd import classify
+        classify.classify_species(GENUS, root / "reads.fq", root / "single.json", step=a.step)
+    elif a.cmd == "shard":
+        import torch
+        import torch.distributed as dist
+        from xspect2_amd import classify
+        share = os.environ.get("XSPECT_SHARE_GPU") == "1"
+        local = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
+        os.environ["XSPECT2_AMD_DEVICE"] = str(local)
+        torch.cuda.set_device(local)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        classify.classify_species_sharded(GENUS, root / "reads.fq", root / "sharded.json", step=a.step)
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        from xspect2_amd.distributed import merge_result_shards, shard_path
+        want = json.loads((root / "single.json").read_text())
+        shards = [shard_path(root / "sharded.json", r, a.world) for r in range(a.world)]
+        got = merge_result_shards(shards)
+        same = got == want and list(got["hits"]) == list(want["hits"])
+        print(json.dumps({"world": a.world, "reads": len(want["hits"]), "equal": same,
+                          "prediction": [got.get("prediction"), want.get("prediction")],
+                          "reads_per_shard": [len(json.loads(p.read_text())["hits"]) for p in shards],
+                          "total_scores_top3": sorted(want["scores"]["total"].items(), key=lambda x: -x[1])[:3]}))
+        return 0 if same else 1
+    print(f"{a.cmd}: {time.time() - t0:.1f}s", file=sys.stderr)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

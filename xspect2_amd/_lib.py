@@ -98,17 +98,22 @@ SIGNATURES = {
     "xs_bank_signature_sizes": (_int, [_vp, _vp, _u64]),
     "xs_bank_doc_name": (ctypes.c_char_p, [_vp, _u64]),
     "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
+    "xs_query_hits": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _int, _vp]),
+    "xs_host_alloc": (_int, [_u64, _pp]),
+    "xs_host_free": (None, [_vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "xs_query_best": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp, _vp, _vp]),
     "xs_gather_reads_device": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "xs_best_device": (_int, [_vp, _u64, _u64, _vp, _vp, _vp]),
     "xs_mlst_sum": (_int, [_vp, _vp, _vp, _u64, _u64, _u32, _vp]),
+    "xs_mlst_query": (_int, [_vp, _vp, _vp, _u64, _u64, _vp, _u64, _u32, _u32, _vp, _vp, _vp, _vp]),
     "xs_bank_set_profiling": (_int, [_vp, _int]),
     "xs_bank_last_probe_ms": (_int, [_vp, ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_probe_stats": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_float)]),
     "xs_bank_probe_rows": (_int, [_vp, ctypes.POINTER(_u64)]),
+    "xs_bank_pass_stats": (_int, [_vp, _vp, _vp]),
     "xs_bank_probe_path": (_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
     "xs_bank_close": (None, [_vp]),
     "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _int, _vp, ctypes.c_char_p, _vp,

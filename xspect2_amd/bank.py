@@ -41,6 +41,44 @@ def bloom_parameters(expected_items: int, fpr: float) -> tuple[int, int]:
     return (max(size_bits, 1) + 7) // 8, nhash
 
 
+def max_kmers(reads: PackedReads, k: int, step: int) -> int:
+    """Largest sampled k-mer count ceil((len - k + 1) / step) of a batch."""
+    if reads.n == 0:
+        return 0
+    L = int(np.diff(reads.offsets).max())
+    return (L - k) // step + 1 if L >= k else 0
+
+
+def narrowest_count_dtype(max_count: int):
+    """uint8 / uint16 / uint32: the narrowest type that holds counts up to max_count."""
+    return np.uint8 if max_count <= 0xFF else np.uint16 if max_count <= 0xFFFF else np.uint32
+
+
+class _PinnedAlloc:
+    """Page-locked host memory from xs_host_alloc, freed with the last array view."""
+
+    def __init__(self, nbytes: int):
+        p = ctypes.c_void_p()
+        check(load().xs_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (self.ptr, False),
+                                    "version": 3}
+
+    def __del__(self):
+        try:
+            load().xs_host_free(self.ptr)
+        except Exception:  # pragma: no cover - interpreter shutdown order
+            pass
+
+
+def pinned_empty(shape, dtype=np.uint32) -> np.ndarray:
+    """An uninitialised array in pinned host memory (reuse it as ``out=`` of
+    ``Bank.query``: results arrive by DMA, without first-touch page faults)."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    return np.asarray(_PinnedAlloc(max(n, 1)))[:n].view(dtype).reshape(shape)
+
+
 class Bank:
     """One filter bank resident on one GPU."""
 
@@ -170,16 +208,35 @@ class Bank:
         check(load().xs_bank_upload(self.handle, _ptr(p), p.size))
 
     # ------------------------------------------------------------ queries
-    def query(self, reads: PackedReads | Iterable, step: int = 1, want_hits: bool = True):
-        """(hits [n, D] uint32, num_kmers [n] uint64) for host reads."""
+    def query(self, reads: PackedReads | Iterable, step: int = 1, want_hits: bool = True,
+              hit_dtype=np.uint32, out: np.ndarray | None = None):
+        """(hits [n, D], num_kmers [n] uint64) for host reads.
+
+        hit_dtype: np.uint32 (xs_query), np.uint8 / np.uint16 (xs_query_hits:
+        narrowed on the device), or "auto": the narrowest of the three that
+        holds the largest per-read k-mer count of the batch, which bounds every
+        count.  out: a reusable C-contiguous [n, D] array of that dtype (for
+        instance from ``pinned_empty``), filled by DMA without page faults."""
         pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
         if step < 1:
             raise ValueError("step must be >= 1")
         cols = self.num_docs
-        hits = np.empty((pr.n, cols), dtype=np.uint32) if want_hits else None
+        if isinstance(hit_dtype, str) and hit_dtype == "auto":
+            hit_dtype = narrowest_count_dtype(max_kmers(pr, self.term_size, step))
+        hit_dtype = np.dtype(hit_dtype)
+        if hit_dtype not in (np.uint8, np.uint16, np.uint32):
+            raise ValueError("hit_dtype must be uint8, uint16 or uint32")
+        hits = None
+        if want_hits:
+            if out is not None:
+                if out.shape != (pr.n, cols) or out.dtype != hit_dtype or not out.flags.c_contiguous:
+                    raise ValueError(f"out must be a C-contiguous {(pr.n, cols)} {hit_dtype} array")
+                hits = out
+            else:
+                hits = np.empty((pr.n, cols), dtype=hit_dtype)
         nk = np.empty(pr.n, dtype=np.uint64)
-        check(load().xs_query(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
-                              _ptr(hits) if hits is not None else None, _ptr(nk)))
+        check(load().xs_query_hits(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
+                                   _ptr(hits) if hits is not None else None, hit_dtype.itemsize, _ptr(nk)))
         return hits, nk
 
     def query_totals(self, reads: PackedReads | Iterable, step: int = 1):
@@ -219,6 +276,35 @@ class Bank:
         check(load().xs_mlst_sum(self.handle, _ptr(h), _ptr(s), s.size, n_seqs, threshold, _ptr(out)))
         return out
 
+    def mlst_query(self, direct: PackedReads | Iterable, chunks: Iterable, chunk_owner, n_owners: int,
+                   step: int = 1, threshold: int = 50):
+        """One MLST locus in one call (xs_mlst_query): hit rows of the `direct`
+        sequences [n_direct, D] uint32, and for the chunks of the long
+        sequences, per owner: summed scores > threshold [n_owners, D] uint64,
+        first passing chunk [n_owners, D] uint32 (0xFFFFFFFF: none) and its
+        score [n_owners, D] uint32."""
+        if step < 1:
+            raise ValueError("step must be >= 1")
+        dp = direct if isinstance(direct, PackedReads) else pack_sequences(direct)
+        cp = pack_sequences(chunks)
+        owner = np.ascontiguousarray(chunk_owner, dtype=np.uint32)
+        if owner.size != cp.n:
+            raise ValueError("one owner per chunk")
+        if cp.n:
+            buf = np.concatenate([dp.buf[:dp.nbytes], cp.buf])
+            offs = np.concatenate([dp.offsets, cp.offsets[1:] + np.uint64(dp.nbytes)])
+        else:
+            buf, offs = dp.buf, dp.offsets
+        D = self.num_docs
+        hits = np.empty((dp.n, D), dtype=np.uint32)
+        scores = np.empty((n_owners, D), dtype=np.uint64)
+        first = np.empty((n_owners, D), dtype=np.uint32)
+        fscore = np.empty((n_owners, D), dtype=np.uint32)
+        check(load().xs_mlst_query(self.handle, _ptr(buf), _ptr(offs), dp.n, cp.n, _ptr(owner), n_owners, step,
+                                   threshold, _ptr(hits) or None, _ptr(scores) or None, _ptr(first) or None,
+                                   _ptr(fscore) or None))
+        return hits, scores, first, fscore
+
     def set_profiling(self, on: bool = True) -> None:
         check(load().xs_bank_set_profiling(self.handle, 1 if on else 0))
 
@@ -234,6 +320,16 @@ class Bank:
         mx = ctypes.c_float(0.0)
         check(load().xs_bank_probe_stats(self.handle, ctypes.byref(n), ctypes.byref(tot), ctypes.byref(mx)))
         return int(n.value), float(tot.value), float(mx.value)
+
+    PASSES = ("prep", "bucket", "lookup", "resolve")
+
+    def pass_stats(self) -> dict:
+        """Partitioned probes, profiling on: {pass: (total ms, instances)} since
+        the last call (xs_bank_pass_stats; then resets)."""
+        ms = np.zeros(4, dtype=np.float64)
+        cnt = np.zeros(4, dtype=np.uint64)
+        check(load().xs_bank_pass_stats(self.handle, _ptr(ms), _ptr(cnt)))
+        return {name: (float(ms[i]), int(cnt[i])) for i, name in enumerate(self.PASSES)}
 
     def probe_rows(self) -> int:
         """rbloom: filter words loaded by the probes since the last call (profiling on)."""
@@ -293,5 +389,5 @@ def _dptr(x) -> int | None:
     return ptr()
 
 
-__all__ = ["Bank", "bloom_parameters", "cobs_signature_size", "KIND_NAMES",
+__all__ = ["Bank", "bloom_parameters", "cobs_signature_size", "KIND_NAMES", "pinned_empty", "max_kmers",
            "XS_BANK_COBS_CLASSIC", "XS_BANK_COBS_COMPACT", "XS_BANK_RBLOOM", "_lib"]

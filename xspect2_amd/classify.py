@@ -91,6 +91,33 @@ def classify_species(model_genus: str, input_path: Path, output_path: Path, step
         print(f"Saved result as {path_out.name}")
 
 
+def classify_species_sharded(model_genus: str, input_path: Path, output_path: Path, step: int = 1,
+                             display_name: bool = False, exclude_ids: list[str] | None = None):
+    """``classify_species`` over the ranks of an initialised torch.distributed
+    process group (one process per GPU, ``torchrun``; BASELINE config 3):
+    every rank loads the model (its bank on ``LOCAL_RANK``), classifies its
+    byte range of each input file, the D+1 totals are all-reduced over RCCL,
+    rank 0 forms the SVM label, and every rank writes its JSON shard
+    (``distributed.shard_path`` of the reference's output name;
+    ``distributed.merge_result_shards`` gives the single-process JSON)."""
+    from . import distributed
+    from .probabilistic_filter_model import ProbabilisticFilterModel
+    from .probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+
+    path = species_model_path(model_genus)
+    cls = ProbabilisticFilterSVMModel if is_svm_model(path) else ProbabilisticFilterModel
+    model = cls.load(path)
+    inputs, out_path = prepare_input_output_paths(Path(input_path))
+    outs = []
+    for idx, current in enumerate(inputs):
+        target = out_path(idx, Path(output_path))
+        distributed.classify_species_sharded(model, current, target, step=step, display_name=display_name,
+                                             exclude_ids=exclude_ids)
+        outs.append(target)
+    model.close()
+    return outs
+
+
 def classify_mlst(input_path: Path, organism: str, mlst_scheme: str, output_path: Path,
                   limit: bool):
     from .probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel

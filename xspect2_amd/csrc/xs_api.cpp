@@ -154,7 +154,7 @@ struct xs_bank {
     std::mutex mu;
     // workspace
     DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
-        best;
+        best, narrow;
     DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
     DevBuf pk_nkc, pk_kofs, pk_scan, pk_entries, pk_tbl, pk_miss, pk_aux;  // partitioned probes (rbloom, COBS)
     // rbloom path choice: member fraction of the last query whose totals have
@@ -180,10 +180,13 @@ struct xs_bank {
     bool profiling = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> events;  // one pair per profiled probe
     size_t events_used = 0;
+    std::vector<hipEvent_t> pass_ev;  // profiling: pass boundaries of the partitioned probes
+    std::vector<int> pass_tag;
+    size_t pass_used = 0;
 
     xs_bank() {
         for (DevBuf* d : {&seqs, &offs, &nseg, &unit_ofs, &unit_read, &n_units, &scan_tmp, &nk, &hits, &partials,
-                          &totals, &tmp, &best, &rows_read, &pk_nkc, &pk_kofs, &pk_scan, &pk_entries, &pk_tbl,
+                          &totals, &tmp, &best, &narrow, &rows_read, &pk_nkc, &pk_kofs, &pk_scan, &pk_entries, &pk_tbl,
                           &pk_miss, &pk_aux, &bloom_tot}) {
             d->guard_ev = &ws_ev;
             d->guard_used = &ws_used;
@@ -561,7 +564,9 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         const BloomPartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                              b->pk_entries.as<uint64_t>(), b->pk_tbl.as<uint16_t>(), b->pk_miss.as<uint32_t>(),
                              b->pk_aux.as<uint32_t>()};
-        HIPCHK(launch_probe_bloom_part(rv, b->bloom_view(), plan, ws, d_hits, partials, blocks, s));
+        PassRecorder rec{&b->pass_ev, &b->pass_tag, &b->pass_used};
+        HIPCHK(launch_probe_bloom_part(rv, b->bloom_view(), plan, ws, d_hits, partials, blocks, s,
+                                       b->profiling ? &rec : nullptr));
     } else if (b->kind == XS_BANK_RBLOOM) {
         HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, partials, blocks, s));
     } else {
@@ -574,7 +579,8 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
             path = XS_PATH_PARTITIONED;
             const PartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                             b->pk_entries.p, b->pk_tbl.as<uint16_t>(), b->pk_aux.as<uint32_t>()};
-            HIPCHK(launch_probe_cobs_part(rv, cv, cplan, ws, d_hits, partials, blocks, s));
+            PassRecorder rec{&b->pass_ev, &b->pass_tag, &b->pass_used};
+            HIPCHK(launch_probe_cobs_part(rv, cv, cplan, ws, d_hits, partials, blocks, s, b->profiling ? &rec : nullptr));
         } else {
             (void)hipGetLastError();  // a workspace that did not fit: the direct probe
             HIPCHK(launch_probe_cobs(rv, cv, d_hits, partials, blocks, s));
@@ -681,10 +687,12 @@ int host_threads() {
     return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
 }
 
-// hits_host: n x cols rows back on the host (needs d_hits); tot_host: cols + 1
-// entries (per-doc sums, then the k-mer total).
+// hits_host: n x cols rows back on the host (needs d_hits), as hit_bytes-wide
+// counts (4: uint32; 1 / 2: narrowed on the device into b->narrow first, the
+// caller having checked that they fit); tot_host: cols + 1 entries (per-doc
+// sums, then the k-mer total).
 int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
-               uint32_t* d_hits, uint32_t* hits_host, uint64_t* d_nk, uint64_t* tot_host) {
+               uint32_t* d_hits, void* hits_host, uint64_t* d_nk, uint64_t* tot_host, int hit_bytes = 4) {
     const uint64_t base = offsets[0];
     for (uint64_t r = 0; r < n; ++r)
         if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
@@ -714,6 +722,8 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     }
     if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
     if (hits_host && !b->d2h_stream) HIPCHK(hipStreamCreateWithFlags(&b->d2h_stream, hipStreamNonBlocking));
+    if (hits_host && hit_bytes != 4)
+        if (int rc = b->narrow.ensure(n * cols * (uint64_t)hit_bytes + 16)) return rc;
     while (hits_host && b->chunk_ev.size() < nc) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -728,7 +738,10 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     auto drain = [&](size_t j) -> int {  // chunk j's hit rows to the host
         const uint64_t r0 = cut[j], m = cut[j + 1] - cut[j];
         HIPCHK(hipStreamWaitEvent(b->d2h_stream, b->chunk_ev[j], 0));
-        return d2h_pageable(b, hits_host + r0 * cols, d_hits + r0 * cols, m * cols * 4, b->d2h_stream);
+        const uint64_t hb = (uint64_t)hit_bytes;
+        const void* src = hit_bytes == 4 ? static_cast<const void*>(d_hits + r0 * cols)
+                                         : static_cast<const void*>(b->narrow.as<uint8_t>() + r0 * cols * hb);
+        return d2h_pageable(b, static_cast<uint8_t*>(hits_host) + r0 * cols * hb, src, m * cols * hb, b->d2h_stream);
     };
     bool used[2] = {false, false};
     for (size_t i = 0; i < nc; ++i) {
@@ -750,6 +763,9 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
                                tot_host ? b->totals.as<uint64_t>() + i * pcols : nullptr, b->stream))
             return rc;
         if (hits_host) {
+            if (hit_bytes != 4)
+                HIPCHK(launch_narrow_hits(d_hits + r0 * cols, b->narrow.as<uint8_t>() + r0 * cols * hit_bytes,
+                                          (r1 - r0) * cols, hit_bytes, b->stream));
             HIPCHK(hipEventRecord(b->chunk_ev[i], b->stream));
             if (i > 0)
                 if (int rc = drain(i - 1)) return rc;
@@ -1018,9 +1034,22 @@ const char* xs_bank_doc_name(const xs_bank* b, uint64_t i) {
     return b->names[i].c_str();
 }
 
-int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
-             uint32_t* hits_out, uint64_t* num_kmers_out) {
+static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                      void* hits_out, int hit_bytes, uint64_t* num_kmers_out) {
     if (!b || !offsets || (!seqs && n)) return fail(XS_ERR_ARG, "null argument");
+    if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
+    if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
+    if (hits_out && hit_bytes != 4) {
+        // a count never exceeds its read's sampled k-mers: they must fit the width
+        const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
+        for (uint64_t r = 0; r < n; ++r) {
+            const uint64_t len = offsets[r + 1] >= offsets[r] ? offsets[r + 1] - offsets[r] : 0;
+            const uint64_t nk = len >= b->k ? (len - b->k) / step + 1 : 0;
+            if (nk > cap)
+                return fail(XS_ERR_ARG, "read %llu has %llu sampled k-mers: counts may not fit %d byte(s)",
+                            (unsigned long long)r, (unsigned long long)nk, hit_bytes);
+        }
+    }
     std::lock_guard<std::mutex> lk(b->mu);
     HIPCHK(hipSetDevice(b->device));
     if (n == 0) return XS_OK;
@@ -1035,10 +1064,35 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
         if (int rc = b->nk.ensure(n * 8)) return rc;
         d_nk = b->nk.as<uint64_t>();
     }
-    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, hits_out, d_nk, nullptr)) return rc;
+    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, hits_out, d_nk, nullptr, hit_bytes)) return rc;
     if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
+}
+
+int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+             uint32_t* hits_out, uint64_t* num_kmers_out) {
+    return query_impl(b, seqs, offsets, n, step, hits_out, 4, num_kmers_out);
+}
+
+int xs_query_hits(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                  void* hits_out, int hit_bytes, uint64_t* num_kmers_out) {
+    return query_impl(b, seqs, offsets, n, step, hits_out, hit_bytes, num_kmers_out);
+}
+
+int xs_host_alloc(uint64_t bytes, void** out) {
+    if (!out) return fail(XS_ERR_ARG, "null argument");
+    *out = nullptr;
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(XS_ERR_HIP, "hipHostMalloc(%llu) failed: %s", (unsigned long long)bytes, hipGetErrorString(e));
+    }
+    return XS_OK;
+}
+
+void xs_host_free(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
@@ -1144,8 +1198,60 @@ int xs_mlst_sum(xs_bank* b, const uint32_t* hits, const uint32_t* seq_of_chunk, 
     }
     HIPCHK(hipMemsetAsync(b->totals.p, 0, n_seqs * D * 8, b->stream));
     HIPCHK(launch_mlst_sum(b->hits.as<uint32_t>(), b->tmp.as<uint32_t>(), n_chunks, D, threshold,
-                           b->totals.as<unsigned long long>(), b->stream));
+                           b->totals.as<unsigned long long>(), nullptr, nullptr, b->stream));
     HIPCHK(hipMemcpyAsync(scores, b->totals.p, n_seqs * D * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+int xs_mlst_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n_direct, uint64_t n_chunks,
+                  const uint32_t* chunk_owner, uint64_t n_owners, uint32_t step, uint32_t threshold,
+                  uint32_t* direct_hits, uint64_t* owner_scores, uint32_t* owner_first,
+                  uint32_t* owner_first_score) {
+    const uint64_t n = n_direct + n_chunks;
+    if (!b || !offsets || (!seqs && n) || (n_chunks && !chunk_owner)) return fail(XS_ERR_ARG, "null argument");
+    if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "MLST queries need a COBS bank");
+    if (owner_first_score && !owner_first) return fail(XS_ERR_ARG, "owner_first_score needs owner_first");
+    for (uint64_t c = 0; c < n_chunks; ++c)
+        if (chunk_owner[c] >= n_owners || (c && chunk_owner[c] < chunk_owner[c - 1]))
+            return fail(XS_ERR_ARG, "chunk_owner must be non-decreasing and < n_owners (chunk %llu)",
+                        (unsigned long long)c);
+    if (n_chunks >= (1ull << 32) - 1) return fail(XS_ERR_ARG, "at most 2^32-2 chunks per call");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t D = b->D, od = n_owners * D;
+    if (n_owners) {
+        if (owner_scores) memset(owner_scores, 0, od * 8);
+        if (owner_first) memset(owner_first, 0xFF, od * 4);
+        if (owner_first_score) memset(owner_first_score, 0, od * 4);
+    }
+    if (n == 0) return XS_OK;
+    if (int rc = ws_enter(b, b->stream)) return rc;
+    if (int rc = b->hits.ensure(n * D * 4)) return rc;
+    uint32_t* d_hits = b->hits.as<uint32_t>();
+    // every record probed in one pass; only the direct rows cross to the host
+    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, nullptr, nullptr)) return rc;
+    if (n_direct && direct_hits)
+        if (int rc = d2h_pageable(b, direct_hits, d_hits, n_direct * D * 4, b->stream)) return rc;
+    if (n_chunks && n_owners) {
+        if (int rc = ws_enter(b, b->stream)) return rc;
+        if (int rc = b->tmp.ensure(n_chunks * 4)) return rc;
+        if (int rc = b->totals.ensure(od * 8)) return rc;
+        if (int rc = b->best.ensure(od * 8)) return rc;
+        uint32_t* d_first = b->best.as<uint32_t>();
+        uint32_t* d_fscore = d_first + od;
+        HIPCHK(hipMemcpyAsync(b->tmp.p, chunk_owner, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(hipMemsetAsync(b->totals.p, 0, od * 8, b->stream));
+        HIPCHK(hipMemsetAsync(d_first, 0xFF, od * 4, b->stream));
+        HIPCHK(hipMemsetAsync(d_fscore, 0, od * 4, b->stream));
+        HIPCHK(launch_mlst_sum(d_hits + n_direct * D, b->tmp.as<uint32_t>(), n_chunks, D, threshold,
+                               b->totals.as<unsigned long long>(), d_first, d_fscore, b->stream));
+        if (owner_scores) HIPCHK(hipMemcpyAsync(owner_scores, b->totals.p, od * 8, hipMemcpyDeviceToHost, b->stream));
+        if (owner_first) HIPCHK(hipMemcpyAsync(owner_first, d_first, od * 4, hipMemcpyDeviceToHost, b->stream));
+        if (owner_first_score)
+            HIPCHK(hipMemcpyAsync(owner_first_score, d_fscore, od * 4, hipMemcpyDeviceToHost, b->stream));
+        if (int rc = ws_leave(b, b->stream)) return rc;
+    }
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
 }
@@ -1213,6 +1319,27 @@ int xs_bank_probe_stats(xs_bank* b, uint64_t* count, double* total_ms, float* ma
     return XS_OK;
 }
 
+int xs_bank_pass_stats(xs_bank* b, double* ms, uint64_t* count) {
+    if (!b || !ms || !count) return fail(XS_ERR_ARG, "null argument");
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    for (int t = 0; t < kPassTags; ++t) {
+        ms[t] = 0.0;
+        count[t] = 0;
+    }
+    for (size_t i = 1; i < b->pass_used; ++i) {
+        const int t = b->pass_tag[i];
+        if (t < 0 || t >= kPassTags) continue;  // a query's opening mark
+        float x = 0.0f;
+        HIPCHK(hipEventSynchronize(b->pass_ev[i]));
+        HIPCHK(hipEventElapsedTime(&x, b->pass_ev[i - 1], b->pass_ev[i]));
+        ms[t] += x;
+        ++count[t];
+    }
+    b->pass_used = 0;
+    return XS_OK;
+}
+
 void xs_bank_close(xs_bank* b) {
     if (!b) return;
     (void)hipSetDevice(b->device);
@@ -1231,6 +1358,7 @@ void xs_bank_close(xs_bank* b) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
+    for (auto& ev : b->pass_ev) (void)hipEventDestroy(ev);
     for (hipStream_t st : {b->stream, b->copy_stream, b->d2h_stream})
         if (st) (void)hipStreamDestroy(st);
     delete b;  // DevBuf destructors free device memory

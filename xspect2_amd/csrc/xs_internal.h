@@ -2,6 +2,8 @@
 // gfx950 kernels (xs_kernels.hip).  Not part of the public ABI.
 #pragma once
 #include <hip/hip_runtime.h>
+
+#include <vector>
 #include <stdint.h>
 
 namespace xs {
@@ -81,6 +83,30 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
                              uint64_t* partials, int blocks, hipStream_t s);
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
                               uint64_t* partials, int blocks, hipStream_t s);
+// Profiling of the partitioned probes: an event recorded on the launch stream
+// at each pass boundary, tagged with the pass that just ended (kPassStart opens
+// a query).  xs_bank_pass_stats sums the gaps per pass.
+enum PassTag { kPassStart = -1, kPassPrep = 0, kPassBucket = 1, kPassLookup = 2, kPassResolve = 3, kPassTags = 4 };
+struct PassRecorder {
+    std::vector<hipEvent_t>* pool;
+    std::vector<int>* tags;
+    size_t* used;
+    hipError_t mark(int tag, hipStream_t s) {
+        if (*used == pool->size()) {
+            hipEvent_t e;
+            hipError_t err = hipEventCreate(&e);
+            if (err != hipSuccess) return err;
+            pool->push_back(e);
+            tags->push_back(0);
+        }
+        (*tags)[*used] = tag;
+        return hipEventRecord((*pool)[(*used)++], s);
+    }
+};
+inline void pass_mark(PassRecorder* r, int tag, hipStream_t s) {
+    if (r) (void)r->mark(tag, s);
+}
+
 // Partitioned rbloom probe (xs_probe_bloompart.hip): k-mers per bucket block,
 // most hash functions it takes, most filter partitions.
 constexpr int kPartKmers = 1024;
@@ -112,7 +138,7 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
                      BloomPartPlan* plan);
 hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,
                                    const BloomPartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
-                                   hipStream_t s);
+                                   hipStream_t s, PassRecorder* rec = nullptr);
 // Partitioned COBS probe (xs_probe_cobspart.hip) for classic banks of <= 128
 // docs (16-B rows) larger than the Infinity Cache.
 constexpr uint32_t kCobsPartWsMiB = 24 << 10;  // default cap of a range's entries + rows
@@ -149,7 +175,7 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
                     CobsPartPlan* plan);
 hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const CobsPartPlan& plan,
                                   const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
-                                  hipStream_t s);
+                                  hipStream_t s, PassRecorder* rec = nullptr);
 hipError_t launch_reduce_partials(const uint64_t* partials, int blocks, uint64_t cols,
                                   uint64_t* totals, hipStream_t s);
 hipError_t launch_build_cobs(const ReadView& rv, const uint32_t* rec_doc, const CobsView& bv,
@@ -158,9 +184,12 @@ hipError_t launch_build_bloom(const ReadView& rv, const BloomView& bv, uint32_t*
                               int blocks, hipStream_t s);
 hipError_t launch_repack(const uint8_t* src, uint64_t src_pitch, uint8_t* dst, uint64_t dst_pitch,
                          uint64_t rows, uint64_t copy_bytes, hipStream_t s);
+// Sum of hits[c][d] > threshold into scores[seq_of_chunk[c]][d]; with `first`
+// (pre-filled with UINT32_MAX) also the first such chunk, and with first_score
+// that chunk's count.
 hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, uint64_t n_chunks,
                            uint64_t D, uint32_t threshold, unsigned long long* scores,
-                           hipStream_t s);
+                           uint32_t* first, uint32_t* first_score, hipStream_t s);
 
 // Host-side constants shared with the kernels.
 inline uint64_t barrett_magic(uint64_t d) { return d ? (~0ull) / d : 0; }
@@ -169,6 +198,9 @@ inline uint64_t barrett_magic(uint64_t d) { return d ? (~0ull) / d : 0; }
 constexpr uint32_t kBestAmbiguous = 0xFFFFFFFFu;
 hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_t* best,
                            uint32_t* best_hits, hipStream_t s);
+
+// dst[i] = src[i] as uint8 (hit_bytes 1) or uint16 (2); the caller guarantees the values fit.
+hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s);
 
 hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
                                uint8_t* out, const uint64_t* out_offs, hipStream_t s);

@@ -263,15 +263,64 @@ __global__ void repack_kernel(const uint8_t* __restrict__ src, uint64_t src_pitc
 
 __global__ void mlst_sum_kernel(const uint32_t* __restrict__ hits,
                                 const uint32_t* __restrict__ seq_of_chunk, uint64_t n_chunks,
-                                uint64_t D, uint32_t threshold, unsigned long long* scores) {
+                                uint64_t D, uint32_t threshold, unsigned long long* scores,
+                                uint32_t* __restrict__ first) {
     const uint64_t total = n_chunks * D;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t v = hits[i];
         if (v > threshold) {
             const uint64_t c = i / D, d = i - c * D;
-            atomicAdd(&scores[(uint64_t)seq_of_chunk[c] * D + d], (unsigned long long)v);
+            const uint64_t o = (uint64_t)seq_of_chunk[c] * D + d;
+            atomicAdd(&scores[o], (unsigned long long)v);
+            if (first) atomicMin(&first[o], (uint32_t)c);
         }
+    }
+}
+
+// The score of each (sequence, allele) in its first passing chunk (after
+// mlst_sum_kernel has found that chunk): with the chunk index it gives the
+// position at which the reference's all_counts dict first saw the allele.
+__global__ void mlst_first_score_kernel(const uint32_t* __restrict__ hits,
+                                        const uint32_t* __restrict__ seq_of_chunk, uint64_t n_chunks,
+                                        uint64_t D, uint32_t threshold, const uint32_t* __restrict__ first,
+                                        uint32_t* __restrict__ first_score) {
+    const uint64_t total = n_chunks * D;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = hits[i];
+        if (v > threshold) {
+            const uint64_t c = i / D, d = i - c * D;
+            const uint64_t o = (uint64_t)seq_of_chunk[c] * D + d;
+            if (first[o] == (uint32_t)c) first_score[o] = v;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ narrow hit rows
+// Hit counts never exceed a read's k-mer count, so a host that wants the
+// matrix back gets it in 1 or 2 bytes per (read, doc) when every read of the
+// call has at most 255 / 65535 sampled k-mers: a quarter (half) of the PCIe
+// bytes and of the host memory the caller has to touch.  Four counts per
+// thread: one 16-B load, one 4- or 8-B store.
+template <class T>
+__global__ void narrow_hits_kernel(const uint32_t* __restrict__ src, T* __restrict__ dst, uint64_t n) {
+    const uint64_t n4 = n / 4;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+    const bool vec = reinterpret_cast<uintptr_t>(src) % 16 == 0 && reinterpret_cast<uintptr_t>(dst) % (4 * sizeof(T)) == 0;
+    if (vec) {
+        for (uint64_t i = t0; i < n4; i += stride) {
+            const uint4 v = reinterpret_cast<const uint4*>(src)[i];
+            if constexpr (sizeof(T) == 1) {
+                reinterpret_cast<uint32_t*>(dst)[i] = v.x | (v.y << 8) | (v.z << 16) | (v.w << 24);
+            } else {
+                reinterpret_cast<uint2*>(dst)[i] = make_uint2(v.x | (v.y << 16), v.z | (v.w << 16));
+            }
+        }
+        for (uint64_t i = n4 * 4 + t0; i < n; i += stride) dst[i] = (T)src[i];
+    } else {
+        for (uint64_t i = t0; i < n; i += stride) dst[i] = (T)src[i];
     }
 }
 
@@ -469,10 +518,20 @@ hipError_t launch_repack(const uint8_t* src, uint64_t src_pitch, uint8_t* dst, u
 
 hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, uint64_t n_chunks,
                            uint64_t D, uint32_t threshold, unsigned long long* scores,
-                           hipStream_t s) {
+                           uint32_t* first, uint32_t* first_score, hipStream_t s) {
     if (n_chunks == 0 || D == 0) return hipSuccess;
-    mlst_sum_kernel<<<grid_for(n_chunks * D, 256, 4096), 256, 0, s>>>(hits, seq_of_chunk, n_chunks,
-                                                                      D, threshold, scores);
+    const unsigned g = grid_for(n_chunks * D, 256, 4096);
+    mlst_sum_kernel<<<g, 256, 0, s>>>(hits, seq_of_chunk, n_chunks, D, threshold, scores, first);
+    if (first && first_score)
+        mlst_first_score_kernel<<<g, 256, 0, s>>>(hits, seq_of_chunk, n_chunks, D, threshold, first, first_score);
+    return hipGetLastError();
+}
+
+hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = grid_for((n + 3) / 4, 256, 8192);
+    if (hit_bytes == 1) narrow_hits_kernel<uint8_t><<<g, 256, 0, s>>>(src, static_cast<uint8_t*>(dst), n);
+    else narrow_hits_kernel<uint16_t><<<g, 256, 0, s>>>(src, static_cast<uint16_t*>(dst), n);
     return hipGetLastError();
 }
 

@@ -415,7 +415,8 @@ static int lookup_grid() {
 
 hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,
                                    const BloomPartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
-                                   hipStream_t s) {
+                                   hipStream_t s, PassRecorder* rec) {
+    pass_mark(rec, kPassStart, s);
     part_counts_kernel<<<grid_for(rv.n + 1, 256, 4096), 256, 0, s>>>(rv.offs, rv.n, rv.k, rv.step, ws.nkc);
     size_t sb = ws.scan_bytes;
     hipError_t e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, sb, ws.nkc, ws.kofs, (int)(rv.n + 1), s);
@@ -428,6 +429,7 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
     uint32_t* blk_read = ws.aux;
     uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.tstride;  // block-major copy
     part_map_kernel<<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
+    pass_mark(rec, kPassPrep, s);
     if (rv.k == 21 && bv.K == 7)
         bloom_bucket_kernel<21, 7><<<(unsigned)plan.tstride, kBucketThreads, 0, s>>>(
             rv, bv, ws.kofs, plan.shift, plan.P, plan.tstride, eoff, eid, tbm, blk_read);
@@ -438,10 +440,13 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
         tbm, plan.P + 1, plan.tstride, ws.tbl, 0, plan.tstride);
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
+    pass_mark(rec, kPassBucket, s);
     bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
                                                                 plan.tstride, eoff, ws.tbl, emiss, qctr);
+    pass_mark(rec, kPassLookup, s);
     bloom_resolve_kernel<<<(unsigned)plan.tstride, 256, 0, s>>>(ws.kofs, rv.n, bv.K, eid, emiss, ws.miss);
     bloom_count_kernel<<<blocks, 256, 0, s>>>(rv, ws.kofs, ws.miss, bv.K, hits, partials, bv.rows_read);
+    pass_mark(rec, kPassResolve, s);
     return hipGetLastError();
 }
 

@@ -593,7 +593,7 @@ static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t
 template <int CK>
 static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uint32_t H, const CobsPartPlan& plan,
                                      const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
-                                     hipStream_t s) {
+                                     hipStream_t s, PassRecorder* rec) {
     hipError_t e;
     const uint64_t ne = plan.rblk * plan.stride;
     uint32_t* ent = reinterpret_cast<uint32_t*>(ws.entries);
@@ -602,6 +602,7 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
     uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.rblk;  // block-major copy
     uint32_t* qctr = ws.aux + (plan.nblk + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
+    pass_mark(rec, kPassPrep, s);
     const bool emb = pb.D <= emb_max_docs<CK>();
     // lookup: 0 (default) LDS-DMA row gathers of 6 entries per lane, one gather in
     // flight per wave at a time, 2 workgroups per CU; 1 register gathers, 8 in
@@ -623,6 +624,7 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
         part_transpose_kernel<<<dim3((nb + 63) / 64, (plan.P + 1 + 63) / 64), 256, 0, s>>>(
             tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
         if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
+        pass_mark(rec, kPassBucket, s);
         switch (var) {
             case 1: lookup_launch<8, CK, 0>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             case 2: lookup_launch<6, CK, 2>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
@@ -630,6 +632,7 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             case 4: lookup_launch<6, CK, 4>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             default: lookup_launch<6, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
+        pass_mark(rec, kPassLookup, s);
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
                 rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0, plan.stride, tbm,
@@ -638,13 +641,15 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             cobs_resolve_kernel<false, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
                 rv, ws.kofs, H, pb.D, pb.nwords, ent, rowv, blk_read, hits, partials, blocks, b0, plan.stride, tbm,
                 plan.P + 1);
+        pass_mark(rec, kPassResolve, s);
     }
     return hipGetLastError();
 }
 
 hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const CobsPartPlan& plan,
                                   const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
-                                  hipStream_t s) {
+                                  hipStream_t s, PassRecorder* rec) {
+    pass_mark(rec, kPassStart, s);
     PartBank pb;
     pb.rows = reinterpret_cast<const uint4*>(bv.rows);
     pb.sig = bv.sig0;
@@ -659,9 +664,9 @@ hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const 
     size_t sb = ws.scan_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, sb, ws.nkc, ws.kofs, (int)(rv.n + 1), s)) != hipSuccess)
         return e;
-    if (plan.ck == 4096) return cobs_part_pipeline<4096>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
-    if (plan.ck == 2048) return cobs_part_pipeline<2048>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
-    return cobs_part_pipeline<1024>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s);
+    if (plan.ck == 4096) return cobs_part_pipeline<4096>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
+    if (plan.ck == 2048) return cobs_part_pipeline<2048>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
+    return cobs_part_pipeline<1024>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
 }
 
 }  // namespace xs

@@ -128,26 +128,43 @@ def transport_dtype(max_count: int):
     return torch.int32
 
 
-def gather_doc_shards(hits, max_count: int):
+def doc_shard_layout(d_local: int, max_count: int):
+    """(docs of every rank, transport dtype) of a docs-sharded gather: one
+    small all-gather of (D_r, largest per-read k-mer count).  It depends only
+    on the banks and the reads' length class, so a serving loop computes it
+    once and passes it to every ``gather_doc_shards``."""
+    import torch
+    dist = _dist()
+    world = dist.get_world_size()
+    meta = torch.tensor([int(d_local), int(max_count)], dtype=torch.int64)
+    allmeta = [torch.zeros(2, dtype=torch.int64, device=collective_device()) for _ in range(world)]
+    dist.all_gather(allmeta, _on_wire(meta))
+    dims = [int(m[0].item()) for m in allmeta]
+    return dims, transport_dtype(max(int(m[1].item()) for m in allmeta))
+
+
+def gather_doc_shards(hits, max_count: int | None = None, layout=None):
     """All-gather per-rank hit columns [n, D_r] (any integer tensor, any
     device) into [n, sum(D_r)] int32 in rank order, on the tensor's device.
 
     The rows travel in ``transport_dtype`` of the largest per-read k-mer count
-    on any rank (one all-reduce agrees on it), padded to the widest D_r; the
+    on any rank, padded to the widest D_r (``layout`` from
+    ``doc_shard_layout``, agreed by one small all-gather when not given); the
     narrowing and widening run where the tensor is (on the GPU for the
     device-resident path)."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
     n, d_local = hits.shape
-    meta = torch.tensor([d_local, int(max_count)], dtype=torch.int64)
-    allmeta = [torch.zeros(2, dtype=torch.int64, device=collective_device()) for _ in range(world)]
-    dist.all_gather(allmeta, _on_wire(meta))
-    dims = [int(m[0].item()) for m in allmeta]
-    dt = transport_dtype(max(int(m[1].item()) for m in allmeta))
+    dims, dt = layout if layout is not None else doc_shard_layout(d_local, max_count)
+    if dims[dist.get_rank()] != d_local:
+        raise ValueError("layout does not match this rank's hit columns")
     d_max = max(dims)
-    pad = torch.zeros((n, d_max), dtype=dt, device=hits.device)
-    pad[:, :d_local] = hits.to(dt)  # lossless: counts <= k-mers per read <= max_count
+    pad = torch.zeros((n, d_max), dtype=dt, device=hits.device) if d_local < d_max else None
+    if pad is None:
+        pad = hits.to(dt)  # lossless: counts <= k-mers per read <= max_count
+    else:
+        pad[:, :d_local] = hits.to(dt)
     # gloo and RCCL gather no int16: 2-byte rows travel as float16 bit patterns
     # (an all-gather copies bits, it does no arithmetic)
     wire = _on_wire(pad.view(torch.float16) if dt == torch.int16 else pad)
@@ -157,8 +174,8 @@ def gather_doc_shards(hits, max_count: int):
     for p, d in zip(parts, dims):
         if dt == torch.int16:
             p = p.view(torch.int16)
-        cols.append(p.to(hits.device)[:, :d].to(torch.int32))
-    return torch.cat(cols, dim=1)
+        cols.append(p.to(hits.device)[:, :d])
+    return torch.cat(cols, dim=1).to(torch.int32)
 
 
 def docs_sharded_hits(reads: PackedReads, step: int,

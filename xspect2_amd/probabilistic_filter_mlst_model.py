@@ -7,14 +7,15 @@ first result is the top allele (``:272-286``); longer ones are split by
 ``sequence_splitter`` (``:382-426``), each chunk keeps alleles scoring > 50
 (``get_cobs_result`` ``:362-380``), kept scores are summed per allele and
 stably sorted by -score (``:248-256``).  What changes: every chunk of every
-record of a locus is probed in one batched GPU call instead of one COBS call
-per chunk.  The PubMLST strain-type POST (``:295-302``) is network I/O and is
+record of a locus (and every short record) is probed in one batched GPU call
+(xs_mlst_query) instead of one COBS call per chunk, and the > 50 chunk sums
+are made on the device.  The PubMLST strain-type POST (``:295-302``) is network I/O and is
 delegated to ``strain_type_resolver``.
 """
 from __future__ import annotations
 
 import json
-from collections import defaultdict, namedtuple
+from collections import namedtuple
 from pathlib import Path
 
 import numpy as np
@@ -183,22 +184,41 @@ class ProbabilisticFilterMlstSchemeModel(ProbabilisticFilterModel):
 
     # ------------------------------------------------------------ queries
     def _locus_rows(self, texts: list[str], step: int):
-        """Per locus: hit rows of every short text, and per long text the chunk rows."""
+        """Per locus, one C-ABI call (xs_mlst_query) for every text: the hit
+        row of each text shorter than 10 kbp, and for each longer text the
+        per-allele sums of its chunk scores > 50 with the first chunk (and its
+        score) that passed, computed on the device from chunk rows that never
+        leave it."""
         short = [i for i, t in enumerate(texts) if len(t) < LONG_SEQUENCE]
         long_ = [i for i, t in enumerate(texts) if len(t) >= LONG_SEQUENCE]
+        packed_short = pack_sequences([texts[i] for i in short])
         out = []
         for li, bank in enumerate(self.indices):
-            rows_short = {}
-            if short:
-                h, _ = bank.query(pack_sequences([texts[i] for i in short]), step=step)
-                rows_short = {i: h[j] for j, i in enumerate(short)}
-            rows_long = {}
-            for i in long_:
+            chunks, owner = [], []
+            for j, i in enumerate(long_):
                 parts = self.sequence_splitter(texts[i], self.avg_locus_bp_size[li])
-                h, _ = bank.query(pack_sequences(parts), step=step)
-                rows_long[i] = h
+                chunks += parts
+                owner += [j] * len(parts)
+            h, sc, first, fs = bank.mlst_query(packed_short, chunks, owner, len(long_), step,
+                                               CHUNK_KMER_THRESHOLD)
+            rows_short = {i: h[j] for j, i in enumerate(short)}
+            rows_long = {i: (sc[j], first[j], fs[j]) for j, i in enumerate(long_)}
             out.append((rows_short, rows_long))
         return out
+
+    def _summed_counts(self, bank: Bank, summed) -> dict:
+        """The reference's ``sorted_counts`` of one long text at one locus
+        (:237-256): per allele the sum of its chunk scores > 50, ordered by
+        -sum with ties in the order the alleles entered ``all_counts``, i.e.
+        by first passing chunk, then by rank in that chunk's COBS order
+        (score descending, doc index)."""
+        scores, first, fscore = summed
+        names = bank.doc_names
+        present = np.flatnonzero(scores > 0)  # kept in some chunk (> 50 there)
+        keys = (present, -fscore[present].astype(np.int64), first[present].astype(np.int64),
+                -scores[present].astype(np.int64))
+        order = present[np.lexsort(keys)]
+        return {names[d]: int(scores[d]) for d in order}
 
     def _assemble(self, i: int, text: str, locus_rows, limit: bool, limit_number: int) -> list:
         scheme_loci = list(self.loci.keys())
@@ -206,18 +226,7 @@ class ProbabilisticFilterMlstSchemeModel(ProbabilisticFilterModel):
         highest_results: dict = {}
         if len(text) >= LONG_SEQUENCE:
             for li, bank in enumerate(self.indices):
-                chunk_rows = locus_rows[li][1][i]
-                cobs_results = []
-                for row in chunk_rows:
-                    keep = np.flatnonzero(row > CHUNK_KMER_THRESHOLD)
-                    split_result = self.get_cobs_result(self._ordered(bank, row, keep), True)
-                    if split_result:
-                        cobs_results.append(split_result)
-                all_counts = defaultdict(int)
-                for res in cobs_results:
-                    for name, value in res.items():
-                        all_counts[name] += value
-                sorted_counts = dict(sorted(all_counts.items(), key=lambda item: -item[1]))
+                sorted_counts = self._summed_counts(bank, locus_rows[li][1][i])
                 if limit:
                     sorted_counts = dict(list(sorted_counts.items())[:limit_number])
                 if not sorted_counts:

@@ -163,9 +163,11 @@ class ProbabilisticFilterModel:
 
     # ------------------------------------------------------------ queries
     def _query(self, packed: PackedReads, step: int):
+        """(hits, num_kmers) of one batch; the hit matrix comes back in the
+        narrowest integer type that holds the batch's largest k-mer count."""
         if self.index is None:
             raise ValueError("The model has not been trained yet")
-        return self.index.query(packed, step=step)
+        return self.index.query(packed, step=step, hit_dtype="auto")
 
     def _hit_dict(self, row: np.ndarray, exclude_ids) -> dict:
         names = self.index.doc_names
@@ -185,7 +187,9 @@ class ProbabilisticFilterModel:
         return self._hit_dict(hits[0], exclude_ids)
 
     def predict_matrix(self, sequence_input, step: int = 1):
-        """Columnar result of a batch: (ids, hits [n, D] uint32, num_kmers [n] uint64).
+        """Columnar result of a batch: (ids, hits [n, D], num_kmers [n] uint64);
+        hits are uint8 / uint16 / uint32, the narrowest type the reads' k-mer
+        counts need.
 
         Same hits as ``predict`` without per-read dictionaries (the form that
         scales to 10^8 reads)."""
@@ -208,13 +212,8 @@ class ProbabilisticFilterModel:
                 raise ValueError("Invalid sequence, must be longer than k")
         if self.index is None:
             raise ValueError("The model has not been trained yet")
-        hits = np.zeros((len(texts), self.index.num_docs), dtype=np.uint32)
-        nk = np.zeros(len(texts), dtype=np.uint64)
-        for lo, hi in _batches(lens):
-            h, n = self._query(pack_sequences(texts[lo:hi]), step)
-            hits[lo:hi] = h
-            nk[lo:hi] = n
-        return ids, lens, hits, nk
+        parts = [self._query(pack_sequences(texts[lo:hi]), step) for lo, hi in _batches(lens)]
+        return ids, lens, *_stack(parts, self.index.num_docs)
 
     def _matrix_file(self, path: Path, step: int, part: int = 0, parts: int = 1):
         """A FASTA/FASTQ file (or its part ``part`` of ``parts``, FileShard)
@@ -235,9 +234,7 @@ class ProbabilisticFilterModel:
             lens.append(L)
             hits.append(h)
             nks.append(n)
-        D = self.index.num_docs
-        hits_m = np.concatenate(hits) if hits else np.zeros((0, D), dtype=np.uint32)
-        nk = np.concatenate(nks) if nks else np.zeros(0, dtype=np.uint64)
+        hits_m, nk = _stack(list(zip(hits, nks)), self.index.num_docs)
         lens_l = np.concatenate(lens).tolist() if lens else []
         return ids, lens_l, hits_m, nk
 
@@ -336,6 +333,17 @@ class ProbabilisticFilterModel:
         if self.index is not None:
             self.index.close()
             self.index = None
+
+
+def _stack(parts: list, D: int) -> tuple[np.ndarray, np.ndarray]:
+    """Hit rows and k-mer counts of consecutive batches as one matrix (no copy
+    for a single batch; batches of different widths widen to the widest)."""
+    if not parts:
+        return np.zeros((0, D), dtype=np.uint8), np.zeros(0, dtype=np.uint64)
+    if len(parts) == 1:
+        return parts[0]
+    dt = max((h.dtype for h, _ in parts), key=lambda t: t.itemsize)
+    return np.concatenate([h.astype(dt, copy=False) for h, _ in parts]), np.concatenate([n for _, n in parts])
 
 
 def _batches(lens: list[int]) -> Iterable[tuple[int, int]]:
