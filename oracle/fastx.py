@@ -97,3 +97,57 @@ def parse_fastq(data: bytes) -> list[tuple[bytes, bytes]]:
 def parse_file(path: Path) -> list[tuple[bytes, bytes]]:
     data = Path(path).read_bytes()
     return parse_fastq(data) if Path(path).suffix[1:] in ("fastq", "fq") else parse_fasta(data)
+
+
+def parse_titles(path: Path) -> list[bytes]:
+    """Record titles (header line minus '>' / '@', right-stripped), in file
+    order: SeqRecord.description as Bio.SeqIO.parse sets it."""
+    data = Path(path).read_bytes()
+    fastq = Path(path).suffix[1:] in ("fastq", "fq")
+    out = []
+    if not fastq:
+        for line in data.split(b"\n"):
+            if line.startswith(b">"):
+                out.append(_rstrip(line[1:]))
+        return out
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    i, n = 0, len(lines)
+    while i < n:  # well-formed input: the same walk as parse_fastq
+        if _rstrip(lines[i]) == b"":
+            i += 1
+            continue
+        out.append(_rstrip(lines[i][1:]))
+        i += 1
+        s = 0
+        while i < n and not lines[i].startswith(b"+"):
+            s += len(_rstrip(lines[i]))
+            i += 1
+        i += 1
+        q = 0
+        while q < s and i < n:
+            q += len(_rstrip(lines[i]))
+            i += 1
+    return out
+
+
+def write_fasta_bio(records, path: Path, width: int = 60, append: bool = False) -> None:
+    """Bio.SeqIO.write(record, handle, "fasta") restated (FastaWriter): the
+    title is the description when its first token is the id, else
+    "id description", else the id; then the sequence in lines of `width`
+    characters (none for an empty sequence).  records: (id, description, seq)
+    bytes triples."""
+    with open(path, "ab" if append else "wb") as fh:
+        for rid, desc, seq in records:
+            rid = rid.replace(b"\n", b" ").replace(b"\r", b" ")
+            desc = desc.replace(b"\n", b" ").replace(b"\r", b" ")
+            if desc and desc.split(None, 1)[0] == rid:
+                title = desc
+            elif desc:
+                title = rid + b" " + desc
+            else:
+                title = rid
+            fh.write(b">" + title + b"\n")
+            for i in range(0, len(seq), width):
+                fh.write(seq[i:i + width] + b"\n")

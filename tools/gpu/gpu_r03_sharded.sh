@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 F=gpurun_out/r03s; mkdir -p $F
 echo "== gpu tests"
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
-  tests/test_gpu_distributed.py tests/test_gpu_fullsize.py tests/test_gpu_models.py \
-  -k "docs_sharded or sharded or config3 or long_contigs or mlst" > $F/tests.log 2>&1 || { tail -60 $F/tests.log; exit 12; }
+  tests/test_gpu_distributed.py tests/test_gpu_fullsize.py tests/test_gpu_models.py tests/test_gpu_parity.py tests/test_pipeline.py \
+  -k "docs_sharded or sharded or config3 or long_contigs or mlst or narrow or pass_stats or oracle" > $F/tests.log 2>&1 || { tail -60 $F/tests.log; exit 12; }
 grep -E "PASS|FAIL|passed|failed" $F/tests.log | tail
 echo "== all gpu tests"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests > $F/all.log 2>&1 || { tail -60 $F/all.log; exit 18; }
@@ -25,3 +25,6 @@ cat $F/check.json; cat $F/single.log $F/shard.log | grep -E "s$|Saved" | tail -4
 echo "== bench: config 3 per-GPU shard (12.5 M reads)"
 timeout -k 10 900 python -u bench.py --reads 12500000 --steps 5 --warmup 2 --no-host-path > $F/bench_c3.json 2> $F/bench_c3.err || { tail -30 $F/bench_c3.err; exit 17; }
 cut -c1-400 $F/bench_c3.json
+echo "== bench: default (config 2) with the host path"
+timeout -k 10 600 python -u bench.py > $F/bench_c2.json 2> $F/bench_c2.err || { tail -30 $F/bench_c2.err; exit 19; }
+cut -c1-600 $F/bench_c2.json
