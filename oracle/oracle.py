@@ -323,3 +323,50 @@ def num_threads() -> int:
 
 if __name__ == "__main__":  # pragma: no cover
     print(build(), os.cpu_count())
+
+
+# ---------------------------------------------------------------- file layouts (spec)
+def cobs_classic_file(names: list[str], k: int, h: int, sig: int, rows: np.ndarray) -> bytes:
+    """COBS classic index file as restated (UNVERIFIED, from recollection of
+    cobs-reloaded): "COBS:CLASSIC_INDEX", u32 version 1, u32 num_docs, u32
+    term_size, u8 canonicalize = 1, u64 signature_size, u64 num_hashes, the
+    doc names each ending in '\\n', "CLASSIC_INDEX", then the S x ceil(D/8)
+    row-major payload (doc d = byte d >> 3, bit d & 7)."""
+    import struct
+    head = b"COBS:CLASSIC_INDEX" + struct.pack("<IIIBQQ", 1, len(names), k, 1, sig, h)
+    head += b"".join(n.encode() + b"\n" for n in names) + b"CLASSIC_INDEX"
+    return head + np.ascontiguousarray(rows, dtype=np.uint8).tobytes()
+
+
+def cobs_compact_file(names: list[str], k: int, h: int, sig: list[int], page: int, rows: np.ndarray) -> bytes:
+    """COBS compact index file as restated (UNVERIFIED): "COBS:COMPACT_INDEX",
+    u32 version 1, u32 term_size, u8 canonicalize = 1, u64 num_groups, per group
+    (u64 signature_size, u64 num_hashes), u64 page_size, u32 num_docs, names,
+    "COMPACT_INDEX", zero padding to a multiple of page_size, then each group's
+    signature_size rows of page_size bytes."""
+    import struct
+    head = b"COBS:COMPACT_INDEX" + struct.pack("<IIBQ", 1, k, 1, len(sig))
+    head += b"".join(struct.pack("<QQ", s, h) for s in sig) + struct.pack("<QI", page, len(names))
+    head += b"".join(n.encode() + b"\n" for n in names) + b"COMPACT_INDEX"
+    head += b"\0" * ((page - len(head) % page) % page)
+    return head + np.ascontiguousarray(rows, dtype=np.uint8).tobytes()
+
+
+def rbloom_file(num_hashes: int, bits: np.ndarray) -> bytes:
+    """rbloom filter file as restated (UNVERIFIED): u64 little-endian K, then
+    the filter bytes (bit i = byte i >> 3, bit i & 7)."""
+    import struct
+    return struct.pack("<Q", num_hashes) + np.ascontiguousarray(bits, dtype=np.uint8).tobytes()
+
+
+def bloom_indexes_py(hash64: int, nhash: int, mbits: int) -> list[int]:
+    """rbloom's K bit indices as restated (UNVERIFIED): a 128-bit LCG
+    state <- state * M + C mod 2^128 from state = the XXH3-64 hash, index =
+    (state >> 64) mod m, K times (Python big integers)."""
+    M = (0x2360ED051FC65DA4 << 64) | 0x4385DF649FCCF645
+    C = (0x5851F42D4C957F2D << 64) | 0x14057B7EF767814F
+    st, out = hash64, []
+    for _ in range(nhash):
+        st = (st * M + C) % (1 << 128)
+        out.append((st >> 64) % mbits)
+    return out

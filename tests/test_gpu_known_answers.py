@@ -162,3 +162,40 @@ def test_mlst_cpn60_allele4(tmp_path, ka, oracle_mod):
     got, gnk = bank.query([seq])
     assert np.array_equal(got, want) and int(gnk[0]) == 401
     assert int(want[0][bank.doc_names.index("Allele_ID_4")]) == 401
+
+
+def test_saved_files_follow_the_spec_layouts(tmp_path, oracle_mod):
+    """The files the library writes (xs_bank_save) are byte-identical to the
+    spec writers of the unverified layouts (oracle.cobs_classic_file,
+    cobs_compact_file, rbloom_file), and read back."""
+    from xspect2_amd.bank import Bank, bloom_parameters
+    from xspect2_amd._lib import XS_BANK_COBS_CLASSIC, XS_BANK_COBS_COMPACT, XS_BANK_RBLOOM
+    rng = np.random.default_rng(9)
+    seqs = [_random(rng, int(rng.integers(200, 900))) for _ in range(20)]
+    names = [f"GCF_{i:09d}" for i in range(10)]
+    gb = Bank.create_cobs(21, 7, [3001], 10, names)
+    gb.build(seqs, [i % 10 for i in range(20)])
+    gb.save(tmp_path / "c.cobs_classic")
+    assert (tmp_path / "c.cobs_classic").read_bytes() == oracle_mod.cobs_classic_file(names, 21, 7, 3001,
+                                                                                      gb.download())
+    gb.close()
+    anames = [f"Allele_ID_{i}" for i in range(20)]
+    cb = Bank.create_cobs(31, 1, [1500, 2100, 900], 20, anames, page_size=1, compact=True)
+    cb.build(seqs, list(range(20)))
+    cb.save(tmp_path / "l.cobs_compact")
+    assert (tmp_path / "l.cobs_compact").read_bytes() == oracle_mod.cobs_compact_file(anames, 31, 1, [1500, 2100, 900],
+                                                                                      1, cb.download())
+    cb2 = Bank.open(tmp_path / "l.cobs_compact", XS_BANK_COBS_COMPACT)
+    assert cb2.doc_names == anames and np.array_equal(cb2.download(), cb.download())
+    cb.close()
+    cb2.close()
+    nbytes, K = bloom_parameters(5000, 0.01)
+    bb = Bank.create_bloom(21, nbytes, K)
+    bb.build(seqs)
+    bb.save(tmp_path / "filter.bloom")
+    assert (tmp_path / "filter.bloom").read_bytes() == oracle_mod.rbloom_file(K, bb.download())
+    bb2 = Bank.open(tmp_path / "filter.bloom", XS_BANK_RBLOOM, term_size=21)
+    assert np.array_equal(bb2.download(), bb.download())
+    bb.close()
+    bb2.close()
+    assert XS_BANK_COBS_CLASSIC == 0
