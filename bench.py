@@ -424,10 +424,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(wl, args)
 
-    names = {"species": "config2: 1M x 150bp reads/GPU vs D=100 COBS classic species bank",
-             "genus": "genus path: 1M x 150bp reads/GPU vs rbloom filter over 100 genomes",
-             "mlst": "config4: 1M x 150bp reads/GPU vs 7 loci x 1430 alleles (COBS compact)",
-             "multigenus": "config5: 1M x 150bp reads vs one 100-species bank per GPU, hits all-gathered"}
+    nr = f"{wl.n / 1e6:g}M x {args.read_len}bp reads"
+    species_cfg = ("config3 per-GPU shard (100M reads / 8 GPUs)" if wl.n == 12_500_000 else
+                   "config2" if wl.n == 1_000_000 else "species")
+    names = {"species": f"{species_cfg}: {nr}/GPU vs D={args.docs} COBS classic species bank",
+             "genus": f"genus path: {nr}/GPU vs rbloom filter over {args.docs} genomes",
+             "mlst": f"config4: {nr}/GPU vs 7 loci x 1430 alleles (COBS compact)",
+             "multigenus": f"config5: {nr} vs one {args.docs}-species bank per GPU, hits all-gathered"}
     par = {"species": f"reads sharded x{world}, bank replicated, RCCL all-reduce of D+1 totals",
            "genus": f"reads sharded x{world}, filter replicated, RCCL all-reduce of totals",
            "mlst": f"reads sharded x{world}, loci banks replicated, RCCL all-reduce of totals",
@@ -558,9 +561,9 @@ def host_path(wl, args, reps=3):
     out = {}
     # hit matrix in the narrowest exact type (narrowed on the device), into a
     # pinned output reused call after call, as a serving loop holds it
-    dt = narrowest_count_dtype(max_kmers(pr, wl.k, args.step))
-    outs = {id(b): pinned_empty((pr.n, b.num_docs), dt) for b in wl.banks}
-    for name, fn in (("hits", lambda b: b.query(pr, step=args.step, hit_dtype=dt, out=outs[id(b)])),
+    hdt = narrowest_count_dtype(max_kmers(pr, wl.k, args.step))
+    outs = {id(b): pinned_empty((pr.n, b.num_docs), hdt) for b in wl.banks}
+    for name, fn in (("hits", lambda b: b.query(pr, step=args.step, hit_dtype=hdt, out=outs[id(b)])),
                      ("hits_u32_pageable", lambda b: b.query(pr, step=args.step)),
                      ("totals", lambda b: b.query_totals(pr, step=args.step))):
         for b in wl.banks:  # warm
@@ -571,9 +574,9 @@ def host_path(wl, args, reps=3):
                 fn(b)
         dt = (time.perf_counter() - t) / reps
         out[name] = {"ms_per_step": dt * 1e3, "probes_per_s": wl.probes_per_step() / wl.world / dt}
-    out["hit_dtype"] = np.dtype(dt).name
+    out["hit_dtype"] = np.dtype(hdt).name
     out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H.  hits: the n x D matrix in "
-                   f"{np.dtype(dt).name} (narrowed on the device; counts <= k-mers per read) into a reused pinned "
+                   f"{np.dtype(hdt).name} (narrowed on the device; counts <= k-mers per read) into a reused pinned "
                    "buffer (xs_query_hits); hits_u32_pageable: xs_query's uint32 matrix into a fresh pageable "
                    "array; totals: D+1 counters.  The headline value starts with the reads in HBM")
     return out

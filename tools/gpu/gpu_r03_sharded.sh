@@ -8,8 +8,8 @@ export TMPDIR=/tmp
 F=gpurun_out/r03s; mkdir -p $F
 echo "== gpu tests"
 timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu \
-  tests/test_gpu_distributed.py tests/test_gpu_fullsize.py tests/test_gpu_models.py tests/test_gpu_parity.py tests/test_pipeline.py \
-  -k "docs_sharded or sharded or config3 or long_contigs or mlst or narrow or pass_stats or equals_oracle" > $F/tests.log 2>&1 || { tail -60 $F/tests.log; exit 12; }
+  tests/test_gpu_distributed.py tests/test_gpu_fullsize.py tests/test_gpu_models.py tests/test_gpu_parity.py tests/test_pipeline.py tests/test_gpu_known_answers.py \
+  -k "docs_sharded or sharded or config3 or long_contigs or mlst or narrow or pass_stats or equals_oracle or spec_layouts or known" > $F/tests.log 2>&1 || { tail -60 $F/tests.log; exit 12; }
 grep -E "PASS|FAIL|passed|failed" $F/tests.log | tail
 echo "== all gpu tests"
 timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread -m gpu tests > $F/all.log 2>&1 || { tail -60 $F/all.log; exit 18; }
