@@ -194,3 +194,51 @@ def test_multigenus_docs_sharded_over_100_docs(tmp_path, world):
         o = np.load(tmp_path / f"g{r}.npz")
         assert np.array_equal(o["hits"], want1)
         assert np.array_equal(o["step2"], want2)
+
+
+def _docs_worker(rank: int, world: int, port: int, tmp: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        banks, reads = _genera(oracle, world)
+        m = ProbabilisticFilterModel(K, f"Genus{rank}", None, None, "Species", Path(tmp) / "m")
+        names = [f"g{rank}_sp{d}" for d in range(banks[rank].D)]
+        m.index = OracleIndex(banks[rank], names)
+        res = distributed.predict_docs_sharded(m, Path(tmp) / "reads.fasta")
+        if rank == 0:
+            res.save(Path(tmp) / "docs_sharded.json")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_predict_docs_sharded_multigenus(tmp_path):
+    """Config 5 as a library call: three genus models of 40-50 species (> 100
+    docs) on three ranks, one FASTA of reads from all of them; the gathered
+    result (labels in rank order) equals one process probing the three banks
+    and concatenating the columns."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    from xspect2_amd.result import MatrixResult
+
+    world = 3
+    banks, reads = _genera(oracle, world)
+    with open(tmp_path / "reads.fasta", "wb") as fh:
+        for i, r in enumerate(reads):
+            fh.write(b">r%d\n%s\n" % (i, r))
+    mp.spawn(_docs_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    hits = np.concatenate([b.query(reads)[0] for b in banks], axis=1)
+    nk = banks[0].query(reads)[1]
+    labels = [f"g{g}_sp{d}" for g in range(world) for d in range(banks[g].D)]
+    want = MatrixResult("multi-genus-docs-sharded", [f"r{i}" for i in range(len(reads))], labels, hits, nk)
+    want.input_source = "reads.fasta"
+    want.save(tmp_path / "want.json")
+    assert len(labels) > 100
+    assert (tmp_path / "docs_sharded.json").read_bytes() == (tmp_path / "want.json").read_bytes()

@@ -103,3 +103,22 @@ def test_classify_species_sharded_world1_equals_classify_species(pg, tmp_path, m
     assert distributed.merge_result_shards([shard]) == want
     assert shard.read_bytes() == (tmp_path / "single.json").read_bytes()  # one shard = the whole file
     assert want["prediction"].startswith("L")
+
+
+def test_predict_docs_sharded_world1_on_device(pg, tmp_path, oracle_mod):
+    """Config 5's library call through the device path (RCCL, world 1):
+    equals the model's own columnar prediction."""
+    import numpy as np
+    from xspect2_amd import distributed
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    ob, gb, docs = _bank(oracle_mod, D=100, seed=3)
+    m = ProbabilisticFilterModel(K, "Genus", None, None, "Species", tmp_path)
+    m.index = gb
+    fa = tmp_path / "r.fasta"
+    fa.write_text("".join(f">r{i}\n{d[o:o + 150].decode()}\n" for i, d in enumerate(docs) for o in (0, 3000)))
+    res = distributed.predict_docs_sharded(m, fa)
+    want = m.predict_columnar(fa)
+    assert res.ids == want.ids and res.labels == want.labels
+    assert np.array_equal(res.hits.astype(np.uint32), want.hits.astype(np.uint32))
+    assert np.array_equal(res.num_kmers, want.num_kmers)
+    gb.close()

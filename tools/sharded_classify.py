@@ -5,6 +5,12 @@
     torchrun --nproc-per-node N tools/sharded_classify.py shard --root DIR
     python tools/sharded_classify.py check  --root DIR --world N     # merged shards == single.json
 
+Config 5 (docs sharded; one genus model per rank, every read on every rank):
+    python tools/sharded_classify.py docs-setup  --root DIR [--reads N]  # 2 genus models of 60 species + reads
+    python tools/sharded_classify.py docs-single --root DIR              # both models in one process
+    torchrun --nproc-per-node 2 tools/sharded_classify.py docs-shard --root DIR
+    python tools/sharded_classify.py docs-check  --root DIR
+
 `shard` runs xspect2_amd.classify.classify_species_sharded: each rank parses
 its byte range of reads.fq, the D+1 totals are all-reduced (RCCL, or gloo
 with XSPECT_SHARE_GPU=1 when the ranks share one GPU), rank 0 forms the SVM
@@ -22,6 +28,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 GENUS = "Acinetobacter"
+GENERA = ["Acinetobacter", "Pseudomonas"]
 
 
 def setup(root: Path, n_reads: int) -> None:
@@ -49,9 +56,33 @@ def setup(root: Path, n_reads: int) -> None:
             fh.write(f"@read_{i} synthetic\n{s}\n+\n{'I' * len(s)}\n")
 
 
+def docs_setup(root: Path, n_reads: int) -> None:
+    """Two genus species models of 60 species each (fit on the GPU) and reads from all 120 genomes."""
+    import numpy as np
+    from xspect2_amd.file_io import Record, write_fasta
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+    from xspect2_amd.synth import make_genomes, make_reads
+
+    allg = []
+    for gi, genus in enumerate(GENERA):
+        genomes = make_genomes(60, 100_000, seed=100 + gi)
+        allg.append(genomes)
+        sp = root / f"species_{genus}"
+        for d in range(60):
+            write_fasta([Record(f"c{d}", genomes[d].tobytes().decode())], sp / f"GCF_{1000 * (gi + 1) + d:09d}.fna")
+        model = ProbabilisticFilterModel(21, genus, None, None, "Species", root / "xspect-data" / "models")
+        model.fit(sp)
+        model.save()
+    reads, _ = make_reads(np.concatenate(allg), n_reads, 150, seed=44)
+    with open(root / "docs_reads.fasta", "w") as fh:
+        for i in range(n_reads):
+            fh.write(f">dread_{i}\n{reads[i].tobytes().decode()}\n")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("cmd", choices=["setup", "single", "shard", "check"])
+    ap.add_argument("cmd", choices=["setup", "single", "shard", "check", "docs-setup", "docs-single", "docs-shard",
+                                    "docs-check"])
     ap.add_argument("--root", required=True)
     ap.add_argument("--reads", type=int, default=200_000)
     ap.add_argument("--world", type=int, default=2)
@@ -81,6 +112,46 @@ def main() -> int:
         classify.classify_species_sharded(GENUS, root / "reads.fq", root / "sharded.json", step=a.step)
         dist.barrier()
         dist.destroy_process_group()
+    elif a.cmd == "docs-setup":
+        docs_setup(root, a.reads)
+    elif a.cmd == "docs-single":
+        import numpy as np
+        from xspect2_amd import classify
+        from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+        from xspect2_amd.result import MatrixResult
+        parts = [ProbabilisticFilterModel.load(classify.species_model_path(g)).predict_columnar(
+            root / "docs_reads.fasta", step=a.step) for g in GENERA]
+        hits = np.concatenate([p.hits.astype(np.uint32) for p in parts], axis=1)
+        res = MatrixResult("multi-genus-docs-sharded", parts[0].ids, [lab for p in parts for lab in p.labels], hits,
+                           parts[0].num_kmers, sparse_sampling_step=a.step)
+        res.input_source = "docs_reads.fasta"
+        res.save(root / "docs_single.json")
+    elif a.cmd == "docs-shard":
+        import torch
+        import torch.distributed as dist
+        from xspect2_amd import classify, distributed
+        from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+        share = os.environ.get("XSPECT_SHARE_GPU") == "1"
+        local = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
+        os.environ["XSPECT2_AMD_DEVICE"] = str(local)
+        torch.cuda.set_device(local)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        model = ProbabilisticFilterModel.load(classify.species_model_path(GENERA[dist.get_rank()]))
+        res = distributed.predict_docs_sharded(model, root / "docs_reads.fasta", step=a.step)
+        if dist.get_rank() == 0:
+            res.save(root / "docs_sharded.json")
+        dist.barrier()
+        dist.destroy_process_group()
+    elif a.cmd == "docs-check":
+        a_ = (root / "docs_single.json").read_bytes()
+        b_ = (root / "docs_sharded.json").read_bytes()
+        d = json.loads(a_)
+        print(json.dumps({"docs": len(d["scores"]["total"]), "reads": len(d["hits"]), "equal_bytes": a_ == b_,
+                          "json_bytes": len(a_)}))
+        return 0 if a_ == b_ else 1
     else:
         from xspect2_amd.distributed import merge_result_shards, shard_path
         want = json.loads((root / "single.json").read_text())

@@ -335,3 +335,64 @@ def merge_result_shards(paths) -> dict:
     if out is not None:  # "total" is the last key of "scores", as get_scores() builds it
         out["scores"]["total"] = out["scores"].pop("total")
     return out
+
+
+# ---------------------------------------------------------------- config 5: docs-sharded classify
+def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: bool = False):
+    """Config 5 (docs sharded): every rank holds a different species model (one
+    genus of a multi-genus collection, its bank on this rank's GPU) and probes
+    every read of the file; the per-read hit columns of all ranks are
+    all-gathered into one MatrixResult over every rank's docs (labels in rank
+    order), the same on every rank.
+
+    Under RCCL each batch goes to the device once, is probed there
+    (``docs_sharded_hits_device``: probe, narrow, all-gather over xGMI, widen)
+    and only the gathered matrix, narrowed to the reads' count width, comes
+    back.  Under gloo (CPU tests, shared-GPU rehearsal) the rows are probed
+    from host buffers and gathered through the host."""
+    import torch
+    from .bank import narrowest_count_dtype
+    from .file_io import check_input_path, read_batches
+    from .result import MatrixResult
+
+    dist = _dist()
+    world = dist.get_world_size()
+    input_file = Path(input_file)
+    check_input_path(input_file)
+    labels_all: list = [None] * world
+    dist.all_gather_object(labels_all, model._labels(display_name))
+    labels = [lab for part in labels_all for lab in part]
+    on_device = collective_device().type == "cuda"
+    ids, hits, nks = [], [], []
+    for batch in read_batches(input_file):
+        L = batch.lengths()
+        if (L <= model.k).any():
+            raise ValueError("Invalid sequence, must be longer than k")
+        pr = batch.packed
+        mx = int(((L - model.k) // step + 1).max()) if batch.n else 0
+        if on_device:
+            dev = torch.device("cuda", model.index.info.device)
+            d_seq = torch.from_numpy(pr.buf[:max(pr.nbytes, 1)]).to(dev)
+            d_off = torch.from_numpy(pr.offsets.view(np.int64)).to(dev)
+            g, d_nk = docs_sharded_hits_device(model.index, d_seq, pr.nbytes, d_off, pr.n, step)
+            dt = narrowest_count_dtype(mx)
+            h = g.to({np.uint8: torch.uint8, np.uint16: torch.int16}.get(dt, torch.int32)).cpu().numpy()
+            h = h.view(np.uint16) if dt == np.uint16 else h.view(np.uint8) if dt == np.uint8 else h.view(np.uint32)
+            nk = d_nk.cpu().numpy().view(np.uint64)
+        else:
+            hl, nk = model._query(pr, step)
+            t = torch.from_numpy(np.ascontiguousarray(hl).astype(np.int32))
+            h = gather_doc_shards(t, mx).numpy().view(np.uint32)  # every rank reads the same batches
+        ids += batch.ids()
+        hits.append(h)
+        nks.append(nk)
+    D = len(labels)
+    if hits:
+        dt = max((h.dtype for h in hits), key=lambda t: t.itemsize)
+        hm = np.concatenate([h.astype(dt, copy=False) for h in hits]) if len(hits) > 1 else hits[0]
+        nk = np.concatenate(nks)
+    else:
+        hm, nk = np.zeros((0, D), np.uint8), np.zeros(0, np.uint64)
+    res = MatrixResult("multi-genus-docs-sharded", ids, labels, hm, nk, sparse_sampling_step=step)
+    res.input_source = input_file.name
+    return res
