@@ -55,8 +55,10 @@ class OracleIndex:
         return h.astype(hit_dtype), nk
 
 
-def _setup(tmp: Path, n_reads: int, svm: bool):
-    """A species model over 6 synthetic genomes (oracle bank), its reads as a FASTQ file."""
+def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True):
+    """A species model over 6 synthetic genomes (oracle bank), its reads as a
+    FASTQ file (written by the parent before the ranks start: a rank must not
+    rewrite a file another rank is reading)."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
     from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
@@ -78,7 +80,8 @@ def _setup(tmp: Path, n_reads: int, svm: bool):
                 v = [round(0.05 + 0.02 * rep, 2)] * 6
                 v[j] = 1.0 - 0.1 * rep
                 rows.append(f"acc{j}{rep}," + ",".join(str(x) for x in v) + f",{lab}")
-        (base / model.slug() / "scores.csv").write_text("\n".join(rows))
+        if write:
+            (base / model.slug() / "scores.csv").write_text("\n".join(rows))
     else:
         model = ProbabilisticFilterModel(K, "Acinetobacter", None, None, "Species", base)
     model.display_names = {n: f"Acinetobacter sp{d}" for d, n in enumerate(names)}
@@ -90,7 +93,8 @@ def _setup(tmp: Path, n_reads: int, svm: bool):
         s = int(rng.integers(0, len(g) - L))
         reads.append((f"read_{i}", g[s:s + L].decode()))
     fq = tmp / "reads.fq"
-    fq.write_text("".join(f"@{rid} x\n{s}\n+\n{'I' * len(s)}\n" for rid, s in reads))
+    if write:
+        fq.write_text("".join(f"@{rid} x\n{s}\n+\n{'I' * len(s)}\n" for rid, s in reads))
     return model, fq
 
 
@@ -105,7 +109,7 @@ def _worker(rank: int, world: int, port: int, tmp: str, n_reads: int, svm: bool)
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        model, fq = _setup(Path(tmp), n_reads, svm)
+        model, fq = _setup(Path(tmp), n_reads, svm, write=False)
         for i, kw in enumerate(CASES):
             distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / f"case{i}.json", **kw)
     finally:
@@ -117,8 +121,8 @@ def test_classify_species_sharded_equals_single_process(tmp_path, world, n_reads
     import torch.multiprocessing as mp
     from xspect2_amd import distributed
 
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_reads, svm), nprocs=world, join=True)
     model, fq = _setup(tmp_path, n_reads, svm)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), n_reads, svm), nprocs=world, join=True)
     for i, kw in enumerate(CASES):
         res = model.predict_columnar(fq, **kw)
         res.input_source = fq.name
