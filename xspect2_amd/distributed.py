@@ -170,12 +170,15 @@ def gather_doc_shards(hits, max_count: int | None = None, layout=None):
     wire = _on_wire(pad.view(torch.float16) if dt == torch.int16 else pad)
     parts = [torch.empty_like(wire) for _ in range(world)]
     dist.all_gather(parts, wire)
-    cols = []
+    # widened straight into the output: one pass over the gathered bytes
+    out = torch.empty((n, sum(dims)), dtype=torch.int32, device=hits.device)
+    c0 = 0
     for p, d in zip(parts, dims):
         if dt == torch.int16:
             p = p.view(torch.int16)
-        cols.append(p.to(hits.device)[:, :d])
-    return torch.cat(cols, dim=1).to(torch.int32)
+        out[:, c0:c0 + d].copy_(p[:, :d])
+        c0 += d
+    return out
 
 
 def docs_sharded_hits(reads: PackedReads, step: int,
