@@ -63,9 +63,10 @@ static std::string make_fastq(int recs, bool wrapped, bool trailing_nl, bool mal
     return out;
 }
 
-static int read_all(const std::string& path, int fmt, int threads, uint64_t batch, uint64_t* recs) {
+static int read_all(const std::string& path, int fmt, int threads, uint64_t batch, uint64_t* recs,
+                    uint32_t part = 0, uint32_t parts = 1) {
     xs_fastx* r = nullptr;
-    int rc = xs_fastx_open(path.c_str(), fmt, threads, 0, &r);
+    int rc = xs_fastx_open_range(path.c_str(), fmt, threads, 0, part, parts, &r);
     if (rc) return rc;
     *recs = 0;
     xs_fastx_batch b;
@@ -102,13 +103,31 @@ int main() {
     auto sweep = [&](const std::string& text, int fmt, bool must_parse) {
         write_file(path, text);
         ++files;
+        uint64_t whole = 0;
         for (uint64_t batch : {1ull, 7ull, 64ull, 1000ull, 1ull << 20})
             for (int threads : {1, 3, 8}) {
                 uint64_t n = 0;
                 const int rc = read_all(path, fmt, threads, batch, &n);
                 if (rc) ++errors;  // malformed inputs must fail with an error code, not a crash
                 if (rc && must_parse) ++unexpected;
+                if (!rc) whole = n;
             }
+        // byte-range parts (one rank each of a read-sharded job): well-formed
+        // files split into parts whose record counts add up to the whole file's
+        for (uint32_t parts : {2u, 3u, 7u}) {
+            uint64_t sum = 0;
+            bool failed = false;
+            for (uint32_t part = 0; part < parts; ++part) {
+                uint64_t n = 0;
+                const int rc = read_all(path, fmt, 1 + part % 3, 64, &n, part, parts);
+                if (rc) {
+                    ++errors;
+                    failed = true;
+                }
+                sum += n;
+            }
+            if (must_parse && (failed || sum != whole)) ++unexpected;
+        }
     };
     for (int trial = 0; trial < 60; ++trial) {
         const bool fq = trial % 2;
@@ -154,7 +173,7 @@ int main() {
                                      nullptr, 1 + trial % 8))
             ++errors;
     }
-    printf("host sanitizer run: %d input files x 15 reader configurations, 20 JSON matrices; "
+    printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices; "
            "%d clean error returns, %d on well-formed input\n", files, errors, unexpected);
     return unexpected ? 1 : 0;
 }

@@ -41,15 +41,21 @@ std::string score_text(uint64_t h, uint64_t n) {
     return s;
 }
 
-struct ScoreCache {  // per thread: score strings of h = 0..n for the last n seen
+struct ScoreCache {  // per thread: score strings of h = 0..n for the n of the last read
     std::unordered_map<uint64_t, std::vector<std::string>> by_n;
+    uint64_t last_n = ~0ull;
+    const std::vector<std::string>* last = nullptr;
     const std::string& get(uint64_t h, uint64_t n) {
-        auto& v = by_n[n];
-        if (v.empty() && n <= (1u << 16)) {
-            v.resize(n + 1);
-            for (uint64_t i = 0; i <= n; ++i) v[i] = score_text(i, n);
+        if (n != last_n) {  // reads of one batch mostly share n: one hash lookup per change
+            auto& v = by_n[n];
+            if (v.empty() && n <= (1u << 16)) {
+                v.resize(n + 1);
+                for (uint64_t i = 0; i <= n; ++i) v[i] = score_text(i, n);
+            }
+            last_n = n;
+            last = &v;
         }
-        if (h < v.size()) return v[h];
+        if (h < last->size()) return (*last)[h];
         thread_local std::string tmp;
         tmp = score_text(h, n);
         return tmp;
@@ -65,56 +71,131 @@ struct Ctx {
     const uint64_t* ids_off;
     const char* labels;
     const uint64_t* labels_off;
-    std::vector<uint32_t> docs;  // emitted docs (doc_mask), ascending
+    std::vector<uint32_t> docs;       // emitted docs (doc_mask), ascending
+    std::vector<std::string> entry;   // per doc: ",\n", the indented label key and ": "
+    std::vector<std::string> count;   // decimal text of small counts
+    size_t row_bound = 0;             // bytes one read's entries can take (ids aside)
 };
 
-// Docs of one hit row in COBS result order: count descending, ties by doc index.
+// Docs of one hit row in COBS result order: count descending, ties by doc index
+// (one sort of 64-bit keys (~count << 32 | doc): no allocation per row).
+template <class T>
+void order_of(const std::vector<uint32_t>& docs, const T* row, std::vector<uint32_t>& ord,
+              std::vector<uint64_t>& keys) {
+    keys.resize(docs.size());
+    for (size_t j = 0; j < docs.size(); ++j) keys[j] = ((uint64_t)(~(uint32_t)row[docs[j]]) << 32) | docs[j];
+    std::sort(keys.begin(), keys.end());
+    ord.resize(docs.size());
+    for (size_t j = 0; j < docs.size(); ++j) ord[j] = (uint32_t)keys[j];
+}
 template <class T>
 void order_of(const std::vector<uint32_t>& docs, const T* row, std::vector<uint32_t>& ord) {
-    ord = docs;
-    std::stable_sort(ord.begin(), ord.end(), [row](uint32_t a, uint32_t b) { return row[a] > row[b]; });
+    std::vector<uint64_t> keys;
+    order_of(docs, row, ord, keys);
+}
+
+// The same order by a counting sort over the counts 0..cap (a read's counts
+// never exceed its k-mer count, the cap passed): bucket offsets from the top
+// count down, docs placed in ascending order within a bucket.  cnt: cap + 2
+// scratch entries.  False (nothing done) if some count exceeds cap.
+template <class T>
+bool order_counting(const std::vector<uint32_t>& docs, const T* row, uint32_t cap, std::vector<uint32_t>& ord,
+                    std::vector<uint32_t>& cnt) {
+    for (uint32_t d : docs)
+        if ((uint32_t)row[d] > cap) return false;
+    cnt.assign((size_t)cap + 2, 0);
+    for (uint32_t d : docs) ++cnt[cap - (uint32_t)row[d] + 1];
+    for (size_t i = 1; i < cnt.size(); ++i) cnt[i] += cnt[i - 1];
+    ord.resize(docs.size());
+    for (uint32_t d : docs) ord[cnt[cap - (uint32_t)row[d]]++] = d;
+    return true;
 }
 
 inline void put_key(std::string& o, const char* base, const uint64_t* off, uint64_t i) {
     o.append(base + off[i], (size_t)(off[i + 1] - off[i]));
 }
 
+constexpr uint32_t kCountText = 1024;  // counts below this are formatted once
+
+template <class T>
+void prepare(Ctx<T>& c) {
+    c.entry.resize(c.D);
+    size_t bound = 64;
+    for (uint64_t d = 0; d < c.D; ++d) {
+        std::string& e = c.entry[d];
+        e = ",\n            ";
+        put_key(e, c.labels, c.labels_off, d);
+        e += ": ";
+        bound += e.size() + 32;  // + the count or score text
+    }
+    c.row_bound = bound;
+    c.count.resize(kCountText);
+    for (uint32_t v = 0; v < kCountText; ++v) c.count[v] = std::to_string(v);
+}
+
+// Appends to a byte buffer through a cursor: capacity is ensured once per
+// read, then every piece is a memcpy.
+struct Sink {
+    std::string& s;
+    size_t len;
+    explicit Sink(std::string& out) : s(out), len(out.size()) {}
+    void ensure(size_t more) {
+        if (len + more > s.size()) s.resize(std::max(s.size() * 2, len + more));
+    }
+    void put(const char* p, size_t n) {
+        memcpy(&s[len], p, n);
+        len += n;
+    }
+    void put(const std::string& x) { put(x.data(), x.size()); }
+    void finish() { s.resize(len); }
+};
+
 // section 0: hits, 1: scores, 2: num_kmers — entries of reads [lo, hi)
 template <class T>
 void format_block(const Ctx<T>& c, int section, uint64_t lo, uint64_t hi, std::string& o) {
-    std::vector<uint32_t> ord;
+    std::vector<uint32_t> ord, cnt;
+    std::vector<uint64_t> keys;
     ScoreCache cache;
     char num[32];
+    Sink k(o);
     for (uint64_t r = lo; r < hi; ++r) {
-        if (r) o += ",\n";
-        o += "        ";
-        put_key(o, c.ids, c.ids_off, r);
+        const size_t idl = (size_t)(c.ids_off[r + 1] - c.ids_off[r]);
+        k.ensure(idl + 64 + (section == 2 ? 0 : c.row_bound));
+        if (r) k.put(",\n", 2);
+        k.put("        ", 8);
+        k.put(c.ids + c.ids_off[r], idl);
         if (section == 2) {
-            int k = snprintf(num, sizeof(num), ": %llu", (unsigned long long)c.nk[r]);
-            o.append(num, (size_t)k);
+            int n = snprintf(num, sizeof(num), ": %llu", (unsigned long long)c.nk[r]);
+            k.put(num, (size_t)n);
             continue;
         }
         if (c.docs.empty()) {
-            o += ": {}";
+            k.put(": {}", 4);
             continue;
         }
-        o += ": {\n";
+        k.put(": {\n", 4);
         const T* row = c.hits + r * c.D;
-        order_of(c.docs, row, ord);
+        if (c.nk[r] >= 4096 || !order_counting(c.docs, row, (uint32_t)c.nk[r], ord, cnt))
+            order_of(c.docs, row, ord, keys);
         for (size_t j = 0; j < ord.size(); ++j) {
-            if (j) o += ",\n";
-            o += "            ";
-            put_key(o, c.labels, c.labels_off, ord[j]);
-            o += ": ";
+            const std::string& e = c.entry[ord[j]];
+            if (j) k.put(e);
+            else k.put(e.data() + 2, e.size() - 2);  // the first entry has no ",\n"
+            const uint32_t v = (uint32_t)row[ord[j]];
             if (section == 0) {
-                int k = snprintf(num, sizeof(num), "%u", (unsigned)row[ord[j]]);
-                o.append(num, (size_t)k);
+                if (v < kCountText) {
+                    k.put(c.count[v]);
+                } else {
+                    int n = snprintf(num, sizeof(num), "%u", v);
+                    k.put(num, (size_t)n);
+                }
             } else {
-                o += cache.get(row[ord[j]], c.nk[r]);
+                k.put(cache.get(v, c.nk[r]));
             }
         }
-        o += "\n        }";
+        k.put("\n        }", 10);
     }
+    k.finish();
 }
 
 template <class T>
@@ -124,28 +205,40 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
     FILE* f = fopen(path, "ab");
     if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
     const int NT = std::max(1, std::min(threads > 0 ? threads : 16, 64));
-    const uint64_t block = 1 << 16;  // reads per formatting round
-    std::vector<std::string> out((size_t)NT);
+    const uint64_t block = 1 << 14;  // reads per formatting round
+    // two sets of per-thread buffers: round i is formatted while round i-1 is written
+    std::vector<std::string> out[2] = {std::vector<std::string>((size_t)NT), std::vector<std::string>((size_t)NT)};
     bool ok = true;
     const char* heads[3] = {"\"hits\": ", "\"scores\": ", "\"num_kmers\": "};
     for (int section = 0; section < 3 && ok; ++section) {
         // an empty section is "{}" as json.dumps writes it (a shard without reads)
         const bool empty = n == 0 && section != 1;
         ok = fputs(heads[section], f) >= 0 && fputs(empty ? "{}" : "{\n", f) >= 0;
-        for (uint64_t b0 = 0; b0 < n && ok; b0 += block) {
+        std::thread writer;
+        bool wok = true;
+        int cur = 0;
+        for (uint64_t b0 = 0; b0 < n && ok; b0 += block, cur ^= 1) {
             const uint64_t b1 = std::min(n, b0 + block);
             const uint64_t per = (b1 - b0 + NT - 1) / NT;
             std::vector<std::thread> th;
-            auto work = [&](int t) {
-                out[t].clear();
+            auto work = [&, b0, b1, per, cur](int t) {
+                out[cur][t].clear();
                 const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
-                if (lo < hi) format_block(c, section, lo, hi, out[t]);
+                if (lo < hi) format_block(c, section, lo, hi, out[cur][t]);
             };
             for (int t = 1; t < NT; ++t) th.emplace_back(work, t);
             work(0);
             for (auto& x : th) x.join();
-            for (int t = 0; t < NT && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
+            if (writer.joinable()) writer.join();
+            ok = wok;
+            if (!ok) break;
+            writer = std::thread([&, cur] {
+                for (int t = 0; t < NT && wok; ++t)
+                    wok = fwrite(out[cur][t].data(), 1, out[cur][t].size(), f) == out[cur][t].size();
+            });
         }
+        if (writer.joinable()) writer.join();
+        ok = ok && wok;
         if (!ok) break;
         if (section == 1) {
             // "total": labels in the first read's order, round(sum hits / sum num_kmers, 2);
@@ -190,9 +283,11 @@ int write_typed(const char* path, uint64_t n, uint64_t num_docs, const void* hit
                 const char* ids_json, const uint64_t* ids_off, const char* labels_json, const uint64_t* labels_off,
                 const uint8_t* doc_mask, const uint64_t* total_hits, uint64_t total_kmers,
                 const uint32_t* total_order_row, int threads) {
-    Ctx<T> c{n, num_docs, static_cast<const T*>(hits), num_kmers, ids_json, ids_off, labels_json, labels_off, {}};
+    Ctx<T> c{n, num_docs, static_cast<const T*>(hits), num_kmers, ids_json, ids_off, labels_json, labels_off,
+             {}, {}, {}, 0};
     for (uint64_t d = 0; d < num_docs; ++d)
         if (!doc_mask || doc_mask[d]) c.docs.push_back((uint32_t)d);
+    prepare(c);
     return write_sections(path, c, total_hits, total_kmers, total_order_row, threads);
 }
 
