@@ -98,21 +98,22 @@ def main():
         res[f"e2e_totals_s{'_pinned' if pinned else ''}"] = dt
         res[f"e2e_totals_reads_per_s{'_pinned' if pinned else ''}"] = n / dt
 
-    # the model path since round 3: hit matrix narrowed on the device (u8 for
-    # 150 bp reads) into reused pinned buffers, parse overlapped
+    # the model path since round 3 (Bank.query(hit_dtype="auto")): the hit
+    # matrix narrowed on the device (u8 for 150 bp reads) into fresh pageable
+    # arrays; and the same into pinned buffers a serving loop reuses
     from xspect2_amd.bank import pinned_empty
-    outs = {}
-    t = time.perf_counter()
-    n = 0
-    for b in read_batches(fq, mb, pinned=True):
-        o = outs.get(b.n)
-        if o is None:
-            o = outs[b.n] = pinned_empty((b.n, args.docs), np.uint8)
-        h, nk = bank.query(b.packed, hit_dtype=np.uint8, out=o)
-        n += b.n
-    dt = time.perf_counter() - t
-    res["e2e_hits_u8_pinned_out_s"] = dt
-    res["e2e_hits_u8_pinned_out_reads_per_s"] = n / dt
+    sizes = [b.n for b in read_batches(fq, mb)]
+    outs = {n_: pinned_empty((n_, args.docs), np.uint8) for n_ in set(sizes)}
+    for name, kw in (("auto", lambda b: {"hit_dtype": "auto"}),
+                     ("u8_pinned_out", lambda b: {"hit_dtype": np.uint8, "out": outs[b.n]})):
+        t = time.perf_counter()
+        n = 0
+        for b in read_batches(fq, mb, pinned=True):
+            h, nk = bank.query(b.packed, **kw(b))
+            n += b.n
+        dt = time.perf_counter() - t
+        res[f"e2e_hits_{name}_s"] = dt
+        res[f"e2e_hits_{name}_reads_per_s"] = n / dt
 
     # per-read best doc, hit matrix kept on the device
     t = time.perf_counter()
