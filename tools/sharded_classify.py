@@ -6,9 +6,9 @@
     python tools/sharded_classify.py check  --root DIR --world N     # merged shards == single.json
 
 Config 5 (docs sharded; one genus model per rank, every read on every rank):
-    python tools/sharded_classify.py docs-setup  --root DIR [--reads N]  # 2 genus models of 60 species + reads
-    python tools/sharded_classify.py docs-single --root DIR              # both models in one process
-    torchrun --nproc-per-node 2 tools/sharded_classify.py docs-shard --root DIR
+    python tools/sharded_classify.py docs-setup  --root DIR --world N [--reads R]  # N genus models of 60 species
+    python tools/sharded_classify.py docs-single --root DIR --world N              # all models in one process
+    torchrun --nproc-per-node N tools/sharded_classify.py docs-shard --root DIR
     python tools/sharded_classify.py docs-check  --root DIR
 
 `shard` runs xspect2_amd.classify.classify_species_sharded: each rank parses
@@ -28,7 +28,7 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 GENUS = "Acinetobacter"
-GENERA = ["Acinetobacter", "Pseudomonas"]
+GENERA = ["Acinetobacter", "Pseudomonas", "Klebsiella", "Escherichia"]
 
 
 def setup(root: Path, n_reads: int) -> None:
@@ -56,15 +56,15 @@ def setup(root: Path, n_reads: int) -> None:
             fh.write(f"@read_{i} synthetic\n{s}\n+\n{'I' * len(s)}\n")
 
 
-def docs_setup(root: Path, n_reads: int) -> None:
-    """Two genus species models of 60 species each (fit on the GPU) and reads from all 120 genomes."""
+def docs_setup(root: Path, n_reads: int, world: int) -> None:
+    """`world` genus species models of 60 species each (fit on the GPU) and reads from all their genomes."""
     import numpy as np
     from xspect2_amd.file_io import Record, write_fasta
     from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
     from xspect2_amd.synth import make_genomes, make_reads
 
     allg = []
-    for gi, genus in enumerate(GENERA):
+    for gi, genus in enumerate(GENERA[:world]):
         genomes = make_genomes(60, 100_000, seed=100 + gi)
         allg.append(genomes)
         sp = root / f"species_{genus}"
@@ -113,14 +113,14 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     elif a.cmd == "docs-setup":
-        docs_setup(root, a.reads)
+        docs_setup(root, a.reads, a.world)
     elif a.cmd == "docs-single":
         import numpy as np
         from xspect2_amd import classify
         from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
         from xspect2_amd.result import MatrixResult
         parts = [ProbabilisticFilterModel.load(classify.species_model_path(g)).predict_columnar(
-            root / "docs_reads.fasta", step=a.step) for g in GENERA]
+            root / "docs_reads.fasta", step=a.step) for g in GENERA[:a.world]]
         hits = np.concatenate([p.hits.astype(np.uint32) for p in parts], axis=1)
         res = MatrixResult("multi-genus-docs-sharded", parts[0].ids, [lab for p in parts for lab in p.labels], hits,
                            parts[0].num_kmers, sparse_sampling_step=a.step)
