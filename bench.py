@@ -427,6 +427,8 @@ def main():
     nr = f"{wl.n / 1e6:g}M x {args.read_len}bp reads"
     species_cfg = ("config3 per-GPU shard (100M reads / 8 GPUs)" if wl.n == 12_500_000 else
                    "config2" if wl.n == 1_000_000 else "species")
+    if world > 1:
+        species_cfg += f" per GPU, reads sharded over {world} GPUs (config 3's layout)"
     names = {"species": f"{species_cfg}: {nr}/GPU vs D={args.docs} COBS classic species bank",
              "genus": f"genus path: {nr}/GPU vs rbloom filter over {args.docs} genomes",
              "mlst": f"config4: {nr}/GPU vs 7 loci x 1430 alleles (COBS compact)",
