@@ -868,3 +868,44 @@ def test_pass_stats_of_the_partitioned_probe(xs, oracle_mod, monkeypatch):
     assert gb.pass_stats()["lookup"] == (0.0, 0)  # reset
     gb.set_profiling(False)
     gb.close()
+
+
+@pytest.mark.parametrize("n_short,n_long,threshold", [(30, 5, 50), (0, 6, 50), (25, 0, 50), (10, 4, 0),
+                                                      (3, 3, 1000)])
+def test_mlst_query_matches_oracle(xs, oracle_mod, n_short, n_long, threshold):
+    """xs_mlst_query against the oracle on a compact bank: direct rows of the
+    short sequences; per long sequence the chunk scores > threshold summed per
+    allele, the first passing chunk (UINT32_MAX where none) and its score;
+    owners with no passing chunk, no short / no long sequences, threshold 0
+    (every nonzero count) and a threshold no chunk reaches."""
+    D, k, page = 90, 21, 4  # 3 groups of 32 docs
+    rng = np.random.default_rng(n_short * 7 + n_long)
+    sig = [int(x) for x in rng.integers(3000, 6000, 3)]
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, 1, sig, page=page, seed=n_short + 3 * n_long, per_doc=1)
+    short = [s[:int(rng.integers(k + 1, len(s) + 1))] for s in seqs[:n_short]]
+    chunks, owner = [], []
+    for j in range(n_long):
+        parts = [seqs[int(rng.integers(0, D))][:int(rng.integers(k + 1, 600))] for _ in range(int(rng.integers(1, 9)))]
+        if j == 1:
+            parts = [_reads(rng, 1, k, min_len=200, max_len=201)[0]]  # random: nothing passes (usually)
+        chunks += parts
+        owner += [j] * len(parts)
+    n_owners = n_long + 1  # one owner without chunks
+    h, sc, first, fs = gb.mlst_query(short, chunks, owner, n_owners, 1, threshold)
+    if short:
+        want_h, _ = ob.query(short)
+        assert np.array_equal(h, want_h)
+    else:
+        assert h.shape == (0, D)
+    rows = ob.query(chunks)[0] if chunks else np.zeros((0, D), np.uint32)
+    want_sc = np.zeros((n_owners, D), np.uint64)
+    want_first = np.full((n_owners, D), 0xFFFFFFFF, np.uint32)
+    want_fs = np.zeros((n_owners, D), np.uint32)
+    for c, (o, row) in enumerate(zip(owner, rows)):
+        m = row > threshold
+        want_sc[o, m] += row[m]
+        new = m & (want_first[o] == 0xFFFFFFFF)
+        want_first[o, new] = c
+        want_fs[o, new] = row[new]
+    assert np.array_equal(sc, want_sc) and np.array_equal(first, want_first) and np.array_equal(fs, want_fs)
+    gb.close()
