@@ -282,6 +282,9 @@ def classify_species_sharded(model, input_file: Path, output_path: Path, step: i
        scores and k-mer counts, the job's "total" and prediction.
 
     ``merge_result_shards`` of the shards equals the single-process JSON.
+    One deviation: a read id repeated in two different shards is kept once
+    per shard in the job's totals, where the single-process dictionaries keep
+    only its last record (repeats inside one shard collapse as there).
     Returns this rank's MatrixResult (a shard)."""
     import torch
     from .file_io import FileShard
