@@ -278,15 +278,26 @@ def test_mlst_model(tmp_path, oracle_mod):
         m2.predict([Record("x", allele)])
 
 
-def test_config1_classify_species_on_an_assembly(tmp_path, species_dir, genomes, oracle_mod, monkeypatch):
+@pytest.mark.parametrize("masked", [True, False])
+def test_config1_classify_species_on_an_assembly(tmp_path, species_dir, genomes, oracle_mod, monkeypatch, masked):
     """BASELINE config 1: `xspect classify species` on one assembly FASTA
     (classify.py:70-92 here, reference src/xspect/classify.py:43-92).  The
     assembly is a multi-contig FASTA of one species' genome (lower case, an N
     run, 70-column lines); every contig is one record of thousands of k-mers,
     so each spans many probe units.  The saved JSON's hits, k-mer counts and
-    totals must equal the oracle's."""
+    totals must equal the oracle's.
+
+    ``masked=False`` repeats the case with upper-case ACGT only, in the
+    training genomes too: its equality does not lean on the unpinned rule for
+    lower case and N, which the masked case does."""
     from xspect2_amd import classify
     from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+
+    if not masked:
+        species_dir = tmp_path / "species_upper"
+        species_dir.mkdir()
+        for i, f in enumerate(sorted((tmp_path / "species").iterdir())):
+            write_fasta([Record(f"c{i}", genomes[i].tobytes().decode())], species_dir / f.name, width=80)
 
     root = tmp_path / "xspect-data"
     monkeypatch.setenv("XSPECT_DATA", str(root))
@@ -297,7 +308,8 @@ def test_config1_classify_species_on_an_assembly(tmp_path, species_dir, genomes,
 
     g1 = genomes[1].tobytes().decode()
     contigs = [Record("contig_1 len=12000", g1[:12_000]),
-               Record("contig_2", g1[12_000:21_000].lower() + "N" * 40 + g1[21_000:26_000]),
+               Record("contig_2", g1[12_000:21_000].lower() + "N" * 40 + g1[21_000:26_000] if masked
+                      else g1[12_000:26_000]),
                Record("contig_3", g1[26_000:])]
     fa = tmp_path / "assembly.fna"
     write_fasta(contigs, fa, width=70)
