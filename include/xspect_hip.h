@@ -136,6 +136,20 @@ int xs_query(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t 
  * if some read has more k-mers than the width holds. */
 int xs_query_hits(xs_bank* bank, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                   void* hits_out, int hit_bytes, uint64_t* num_kmers_out);
+/* xs_query_hits / xs_query_totals for reads already in HBM (an
+ * xs_fastx_dbatch: d_seqs, seq_bytes, d_offsets with [0] = 0, max_len = its
+ * longest read, which bounds every count for the width check).  Outputs are
+ * host memory, each optional: hits_out n x D (hit_bytes 1, 2 or 4), the
+ * sampled k-mer counts, totals_out D+1 (per-doc sums, then the k-mer total).
+ * The probe runs in read chunks whose hit rows go back while the next chunk
+ * is probed. */
+int xs_query_hits_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes, const uint64_t* d_offsets,
+                         uint64_t n, uint64_t max_len, uint32_t step, void* hits_out, int hit_bytes,
+                         uint64_t* num_kmers_out, uint64_t* totals_out);
+
+/* Blocking device -> host copy of `bytes` (e.g. an xs_fastx_dbatch's
+ * sequences, for checks). */
+int xs_memcpy_to_host(void* host, const void* dev, uint64_t bytes);
 
 /* Pinned (page-locked) host memory for outputs the caller reuses across calls:
  * results land there by DMA, with no page faults on a fresh pageable buffer. */
@@ -297,6 +311,37 @@ int xs_fastx_open_range(const char* path, int format, int threads, int flags, ui
  * Malformed records return XS_ERR_FORMAT with Biopython's message. */
 int xs_fastx_next(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_batch* out);
 void xs_fastx_close(xs_fastx* reader);
+
+/* Device mode of the same reader (SURVEY.md §8 f1 on the GPU): each window of
+ * text — cut exactly as xs_fastx_next cuts it — is copied into pinned memory
+ * by host threads and on to HBM, and its records are found on `device`
+ * (xs_fastx_dev.hip).  The next window's text is loaded while the caller works
+ * on the returned batch.  A window outside the device rules (wrapped FASTQ,
+ * blank lines between FASTQ records, empty FASTQ sequences, ' ' or '\r' inside
+ * FASTA sequence lines, malformed records) is parsed by the host parser, so
+ * batches, ids, titles and error messages equal xs_fastx_next's. */
+typedef struct xs_fastx_dbatch {
+    uint64_t n;                  /* records in this batch (0: end of the text) */
+    uint64_t seq_bytes;          /* bytes of seqs */
+    const void* seqs;            /* DEVICE: record r = seqs[offsets[r] .. offsets[r+1]), 64 zero bytes past the end */
+    const uint64_t* offsets;     /* DEVICE: n+1 entries, offsets[0] = 0 */
+    const uint64_t* host_offsets;/* host: the same n+1 offsets */
+    uint64_t max_len;            /* longest record of the batch */
+    const char* ids;             /* host: record ids (first header token), packed */
+    const uint64_t* id_offsets;  /* host: n+1 entries */
+    const char* descs;           /* host: record titles */
+    const uint64_t* desc_offsets;/* host: n+1 entries */
+    uint64_t text_offset;        /* file offset parsed up to */
+    uint64_t text_bytes;         /* end offset of the reader's text */
+    int parsed_on_device;        /* 0: this window went through the host parser */
+} xs_fastx_dbatch;
+
+/* As xs_fastx_open_range, for xs_fastx_next_device on `device`. */
+int xs_fastx_open_device(const char* path, int format, int threads, int device, uint32_t part, uint32_t parts,
+                         xs_fastx** out);
+/* Next batch, complete on the device when this returns.  Buffers stay valid
+ * until the SECOND following call.  Errors as xs_fastx_next. */
+int xs_fastx_next_device(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_dbatch* out);
 
 /* Write records as Bio.SeqIO.write(record, fh, "fasta") does (the genus
  * filter's output, src/xspect/file_io.py:166-191): ">" title, then the

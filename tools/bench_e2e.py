@@ -3,6 +3,9 @@
 Writes a synthetic FASTQ of --reads x 150 bp reads (seeded genomes of the
 bench's config-2 bank), then times:
   parse      native reader alone (xs_fastx_next over the whole file)
+  dparse     the reader's device mode alone (text -> HBM, records found on the GPU)
+  e2e_dev_*  the same streaming with the device-mode reader (DeviceSeqBatch ->
+             xs_query_hits_device): min over --reps passes, and the first pass
   e2e        ProbabilisticFilterModel-style streaming: read_batches -> Bank.query
              (H2D, probe, D2H of the n x D hit matrix), parse overlapped
   e2e_tot    same, but per-doc totals only (xs_query_totals, no hit matrix)
@@ -36,6 +39,8 @@ def main():
     ap.add_argument("--genome-len", type=int, default=4_000_000)
     ap.add_argument("--batch-mb", type=int, default=256)
     ap.add_argument("--dir", default=None)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--quick", action="store_true", help="parse and e2e legs only")
     args = ap.parse_args()
 
     import torch
@@ -77,6 +82,54 @@ def main():
     assert n == reads.shape[0]
     res["parse_s"] = dt
     res["parse_GBps"] = size / dt / 1e9
+
+    # device-mode reader: parse only, then file -> hits / totals
+    def timed(fn):
+        ts = []
+        for _ in range(max(1, args.reps)):
+            t = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t)
+        return min(ts), ts[0]
+
+    def dparse():
+        n_ = 0
+        on_dev = True
+        for b in read_batches(fq, mb, device=0):
+            n_ += b.n
+            on_dev &= b.parsed_on_device
+        assert n_ == reads.shape[0] and on_dev
+    res["dparse_s"], res["dparse_first_s"] = timed(dparse)
+    res["dparse_GBps"] = size / res["dparse_s"] / 1e9
+    print("dparse", res["dparse_s"], file=sys.stderr, flush=True)
+    from xspect2_amd.file_io import FastxReader
+    with FastxReader(fq, device=0) as rdd, FastxReader(fq) as rdh:  # batches live as long as their readers
+        first_dev, first_host = rdd.next_batch(mb), rdh.next_batch(mb)
+        hd, nd = bank.query(first_dev, hit_dtype="auto")
+        hh, nh = bank.query(first_host.packed, hit_dtype="auto")
+        res["device_reader_first_batch_equal"] = bool(np.array_equal(hd, hh) and np.array_equal(nd, nh)
+                                                      and first_dev.ids() == first_host.ids())
+    del first_dev, first_host
+    from xspect2_amd.bank import pinned_empty as _pe
+    dev_sizes = [b.n for b in read_batches(fq, mb, device=0)]
+    dev_outs = {n_: _pe((n_, args.docs), np.uint8) for n_ in set(dev_sizes)}
+    for name, fn in (("hits_auto", lambda b: bank.query(b, hit_dtype="auto")),
+                     ("hits_u8_pinned_out", lambda b: bank.query(b, hit_dtype=np.uint8, out=dev_outs[b.n])),
+                     ("totals", lambda b: bank.query_totals(b))):
+        def run(fn=fn):
+            for b in read_batches(fq, mb, device=0):
+                fn(b)
+        res[f"e2e_dev_{name}_s"], res[f"e2e_dev_{name}_first_s"] = timed(run)
+        res[f"e2e_dev_{name}_reads_per_s"] = reads.shape[0] / res[f"e2e_dev_{name}_s"]
+        print(name, res[f"e2e_dev_{name}_s"], file=sys.stderr, flush=True)
+    if args.quick:
+        for pinned in (False, True):
+            t = time.perf_counter()
+            for b in read_batches(fq, mb, pinned=pinned):
+                bank.query(b.packed, hit_dtype="auto")
+            res[f"e2e_hits_auto_s{'_pinned' if pinned else ''}"] = time.perf_counter() - t
+        print(json.dumps(res))
+        return
 
     for pinned in (False, True):
         # warm

@@ -74,6 +74,24 @@ class FastxBatch(ctypes.Structure):
     ]
 
 
+class FastxDBatch(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("seq_bytes", ctypes.c_uint64),
+        ("seqs", ctypes.c_void_p),       # device
+        ("offsets", ctypes.c_void_p),    # device
+        ("host_offsets", ctypes.c_void_p),
+        ("max_len", ctypes.c_uint64),
+        ("ids", ctypes.c_void_p),
+        ("id_offsets", ctypes.c_void_p),
+        ("descs", ctypes.c_void_p),
+        ("desc_offsets", ctypes.c_void_p),
+        ("text_offset", ctypes.c_uint64),
+        ("text_bytes", ctypes.c_uint64),
+        ("parsed_on_device", ctypes.c_int),
+    ]
+
+
 _vp = ctypes.c_void_p
 _u32 = ctypes.c_uint32
 _u64 = ctypes.c_uint64
@@ -99,6 +117,8 @@ SIGNATURES = {
     "xs_bank_doc_name": (ctypes.c_char_p, [_vp, _u64]),
     "xs_query": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
     "xs_query_hits": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _int, _vp]),
+    "xs_query_hits_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u64, _u32, _vp, _int, _vp, _vp]),
+    "xs_memcpy_to_host": (_int, [_vp, _vp, _u64]),
     "xs_host_alloc": (_int, [_u64, _pp]),
     "xs_host_free": (None, [_vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
@@ -122,6 +142,8 @@ SIGNATURES = {
     "xs_fastx_open_range": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),
     "xs_fastx_close": (None, [_vp]),
+    "xs_fastx_open_device": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
+    "xs_fastx_next_device": (_int, [_vp, _u64, ctypes.POINTER(FastxDBatch)]),
     "xs_write_fasta": (_int, [ctypes.c_char_p, _int, _vp, _vp, ctypes.c_char_p, _vp, _vp, _u64, _u32]),
 }
 

@@ -41,6 +41,15 @@ def bloom_parameters(expected_items: int, fpr: float) -> tuple[int, int]:
     return (max(size_bits, 1) + 7) // 8, nhash
 
 
+def _device_batch(reads) -> bool:
+    """A device-mode reader batch (file_io.DeviceSeqBatch): reads in HBM."""
+    return hasattr(reads, "seqs_ptr")
+
+
+def _kmers_of(length: int, k: int, step: int) -> int:
+    return (length - k) // step + 1 if length >= k else 0
+
+
 def max_kmers(reads: PackedReads, k: int, step: int) -> int:
     """Largest sampled k-mer count ceil((len - k + 1) / step) of a batch."""
     if reads.n == 0:
@@ -217,12 +226,16 @@ class Bank:
         holds the largest per-read k-mer count of the batch, which bounds every
         count.  out: a reusable C-contiguous [n, D] array of that dtype (for
         instance from ``pinned_empty``), filled by DMA without page faults."""
-        pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
+        dev = _device_batch(reads)
+        if dev:
+            reads.check_valid()
+        pr = reads if dev or isinstance(reads, PackedReads) else pack_sequences(reads)
         if step < 1:
             raise ValueError("step must be >= 1")
         cols = self.num_docs
         if isinstance(hit_dtype, str) and hit_dtype == "auto":
-            hit_dtype = narrowest_count_dtype(max_kmers(pr, self.term_size, step))
+            hit_dtype = narrowest_count_dtype(_kmers_of(reads.max_len, self.term_size, step) if dev
+                                              else max_kmers(pr, self.term_size, step))
         hit_dtype = np.dtype(hit_dtype)
         if hit_dtype not in (np.uint8, np.uint16, np.uint32):
             raise ValueError("hit_dtype must be uint8, uint16 or uint32")
@@ -235,12 +248,25 @@ class Bank:
             else:
                 hits = np.empty((pr.n, cols), dtype=hit_dtype)
         nk = np.empty(pr.n, dtype=np.uint64)
-        check(load().xs_query_hits(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
-                                   _ptr(hits) if hits is not None else None, hit_dtype.itemsize, _ptr(nk)))
+        if dev:
+            check(load().xs_query_hits_device(self.handle, pr.seqs_ptr, pr.seq_bytes, pr.offsets_ptr, pr.n,
+                                              pr.max_len, step, _ptr(hits) if hits is not None else None,
+                                              hit_dtype.itemsize, _ptr(nk), None))
+        else:
+            check(load().xs_query_hits(self.handle, _ptr(pr.buf), _ptr(pr.offsets), pr.n, step,
+                                       _ptr(hits) if hits is not None else None, hit_dtype.itemsize, _ptr(nk)))
         return hits, nk
 
     def query_totals(self, reads: PackedReads | Iterable, step: int = 1):
         """(totals [D] uint64, total k-mers) without materialising the hit matrix."""
+        if _device_batch(reads):
+            reads.check_valid()
+            if step < 1:
+                raise ValueError("step must be >= 1")
+            t = np.zeros(self.num_docs + 1, dtype=np.uint64)
+            check(load().xs_query_hits_device(self.handle, reads.seqs_ptr, reads.seq_bytes, reads.offsets_ptr,
+                                              reads.n, reads.max_len, step, None, 4, None, _ptr(t)))
+            return t[:-1].copy(), int(t[-1])
         pr = reads if isinstance(reads, PackedReads) else pack_sequences(reads)
         tot = np.zeros(self.num_docs, dtype=np.uint64)
         nk = ctypes.c_uint64(0)

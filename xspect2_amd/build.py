@@ -10,7 +10,7 @@ PKG = Path(__file__).resolve().parent
 ROOT = PKG.parent
 CSRC = PKG / "csrc"
 SO_PATH = PKG / "libxspect_hip.so"
-SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_json.cpp", CSRC / "xs_kernels.hip",
+SOURCES = [CSRC / "xs_api.cpp", CSRC / "xs_fastx.cpp", CSRC / "xs_fastx_dev.hip", CSRC / "xs_json.cpp", CSRC / "xs_kernels.hip",
            CSRC / "xs_probe_fast.hip", CSRC / "xs_probe_wide.hip", CSRC / "xs_probe_slots.hip",
            CSRC / "xs_probe_general.hip", CSRC / "xs_probe_bloompart.hip",
            CSRC / "xs_probe_cobspart.hip"]

@@ -687,27 +687,47 @@ int host_threads() {
     return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
 }
 
+// Reads already in HBM (a device-mode reader's batch): query_host then only
+// chunks the probe and the hit-row D2H.
+struct DevReads {
+    const uint8_t* seqs;
+    uint64_t seq_bytes;
+    const uint64_t* offs;  // n+1, offs[0] = 0
+};
+constexpr uint64_t kDevChunkReads = 1u << 18;
+
 // hits_host: n x cols rows back on the host (needs d_hits), as hit_bytes-wide
 // counts (4: uint32; 1 / 2: narrowed on the device into b->narrow first, the
 // caller having checked that they fit); tot_host: cols + 1 entries (per-doc
-// sums, then the k-mer total).
+// sums, then the k-mer total).  dev: the reads are on the device (seqs and
+// offsets unused); chunks are then cut by read count.
 int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
-               uint32_t* d_hits, void* hits_host, uint64_t* d_nk, uint64_t* tot_host, int hit_bytes = 4) {
-    const uint64_t base = offsets[0];
-    for (uint64_t r = 0; r < n; ++r)
-        if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
-    const uint64_t bytes = offsets[n] - base;
+               uint32_t* d_hits, void* hits_host, uint64_t* d_nk, uint64_t* tot_host, int hit_bytes = 4,
+               const DevReads* dev = nullptr) {
+    const uint64_t base = dev ? 0 : offsets[0];
+    if (!dev)
+        for (uint64_t r = 0; r < n; ++r)
+            if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    const uint64_t bytes = dev ? dev->seq_bytes : offsets[n] - base;
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     const uint64_t pcols = cols + 1;
     std::vector<uint64_t> cut{0};
-    for (size_t limit = kHostFirst; cut.back() < n; limit = kHostChunk) {
-        const uint64_t r0 = cut.back();
-        uint64_t e = (uint64_t)(std::upper_bound(offsets + r0 + 1, offsets + n + 1, offsets[r0] + limit) - offsets) - 1;
-        cut.push_back(e > r0 ? e : r0 + 1);  // a read over the limit is a chunk of its own
+    if (dev) {
+        const uint64_t per = std::max<uint64_t>(kDevChunkReads, (n + 3) / 4);
+        while (cut.back() < n) cut.push_back(std::min(n, cut.back() + per));
+    } else {
+        for (size_t limit = kHostFirst; cut.back() < n; limit = kHostChunk) {
+            const uint64_t r0 = cut.back();
+            uint64_t e =
+                (uint64_t)(std::upper_bound(offsets + r0 + 1, offsets + n + 1, offsets[r0] + limit) - offsets) - 1;
+            cut.push_back(e > r0 ? e : r0 + 1);  // a read over the limit is a chunk of its own
+        }
     }
     const size_t nc = cut.size() - 1;
-    if (int rc = b->seqs.ensure(bytes + kPad)) return rc;
-    if (int rc = b->offs.ensure((n + 1) * 8)) return rc;
+    if (!dev) {
+        if (int rc = b->seqs.ensure(bytes + kPad)) return rc;
+        if (int rc = b->offs.ensure((n + 1) * 8)) return rc;
+    }
     if (int rc = b->nseg.ensure((n + 1) * 8)) return rc;
     if (int rc = b->unit_ofs.ensure((n + 1) * 8)) return rc;
     if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
@@ -729,11 +749,13 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         b->chunk_ev.push_back(e);
     }
-    uint8_t* d_seqs = b->seqs.as<uint8_t>();
-    uint64_t* d_offs = b->offs.as<uint64_t>();
-    std::vector<uint64_t> rebased(n + 1);
-    for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
-    HIPCHK(hipMemcpyAsync(d_offs, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
+    const uint8_t* d_seqs = dev ? dev->seqs : b->seqs.as<uint8_t>();
+    const uint64_t* d_offs = dev ? dev->offs : b->offs.as<uint64_t>();
+    std::vector<uint64_t> rebased(dev ? 0 : n + 1);
+    if (!dev) {
+        for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
+        HIPCHK(hipMemcpyAsync(b->offs.p, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
+    }
     const int threads = host_threads();
     auto drain = [&](size_t j) -> int {  // chunk j's hit rows to the host
         const uint64_t r0 = cut[j], m = cut[j + 1] - cut[j];
@@ -746,19 +768,22 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     bool used[2] = {false, false};
     for (size_t i = 0; i < nc; ++i) {
         const uint64_t r0 = cut[i], r1 = cut[i + 1];
-        const uint64_t o0 = offsets[r0] - base, o1 = offsets[r1] - base, nb = o1 - o0;
-        const int slot = (int)(i & 1);
-        if (used[slot]) HIPCHK(hipEventSynchronize(b->hstage_ev[slot]));  // the slot's last H2D is done
-        if (nb && nb <= kHostChunk) {
-            par_memcpy(b->hstage[slot].p, seqs + base + o0, nb, threads);
-            HIPCHK(hipMemcpyAsync(d_seqs + o0, b->hstage[slot].p, nb, hipMemcpyHostToDevice, b->copy_stream));
-        } else if (nb) {  // one read larger than a slot
-            HIPCHK(hipMemcpyAsync(d_seqs + o0, seqs + base + o0, nb, hipMemcpyHostToDevice, b->copy_stream));
+        if (!dev) {
+            const uint64_t o0 = offsets[r0] - base, o1 = offsets[r1] - base, nb = o1 - o0;
+            const int slot = (int)(i & 1);
+            uint8_t* stage_dst = b->seqs.as<uint8_t>() + o0;
+            if (used[slot]) HIPCHK(hipEventSynchronize(b->hstage_ev[slot]));  // the slot's last H2D is done
+            if (nb && nb <= kHostChunk) {
+                par_memcpy(b->hstage[slot].p, seqs + base + o0, nb, threads);
+                HIPCHK(hipMemcpyAsync(stage_dst, b->hstage[slot].p, nb, hipMemcpyHostToDevice, b->copy_stream));
+            } else if (nb) {  // one read larger than a slot
+                HIPCHK(hipMemcpyAsync(stage_dst, seqs + base + o0, nb, hipMemcpyHostToDevice, b->copy_stream));
+            }
+            HIPCHK(hipEventRecord(b->hstage_ev[slot], b->copy_stream));
+            used[slot] = true;
+            HIPCHK(hipStreamWaitEvent(b->stream, b->hstage_ev[slot], 0));
         }
-        HIPCHK(hipEventRecord(b->hstage_ev[slot], b->copy_stream));
-        used[slot] = true;
-        HIPCHK(hipStreamWaitEvent(b->stream, b->hstage_ev[slot], 0));
-        const Inputs in{d_seqs, o1, d_offs + r0, r1 - r0};
+        const Inputs in{d_seqs, dev ? bytes : offsets[r1] - base, d_offs + r0, r1 - r0};
         if (int rc = run_query(b, in, step, d_hits ? d_hits + r0 * cols : nullptr, d_nk ? d_nk + r0 : nullptr,
                                tot_host ? b->totals.as<uint64_t>() + i * pcols : nullptr, b->stream))
             return rc;
@@ -1078,6 +1103,50 @@ int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, 
 int xs_query_hits(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                   void* hits_out, int hit_bytes, uint64_t* num_kmers_out) {
     return query_impl(b, seqs, offsets, n, step, hits_out, hit_bytes, num_kmers_out);
+}
+
+int xs_query_hits_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, const uint64_t* d_offsets, uint64_t n,
+                         uint64_t max_len, uint32_t step, void* hits_out, int hit_bytes, uint64_t* num_kmers_out,
+                         uint64_t* totals_out) {
+    if (!b || (n && (!d_seqs || !d_offsets))) return fail(XS_ERR_ARG, "null argument");
+    if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
+    if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
+    if (hits_out && hit_bytes != 4) {
+        const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
+        const uint64_t nk = max_len >= b->k ? (max_len - b->k) / step + 1 : 0;
+        if (nk > cap)
+            return fail(XS_ERR_ARG, "a read has %llu sampled k-mers: counts may not fit %d byte(s)",
+                        (unsigned long long)nk, hit_bytes);
+    }
+    std::lock_guard<std::mutex> lk(b->mu);
+    HIPCHK(hipSetDevice(b->device));
+    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+    if (n == 0) {
+        if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
+        return XS_OK;
+    }
+    uint32_t* d_hits = nullptr;
+    if (hits_out) {
+        if (int rc = b->hits.ensure(n * cols * 4)) return rc;
+        d_hits = b->hits.as<uint32_t>();
+    }
+    if (num_kmers_out)
+        if (int rc = b->nk.ensure(n * 8)) return rc;
+    std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
+    const DevReads dev{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets};
+    if (int rc = query_host(b, nullptr, nullptr, n, step, d_hits, hits_out, num_kmers_out ? b->nk.as<uint64_t>() : nullptr,
+                            totals_out ? tot.data() : nullptr, hit_bytes, &dev))
+        return rc;
+    if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
+    HIPCHK(hipStreamSynchronize(b->stream));
+    if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
+    return XS_OK;
+}
+
+int xs_memcpy_to_host(void* host, const void* dev, uint64_t bytes) {
+    if (bytes && (!host || !dev)) return fail(XS_ERR_ARG, "null argument");
+    if (bytes) HIPCHK(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+    return XS_OK;
 }
 
 int xs_host_alloc(uint64_t bytes, void** out) {

@@ -23,6 +23,12 @@
 // can probe batch i while batch i+1 is parsed.  FASTQ with wrapped sequence
 // or quality lines cannot be split safely; such files are parsed by one
 // thread.
+//
+// Device mode (xs_fastx_open_device): the host only copies each window's text
+// into pinned memory (parallel pread) and on to HBM, overlapped with the
+// caller's work on the previous batch; the records are found on the GPU
+// (xs_fastx_dev.hip).  A window the device rules do not cover is parsed here
+// instead, so both modes yield the same batches.
 #include "../../include/xspect_hip.h"
 
 #include <hip/hip_runtime.h>
@@ -33,9 +39,11 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -346,6 +354,115 @@ struct Batch {
     uint64_t n = 0, seq_bytes = 0;
 };
 
+// ---- device mode -------------------------------------------------------------
+// Pinned host buffers outlive their reader in a small process-wide pool: a
+// hipHostMalloc of a few hundred MiB costs tens of ms, more than a window's
+// whole parse.
+std::mutex g_pin_mu;
+std::vector<std::pair<void*, size_t>> g_pin_pool;
+constexpr size_t kPinPoolMax = 4;
+
+struct PinBuf {
+    char* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {  // contents are not preserved
+        if (bytes <= cap && p) return XS_OK;
+        release();
+        {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            size_t best = g_pin_pool.size();
+            for (size_t i = 0; i < g_pin_pool.size(); ++i)
+                if (g_pin_pool[i].second >= bytes && (best == g_pin_pool.size() || g_pin_pool[i].second < g_pin_pool[best].second))
+                    best = i;
+            if (best < g_pin_pool.size()) {
+                p = static_cast<char*>(g_pin_pool[best].first);
+                cap = g_pin_pool[best].second;
+                g_pin_pool.erase(g_pin_pool.begin() + (ptrdiff_t)best);
+                return XS_OK;
+            }
+        }
+        const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+        if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
+            p = nullptr;
+            return xs::set_error(XS_ERR_HIP, "hipHostMalloc failed for the device reader");
+        }
+        cap = want;
+        return XS_OK;
+    }
+    void release() {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        if (g_pin_pool.size() < kPinPoolMax) {
+            g_pin_pool.emplace_back(p, cap);
+        } else {
+            (void)hipHostFree(p);
+        }
+        p = nullptr;
+        cap = 0;
+    }
+    ~PinBuf() { release(); }
+};
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {  // contents are not preserved
+        if (bytes <= cap && p) return XS_OK;
+        release();
+        const size_t want = std::max<size_t>(bytes + bytes / 8, 4096);
+        if (hipMalloc(&p, want) != hipSuccess) {
+            p = nullptr;
+            return xs::set_error(XS_ERR_HIP, "hipMalloc failed for the device reader");
+        }
+        cap = want;
+        return XS_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+    ~DBuf() { release(); }
+};
+
+constexpr size_t kPieceBytes = 4u << 20;  // pread + DMA unit of a window's text
+constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
+
+struct DevSide {
+    int device = 0;
+    hipStream_t stream = nullptr;  // parse kernels
+    hipStream_t copy = nullptr;    // text DMA
+    hipEvent_t text_ev = nullptr;
+    PinBuf pin;         // the window's text
+    PinBuf status;      // small D2H results
+    DBuf text;          // the window's text, zero-padded to whole tiles
+    DBuf tiles, tile_ofs, nl, temp, flag;
+    DBuf hdr, hofs, line_src, line_len, line_ofs, rec_line, lens, maxlen;
+    DBuf seq_src, seq_len, id_src, id_len, desc_src, desc_len, id_ofs, desc_ofs, ids_d, descs_d;
+    DBuf seqs[2], offs[2];
+    PinBuf ids[2], id_offs[2], descs[2], desc_offs[2], hoffs[2];
+    int flip = 0;
+    // text of the next window, loaded by `worker` while the caller works
+    std::thread worker;
+    bool pending = false;
+    size_t pf_lo = 0, pf_hi = 0;
+    int pf_rc = XS_OK;
+    std::string pf_err;
+    ~DevSide() {
+        if (worker.joinable()) worker.join();
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        if (copy) (void)hipStreamSynchronize(copy);
+        if (text_ev) (void)hipEventDestroy(text_ev);
+        if (stream) (void)hipStreamDestroy(stream);
+        if (copy) (void)hipStreamDestroy(copy);
+    }
+};
+
 }  // namespace
 
 struct xs_fastx {
@@ -361,11 +478,364 @@ struct xs_fastx {
     Batch batch[2];
     int flip = 0;
     std::vector<Part> parts;
+    DevSide* dev = nullptr;
     ~xs_fastx() {
+        delete dev;
         if (base && size) munmap(const_cast<char*>(base), size);
         if (fd >= 0) close(fd);
     }
 };
+
+namespace {
+
+// End of the window that starts at lo: the first record start at or after
+// lo + budget (the whole rest if that is within budget; one record at least).
+const char* window_end(const xs_fastx* r, const char* lo, const char* end, size_t budget) {
+    auto boundary = r->format == XS_FASTX_FASTA ? fasta_boundary : fastq_boundary;
+    const char* hi = (size_t)(end - lo) <= budget ? end : boundary(lo, lo + budget, end);
+    if (hi == lo) hi = boundary(lo, lo + 1, end);  // one record larger than the budget
+    return hi;
+}
+
+// Parse [lo, hi) (cut at record starts) on up to r->threads threads into r->parts.
+int parse_window(xs_fastx* r, const char* lo, const char* hi, int* nparts) {
+    const bool fasta = r->format == XS_FASTX_FASTA;
+    auto boundary = fasta ? fasta_boundary : fastq_boundary;
+    const size_t span = (size_t)(hi - lo);
+    const int T = (int)std::min<size_t>((size_t)r->threads, std::max<size_t>(1, span >> 20));  // >= 1 MiB per part
+    std::vector<const char*> cut(T + 1);
+    cut[0] = lo;
+    cut[T] = hi;
+    for (int i = 1; i < T; ++i) cut[i] = std::max(cut[i - 1], boundary(lo, lo + span * i / T, hi));
+    auto work = [&](int i) {
+        Part& pt = r->parts[i];
+        pt.clear();
+        if (cut[i] < cut[i + 1]) {
+            if (fasta) parse_fasta(cut[i], cut[i + 1], 0, pt);
+            else parse_fastq(cut[i], cut[i + 1], 0, pt);
+        } else {
+            pt.stop = cut[i + 1];
+        }
+    };
+    std::vector<std::thread> th;
+    for (int i = 1; i < T; ++i) th.emplace_back(work, i);
+    work(0);
+    for (auto& x : th) x.join();
+    r->parts[T - 1].stop = hi;
+    *nparts = T;
+    for (int i = 0; i < T; ++i)
+        if (!r->parts[i].err.empty()) return xs::set_error(XS_ERR_FORMAT, r->parts[i].err.c_str());
+    return XS_OK;
+}
+
+// Concatenate r->parts[0 .. nparts) into bt (the layout xs_query takes).
+int pack_parts(xs_fastx* r, Batch& bt, int nparts) {
+    uint64_t n = 0, sbytes = 0, ibytes = 0, dbytes = 0;
+    for (int i = 0; i < nparts; ++i) {
+        n += r->parts[i].lens.size();
+        sbytes += r->parts[i].seq.size();
+        ibytes += r->parts[i].ids.size();
+        dbytes += r->parts[i].descs.size();
+    }
+    if (int rc = bt.seqs.ensure(sbytes + 64)) return rc;
+    if (int rc = bt.offs.ensure((n + 1) * 8)) return rc;
+    if (int rc = bt.ids.ensure(ibytes + 1)) return rc;
+    if (int rc = bt.id_offs.ensure((n + 1) * 8)) return rc;
+    if (int rc = bt.descs.ensure(dbytes + 1)) return rc;
+    if (int rc = bt.desc_offs.ensure((n + 1) * 8)) return rc;
+    auto* offs = reinterpret_cast<uint64_t*>(bt.offs.p);
+    auto* ioffs = reinterpret_cast<uint64_t*>(bt.id_offs.p);
+    auto* doffs = reinterpret_cast<uint64_t*>(bt.desc_offs.p);
+    std::vector<uint64_t> rec0(nparts + 1, 0), s0(nparts + 1, 0), i0(nparts + 1, 0), d0(nparts + 1, 0);
+    for (int i = 0; i < nparts; ++i) {
+        rec0[i + 1] = rec0[i] + r->parts[i].lens.size();
+        s0[i + 1] = s0[i] + r->parts[i].seq.size();
+        i0[i + 1] = i0[i] + r->parts[i].ids.size();
+        d0[i + 1] = d0[i] + r->parts[i].descs.size();
+    }
+    auto pack = [&](int i) {
+        const Part& pt = r->parts[i];
+        if (!pt.seq.empty()) memcpy(bt.seqs.p + s0[i], pt.seq.data(), pt.seq.size());
+        if (!pt.ids.empty()) memcpy(bt.ids.p + i0[i], pt.ids.data(), pt.ids.size());
+        if (!pt.descs.empty()) memcpy(bt.descs.p + d0[i], pt.descs.data(), pt.descs.size());
+        uint64_t so = s0[i], io = i0[i], dd = d0[i];
+        for (size_t j = 0; j < pt.lens.size(); ++j) {
+            offs[rec0[i] + j] = so;
+            ioffs[rec0[i] + j] = io;
+            doffs[rec0[i] + j] = dd;
+            so += pt.lens[j];
+            io += pt.id_lens[j];
+            dd += pt.desc_lens[j];
+        }
+    };
+    {
+        std::vector<std::thread> th;
+        for (int i = 1; i < nparts; ++i) th.emplace_back(pack, i);
+        if (nparts) pack(0);
+        for (auto& x : th) x.join();
+    }
+    offs[n] = sbytes;
+    ioffs[n] = ibytes;
+    doffs[n] = dbytes;
+    memset(bt.seqs.p + sbytes, 0, 64);  // defined bytes past the end
+    bt.n = n;
+    bt.seq_bytes = sbytes;
+    return XS_OK;
+}
+
+void fill_host_batch(const xs_fastx* r, const Batch& bt, xs_fastx_batch* out) {
+    out->n = bt.n;
+    out->seqs = bt.seqs.p;
+    out->seq_bytes = bt.seq_bytes;
+    out->offsets = reinterpret_cast<const uint64_t*>(bt.offs.p);
+    out->ids = bt.ids.p;
+    out->id_offsets = reinterpret_cast<const uint64_t*>(bt.id_offs.p);
+    out->text_offset = r->cur;
+    out->text_bytes = r->stop;
+    out->descs = bt.descs.p;
+    out->desc_offsets = reinterpret_cast<const uint64_t*>(bt.desc_offs.p);
+}
+
+#define FXCHK(expr)                                                                                     \
+    do {                                                                                                \
+        hipError_t _e = (expr);                                                                         \
+        if (_e != hipSuccess) return xs::set_error(XS_ERR_HIP, hipGetErrorString(_e));                 \
+    } while (0)
+
+// The text of [lo, hi) (file offsets) into d.pin and on to d.text (zero-padded
+// to whole tiles), piece by piece: host threads pread the pieces, the DMA of
+// each piece is queued on d.copy as soon as it is in.  d.text_ev marks the end.
+int load_text(xs_fastx* r, size_t lo, size_t hi) {
+    DevSide& d = *r->dev;
+    FXCHK(hipSetDevice(d.device));
+    const size_t span = hi - lo;
+    const size_t tiles = std::max<size_t>(1, (span + xs::kFxTile - 1) / xs::kFxTile);
+    const size_t padded = tiles * xs::kFxTile;
+    if (int rc = d.pin.ensure(span + 1)) return rc;
+    if (int rc = d.text.ensure(padded + 16)) return rc;
+    const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
+    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)r->threads, pieces));
+    std::vector<std::atomic<int>> done(pieces);
+    for (auto& x : done) x.store(0);
+    std::atomic<bool> failed{false};
+    auto work = [&](int t) {
+        for (size_t p = (size_t)t; p < pieces; p += (size_t)T) {
+            size_t o = p * kPieceBytes;
+            const size_t e = std::min(span, o + kPieceBytes);
+            while (o < e) {
+                const ssize_t got = pread(r->fd, d.pin.p + o, e - o, (off_t)(lo + o));
+                if (got <= 0) {
+                    failed.store(true);
+                    break;
+                }
+                o += (size_t)got;
+            }
+            done[p].store(1, std::memory_order_release);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+    int rc = XS_OK;
+    for (size_t p = 0; p < pieces; ++p) {
+        while (!done[p].load(std::memory_order_acquire)) std::this_thread::yield();
+        if (failed.load()) break;
+        const size_t o = p * kPieceBytes, n = std::min(span, o + kPieceBytes) - o;
+        hipError_t e = hipMemcpyAsync(d.text.as<char>() + o, d.pin.p + o, n, hipMemcpyHostToDevice, d.copy);
+        if (e != hipSuccess) {
+            rc = xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
+            break;
+        }
+    }
+    for (auto& x : th) x.join();
+    if (rc) return rc;
+    if (failed.load()) return xs::set_error(XS_ERR_IO, "read failed while loading the window's text");
+    FXCHK(hipMemsetAsync(d.text.as<char>() + span, 0, padded + 16 - span, d.copy));
+    FXCHK(hipEventRecord(d.text_ev, d.copy));
+    return XS_OK;
+}
+
+void start_prefetch(xs_fastx* r, size_t lo, size_t hi) {
+    DevSide& d = *r->dev;
+    d.pending = true;
+    d.pf_lo = lo;
+    d.pf_hi = hi;
+    d.worker = std::thread([r, lo, hi] {
+        DevSide& dd = *r->dev;
+        dd.pf_rc = load_text(r, lo, hi);
+        if (dd.pf_rc) dd.pf_err = xs_last_error();
+    });
+}
+
+// Wait for the text of [lo, hi) to be queued for d.text (loading it now if no
+// prefetch of exactly that window is pending).
+int text_for(xs_fastx* r, size_t lo, size_t hi) {
+    DevSide& d = *r->dev;
+    if (d.pending) {
+        d.worker.join();
+        d.pending = false;
+        if (d.pf_lo == lo && d.pf_hi == hi) {
+            if (d.pf_rc) return xs::set_error(d.pf_rc, d.pf_err.c_str());
+            return XS_OK;
+        }
+    }
+    return load_text(r, lo, hi);
+}
+
+// Record finding on the device for the window [lo, hi) whose text is queued
+// for d.text.  *ok = false: the window needs the host parser (nothing of the
+// batch is kept).  On success the batch is in slot `slot` and `out` is filled.
+int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fastx_dbatch* out) {
+    DevSide& d = *r->dev;
+    *ok = false;
+    const size_t span = hi - lo;
+    if (span == 0 || span >= (1ull << 31) - xs::kFxTile) return XS_OK;  // u32 positions, int scan sizes
+    const hipStream_t s = d.stream;
+    FXCHK(hipStreamWaitEvent(s, d.text_ev, 0));
+    const uint64_t tiles = (span + xs::kFxTile - 1) / xs::kFxTile;
+    if (int rc = d.tiles.ensure((tiles + 1) * 8)) return rc;
+    if (int rc = d.tile_ofs.ensure((tiles + 1) * 8)) return rc;
+    if (int rc = d.status.ensure(64)) return rc;
+    if (int rc = d.flag.ensure(8)) return rc;
+    size_t tb = xs::fx_temp_bytes(tiles + 1);
+    if (int rc = d.temp.ensure(tb)) return rc;
+    auto* st = reinterpret_cast<uint64_t*>(d.status.p);
+    FXCHK(xs::launch_fx_count(d.text.as<uint8_t>(), tiles, d.tiles.as<uint64_t>(), s));
+    FXCHK(hipMemsetAsync(d.tiles.as<uint64_t>() + tiles, 0, 8, s));
+    FXCHK(xs::launch_scan(d.temp.p, tb, d.tiles.as<uint64_t>(), d.tile_ofs.as<uint64_t>(), tiles + 1, s));
+    FXCHK(hipMemcpyAsync(st, d.tile_ofs.as<uint64_t>() + tiles, 8, hipMemcpyDeviceToHost, s));
+    FXCHK(hipStreamSynchronize(s));
+    const uint64_t newlines = st[0];
+    const bool tail = r->base[hi - 1] != '\n';  // a last line without '\n' ends at hi
+    const uint64_t L = newlines + (tail ? 1 : 0);
+    const bool fasta = r->format == XS_FASTX_FASTA;
+    if (!fasta && (L == 0 || L % 4)) return XS_OK;
+    const uint64_t nmax = fasta ? L : L / 4;  // records, or an upper bound of them
+    if (int rc = d.nl.ensure(L * 4 + 4)) return rc;
+    tb = xs::fx_temp_bytes((fasta ? L : nmax) + 1);
+    if (int rc = d.temp.ensure(tb)) return rc;
+    FXCHK(xs::launch_fx_positions(d.text.as<uint8_t>(), tiles, d.tile_ofs.as<uint64_t>(), d.nl.as<uint32_t>(), s));
+    if (tail) FXCHK(hipMemsetD32Async(d.nl.as<uint32_t>() + newlines, (int)span, 1, s));
+    FXCHK(hipMemsetAsync(d.flag.p, 0, 4, s));
+    for (DBuf* b : {&d.seq_src, &d.id_src, &d.desc_src})
+        if (int rc = b->ensure((nmax + 1) * 4)) return rc;
+    for (DBuf* b : {&d.seq_len, &d.id_len, &d.desc_len, &d.id_ofs, &d.desc_ofs})
+        if (int rc = b->ensure((nmax + 1) * 8)) return rc;
+    if (int rc = d.offs[slot].ensure((nmax + 1) * 8)) return rc;
+    if (int rc = d.maxlen.ensure(8)) return rc;
+    const xs::FxRuns runs{d.seq_src.as<uint32_t>(), d.seq_len.as<uint64_t>(), d.id_src.as<uint32_t>(),
+                          d.id_len.as<uint64_t>(), d.desc_src.as<uint32_t>(), d.desc_len.as<uint64_t>()};
+    uint64_t* offs = d.offs[slot].as<uint64_t>();
+    const uint8_t* text = d.text.as<uint8_t>();
+    const uint32_t* nl = d.nl.as<uint32_t>();
+    // status: [0] bad, [1] records, [2] sequence bytes, [3] id bytes, [4] title bytes, [5] longest record
+    if (fasta) {
+        for (DBuf* b : {&d.hdr, &d.hofs, &d.line_len, &d.line_ofs, &d.lens})
+            if (int rc = b->ensure((L + 1) * 8)) return rc;
+        for (DBuf* b : {&d.line_src, &d.rec_line})
+            if (int rc = b->ensure((L + 1) * 4)) return rc;
+        // records past the last header keep zero-length ids and titles
+        FXCHK(hipMemsetAsync(d.id_len.p, 0, (L + 1) * 8, s));
+        FXCHK(hipMemsetAsync(d.desc_len.p, 0, (L + 1) * 8, s));
+        FXCHK(hipMemsetAsync(d.lens.p, 0, (L + 1) * 8, s));
+        FXCHK(xs::launch_fa_headers(text, nl, L, d.hdr.as<uint64_t>(), s));
+        FXCHK(hipMemsetAsync(d.hdr.as<uint64_t>() + L, 0, 8, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.hdr.as<uint64_t>(), d.hofs.as<uint64_t>(), L + 1, s));
+        FXCHK(xs::launch_fa_lines(text, nl, L, d.hofs.as<uint64_t>(), d.line_src.as<uint32_t>(),
+                                  d.line_len.as<uint64_t>(), d.rec_line.as<uint32_t>(), runs, d.flag.as<uint32_t>(), s));
+        FXCHK(hipMemsetAsync(d.line_len.as<uint64_t>() + L, 0, 8, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.line_len.as<uint64_t>(), d.line_ofs.as<uint64_t>(), L + 1, s));
+        FXCHK(xs::launch_fa_offsets(d.rec_line.as<uint32_t>(), d.line_ofs.as<uint64_t>(), L,
+                                    d.hofs.as<uint64_t>() + L, offs, d.lens.as<uint64_t>(), s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.id_len.as<uint64_t>(), d.id_ofs.as<uint64_t>(), L + 1, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.desc_len.as<uint64_t>(), d.desc_ofs.as<uint64_t>(), L + 1, s));
+        FXCHK(xs::launch_max_u64(d.temp.p, tb, d.lens.as<uint64_t>(), L, d.maxlen.as<uint64_t>(), s));
+        FXCHK(hipMemcpyAsync(st + 1, d.hofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 2, d.line_ofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 3, d.id_ofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 4, d.desc_ofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
+    } else {
+        const uint64_t n = nmax;
+        FXCHK(xs::launch_fq_records(text, nl, n, runs, d.flag.as<uint32_t>(), s));
+        for (DBuf* b : {&d.seq_len, &d.id_len, &d.desc_len}) FXCHK(hipMemsetAsync(b->as<uint64_t>() + n, 0, 8, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.seq_len.as<uint64_t>(), offs, n + 1, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.id_len.as<uint64_t>(), d.id_ofs.as<uint64_t>(), n + 1, s));
+        FXCHK(xs::launch_scan(d.temp.p, tb, d.desc_len.as<uint64_t>(), d.desc_ofs.as<uint64_t>(), n + 1, s));
+        FXCHK(xs::launch_max_u64(d.temp.p, tb, d.seq_len.as<uint64_t>(), n, d.maxlen.as<uint64_t>(), s));
+        st[1] = n;
+        FXCHK(hipMemcpyAsync(st + 2, offs + n, 8, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 3, d.id_ofs.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 4, d.desc_ofs.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+    }
+    st[0] = 0;
+    FXCHK(hipMemcpyAsync(st, d.flag.p, 4, hipMemcpyDeviceToHost, s));
+    FXCHK(hipMemcpyAsync(st + 5, d.maxlen.p, 8, hipMemcpyDeviceToHost, s));
+    FXCHK(hipStreamSynchronize(s));
+    if ((uint32_t)st[0]) return XS_OK;
+    const uint64_t n = st[1], sbytes = st[2], ibytes = st[3], dbytes = st[4];
+    if (int rc = d.seqs[slot].ensure(sbytes + kDevPad)) return rc;
+    if (int rc = d.ids_d.ensure(ibytes + 1)) return rc;
+    if (int rc = d.descs_d.ensure(dbytes + 1)) return rc;
+    if (int rc = d.ids[slot].ensure(ibytes + 1)) return rc;
+    if (int rc = d.descs[slot].ensure(dbytes + 1)) return rc;
+    if (int rc = d.id_offs[slot].ensure((n + 1) * 8)) return rc;
+    if (int rc = d.desc_offs[slot].ensure((n + 1) * 8)) return rc;
+    if (int rc = d.hoffs[slot].ensure((n + 1) * 8)) return rc;
+    uint8_t* seqs = d.seqs[slot].as<uint8_t>();
+    if (fasta) FXCHK(xs::launch_fx_copy(text, d.line_src.as<uint32_t>(), d.line_ofs.as<uint64_t>(), L, seqs, s));
+    else FXCHK(xs::launch_fx_copy(text, d.seq_src.as<uint32_t>(), offs, n, seqs, s));
+    FXCHK(hipMemsetAsync(seqs + sbytes, 0, kDevPad, s));
+    FXCHK(xs::launch_fx_copy(text, d.id_src.as<uint32_t>(), d.id_ofs.as<uint64_t>(), n, d.ids_d.as<uint8_t>(), s));
+    FXCHK(xs::launch_fx_copy(text, d.desc_src.as<uint32_t>(), d.desc_ofs.as<uint64_t>(), n,
+                             d.descs_d.as<uint8_t>(), s));
+    if (ibytes) FXCHK(hipMemcpyAsync(d.ids[slot].p, d.ids_d.p, ibytes, hipMemcpyDeviceToHost, s));
+    if (dbytes) FXCHK(hipMemcpyAsync(d.descs[slot].p, d.descs_d.p, dbytes, hipMemcpyDeviceToHost, s));
+    FXCHK(hipMemcpyAsync(d.id_offs[slot].p, d.id_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    FXCHK(hipMemcpyAsync(d.desc_offs[slot].p, d.desc_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    FXCHK(hipMemcpyAsync(d.hoffs[slot].p, offs, (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    FXCHK(hipStreamSynchronize(s));
+    *ok = true;
+    out->n = n;
+    out->seq_bytes = sbytes;
+    out->seqs = seqs;
+    out->offsets = offs;
+    out->host_offsets = reinterpret_cast<const uint64_t*>(d.hoffs[slot].p);
+    out->max_len = st[5];
+    out->ids = d.ids[slot].p;
+    out->id_offsets = reinterpret_cast<const uint64_t*>(d.id_offs[slot].p);
+    out->descs = d.descs[slot].p;
+    out->desc_offsets = reinterpret_cast<const uint64_t*>(d.desc_offs[slot].p);
+    out->parsed_on_device = 1;
+    return XS_OK;
+}
+
+// A host batch into device slot `slot` (the host parser's result for a window
+// the device rules do not cover, or a wrapped FASTQ file's batch).
+int upload_host_batch(xs_fastx* r, const xs_fastx_batch& hb, int slot, xs_fastx_dbatch* out) {
+    DevSide& d = *r->dev;
+    if (int rc = d.seqs[slot].ensure(hb.seq_bytes + kDevPad)) return rc;
+    if (int rc = d.offs[slot].ensure((hb.n + 1) * 8)) return rc;
+    uint8_t* seqs = d.seqs[slot].as<uint8_t>();
+    if (hb.seq_bytes) FXCHK(hipMemcpyAsync(seqs, hb.seqs, hb.seq_bytes, hipMemcpyHostToDevice, d.stream));
+    FXCHK(hipMemsetAsync(seqs + hb.seq_bytes, 0, kDevPad, d.stream));
+    FXCHK(hipMemcpyAsync(d.offs[slot].p, hb.offsets, (hb.n + 1) * 8, hipMemcpyHostToDevice, d.stream));
+    FXCHK(hipStreamSynchronize(d.stream));
+    uint64_t mx = 0;
+    for (uint64_t i = 0; i < hb.n; ++i) mx = std::max(mx, hb.offsets[i + 1] - hb.offsets[i]);
+    out->n = hb.n;
+    out->seq_bytes = hb.seq_bytes;
+    out->seqs = seqs;
+    out->offsets = d.offs[slot].as<uint64_t>();
+    out->host_offsets = hb.offsets;
+    out->max_len = mx;
+    out->ids = hb.ids;
+    out->id_offsets = hb.id_offsets;
+    out->descs = hb.descs;
+    out->desc_offsets = hb.desc_offsets;
+    out->parsed_on_device = 0;
+    return XS_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -445,114 +915,109 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     // a window can hold no record (text before the first one): go on until
     // records are found or the file ends
     for (;;) {
-    const char* lo = r->base + r->cur;
-    nparts = 0;
-    if (lo < end) {
-        const bool fasta = r->format == XS_FASTX_FASTA;
-        if (!fasta && r->wrapped) {
-            // sequential: the parser itself stops at the first record past the budget
-            Part& pt = r->parts[0];
-            pt.clear();
-            parse_fastq(lo, end, budget, pt);
-            nparts = 1;
-        } else {
-            auto boundary = fasta ? fasta_boundary : fastq_boundary;
-            const char* hi = (size_t)(end - lo) <= budget ? end : boundary(lo, lo + budget, end);
-            if (hi == lo) hi = boundary(lo, lo + 1, end);  // one record larger than the budget
-            const size_t span = (size_t)(hi - lo);
-            int T = (int)std::min<size_t>((size_t)r->threads, std::max<size_t>(1, span >> 20));  // >= 1 MiB per part
-            std::vector<const char*> cut(T + 1);
-            cut[0] = lo;
-            cut[T] = hi;
-            for (int i = 1; i < T; ++i) cut[i] = std::max(cut[i - 1], boundary(lo, lo + span * i / T, hi));
-            auto work = [&](int i) {
-                Part& pt = r->parts[i];
+        const char* lo = r->base + r->cur;
+        nparts = 0;
+        if (lo < end) {
+            if (r->format == XS_FASTX_FASTQ && r->wrapped) {
+                // sequential: the parser itself stops at the first record past the budget
+                Part& pt = r->parts[0];
                 pt.clear();
-                if (cut[i] < cut[i + 1]) {
-                    if (fasta) parse_fasta(cut[i], cut[i + 1], 0, pt);
-                    else parse_fastq(cut[i], cut[i + 1], 0, pt);
-                } else {
-                    pt.stop = cut[i + 1];
-                }
-            };
-            std::vector<std::thread> th;
-            for (int i = 1; i < T; ++i) th.emplace_back(work, i);
-            work(0);
-            for (auto& x : th) x.join();
-            r->parts[T - 1].stop = hi;
-            nparts = T;
+                parse_fastq(lo, end, budget, pt);
+                nparts = 1;
+                if (!pt.err.empty()) return xs::set_error(XS_ERR_FORMAT, pt.err.c_str());
+            } else if (int rc = parse_window(r, lo, window_end(r, lo, end, budget), &nparts)) {
+                return rc;
+            }
         }
-        for (int i = 0; i < nparts; ++i)
-            if (!r->parts[i].err.empty()) return xs::set_error(XS_ERR_FORMAT, r->parts[i].err.c_str());
+        if (nparts) r->cur = (size_t)(r->parts[nparts - 1].stop - r->base);
+        size_t got = 0;
+        for (int i = 0; i < nparts; ++i) got += r->parts[i].lens.size();
+        if (got || r->cur >= r->stop || !nparts) break;
     }
-    if (nparts) r->cur = (size_t)(r->parts[nparts - 1].stop - r->base);
-    size_t got = 0;
-    for (int i = 0; i < nparts; ++i) got += r->parts[i].lens.size();
-    if (got || r->cur >= r->stop || !nparts) break;
-    }
-    // pack the parts
-    uint64_t n = 0, sbytes = 0, ibytes = 0, dbytes = 0;
-    for (int i = 0; i < nparts; ++i) {
-        n += r->parts[i].lens.size();
-        sbytes += r->parts[i].seq.size();
-        ibytes += r->parts[i].ids.size();
-        dbytes += r->parts[i].descs.size();
-    }
-    if (int rc = bt.seqs.ensure(sbytes + 64)) return rc;
-    if (int rc = bt.offs.ensure((n + 1) * 8)) return rc;
-    if (int rc = bt.ids.ensure(ibytes + 1)) return rc;
-    if (int rc = bt.id_offs.ensure((n + 1) * 8)) return rc;
-    if (int rc = bt.descs.ensure(dbytes + 1)) return rc;
-    if (int rc = bt.desc_offs.ensure((n + 1) * 8)) return rc;
-    auto* offs = reinterpret_cast<uint64_t*>(bt.offs.p);
-    auto* ioffs = reinterpret_cast<uint64_t*>(bt.id_offs.p);
-    auto* doffs = reinterpret_cast<uint64_t*>(bt.desc_offs.p);
-    std::vector<uint64_t> rec0(nparts + 1, 0), s0(nparts + 1, 0), i0(nparts + 1, 0), d0(nparts + 1, 0);
-    for (int i = 0; i < nparts; ++i) {
-        rec0[i + 1] = rec0[i] + r->parts[i].lens.size();
-        s0[i + 1] = s0[i] + r->parts[i].seq.size();
-        i0[i + 1] = i0[i] + r->parts[i].ids.size();
-        d0[i + 1] = d0[i] + r->parts[i].descs.size();
-    }
-    auto pack = [&](int i) {
-        const Part& pt = r->parts[i];
-        if (!pt.seq.empty()) memcpy(bt.seqs.p + s0[i], pt.seq.data(), pt.seq.size());
-        if (!pt.ids.empty()) memcpy(bt.ids.p + i0[i], pt.ids.data(), pt.ids.size());
-        if (!pt.descs.empty()) memcpy(bt.descs.p + d0[i], pt.descs.data(), pt.descs.size());
-        uint64_t so = s0[i], io = i0[i], dd = d0[i];
-        for (size_t j = 0; j < pt.lens.size(); ++j) {
-            offs[rec0[i] + j] = so;
-            ioffs[rec0[i] + j] = io;
-            doffs[rec0[i] + j] = dd;
-            so += pt.lens[j];
-            io += pt.id_lens[j];
-            dd += pt.desc_lens[j];
-        }
-    };
-    {
-        std::vector<std::thread> th;
-        for (int i = 1; i < nparts; ++i) th.emplace_back(pack, i);
-        if (nparts) pack(0);
-        for (auto& x : th) x.join();
-    }
-    offs[n] = sbytes;
-    ioffs[n] = ibytes;
-    doffs[n] = dbytes;
-    memset(bt.seqs.p + sbytes, 0, 64);  // defined bytes past the end
-    bt.n = n;
-    bt.seq_bytes = sbytes;
-    r->records += n;
-    out->n = n;
-    out->seqs = bt.seqs.p;
-    out->seq_bytes = sbytes;
-    out->offsets = offs;
-    out->ids = bt.ids.p;
-    out->id_offsets = ioffs;
-    out->text_offset = r->cur;
-    out->text_bytes = r->stop;
-    out->descs = bt.descs.p;
-    out->desc_offsets = doffs;
+    if (int rc = pack_parts(r, bt, nparts)) return rc;
+    r->records += bt.n;
+    fill_host_batch(r, bt, out);
     return XS_OK;
+}
+
+int xs_fastx_open_device(const char* path, int format, int threads, int device, uint32_t part, uint32_t parts,
+                         xs_fastx** out) {
+    if (int rc = xs_fastx_open_range(path, format, threads, 0, part, parts, out)) return rc;
+    xs_fastx* r = *out;
+    r->dev = new DevSide();
+    r->dev->device = device;
+    auto fail = [&](hipError_t e) {
+        xs_fastx_close(r);
+        *out = nullptr;
+        return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
+    };
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->dev->text_ev, hipEventDisableTiming);
+    if (e != hipSuccess) return fail(e);
+    return XS_OK;
+}
+
+int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* out) {
+    if (!r || !out) return xs::set_error(XS_ERR_ARG, "null argument");
+    if (!r->dev) return xs::set_error(XS_ERR_ARG, "reader was not opened with xs_fastx_open_device");
+    memset(out, 0, sizeof(*out));
+    DevSide& d = *r->dev;
+    FXCHK(hipSetDevice(d.device));
+    const int slot = d.flip;
+    d.flip ^= 1;
+    if (r->format == XS_FASTX_FASTQ && r->wrapped) {  // records cannot be cut by pattern: host parser
+        xs_fastx_batch hb;
+        if (int rc = xs_fastx_next(r, max_text_bytes, &hb)) return rc;
+        if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
+        out->text_offset = hb.text_offset;
+        out->text_bytes = hb.text_bytes;
+        return XS_OK;
+    }
+    const char* end = r->base + r->stop;
+    const size_t budget = std::max<uint64_t>(max_text_bytes, 1);
+    for (;;) {
+        if (r->cur >= r->stop) {
+            if (d.pending) {
+                d.worker.join();
+                d.pending = false;
+            }
+            out->text_offset = r->cur;
+            out->text_bytes = r->stop;
+            return XS_OK;
+        }
+        const char* lo = r->base + r->cur;
+        const char* hi = window_end(r, lo, end, budget);
+        const size_t flo = (size_t)(lo - r->base), fhi = (size_t)(hi - r->base);
+        if (int rc = text_for(r, flo, fhi)) return rc;
+        bool ok = false;
+        if (int rc = parse_on_device(r, flo, fhi, slot, &ok, out)) return rc;
+        if (!ok) {  // the host parser's batch for exactly this window
+            int nparts = 0;
+            if (int rc = parse_window(r, lo, hi, &nparts)) return rc;
+            Batch& bt = r->batch[r->flip];
+            r->flip ^= 1;
+            if (int rc = pack_parts(r, bt, nparts)) return rc;
+            xs_fastx_batch hb;
+            memset(&hb, 0, sizeof(hb));
+            fill_host_batch(r, bt, &hb);
+            if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
+        }
+        r->cur = fhi;
+        // the next window's text loads while the caller works on this batch
+        if (r->cur < r->stop) {
+            const char* nlo = r->base + r->cur;
+            start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, budget) - r->base));
+        }
+        if (out->n) {
+            r->records += out->n;
+            out->text_offset = r->cur;
+            out->text_bytes = r->stop;
+            return XS_OK;
+        }
+        memset(out, 0, sizeof(*out));  // no record in this window (text before the first one)
+    }
 }
 
 void xs_fastx_close(xs_fastx* r) { delete r; }

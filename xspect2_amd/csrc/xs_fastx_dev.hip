@@ -1,0 +1,288 @@
+// xs_fastx_dev.hip — gfx950 record finding for the reader's device mode
+// (xs_fastx_open_device / xs_fastx_next_device).
+//
+// The host only copies a window of file text (cut at a record start, as the
+// host reader cuts it) into pinned memory and on to HBM; the records are found
+// here, in passes over the text at HBM rate:
+//   count     : '\n' per 16 KiB tile (SWAR byte compare, coalesced 16-B loads)
+//   scan      : tile starts in the line index (hipCUB)
+//   positions : every '\n' position, in text order (block scan per 4 KiB row)
+//   records   : FASTQ, one thread per 4-line record: Biopython's checks
+//               (FastqGeneralIterator, restated in xs_fastx.cpp), spans of the
+//               sequence, id and title; FASTA, one thread per line: header or
+//               sequence line, the line's kept length
+//   scan      : output offsets of sequences, ids and titles
+//   copy      : one wave per run (line, sequence, id), lanes copy bytes
+// A window whose text the fast rules do not cover (wrapped FASTQ lines, blank
+// lines between FASTQ records, an empty FASTQ sequence, ' ' or '\r' inside a
+// FASTA sequence line, any FASTQ format error) is flagged and the host parses
+// that window instead, so the result — or Biopython's error message — is the
+// host reader's in every case.
+#include <hipcub/hipcub.hpp>
+
+#include "xs_device.h"
+
+namespace xs {
+namespace {
+
+constexpr int kFxThreads = 256;
+constexpr int kFxRow = kFxThreads * 16;  // bytes per coalesced row of a tile
+static_assert(kFxTile == 4 * kFxRow, "a tile is four rows of 16 B per thread");
+
+// Bit 7 of each byte of w set where that byte is '\n' (no carries cross bytes).
+__device__ __forceinline__ uint32_t nl_bits(uint32_t w) {
+    const uint32_t x = w ^ 0x0a0a0a0au;
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+
+// Python's str.isspace() over ASCII (the host reader's is_ws).
+__device__ __forceinline__ bool fx_ws(uint8_t c) {
+    return c == ' ' || (c >= '\t' && c <= '\r') || (c >= 0x1c && c <= 0x1f);
+}
+
+__device__ __forceinline__ uint32_t fx_rstrip(const uint8_t* t, uint32_t b, uint32_t e) {
+    while (e > b && fx_ws(t[e - 1])) --e;
+    return e;
+}
+
+__device__ __forceinline__ uint32_t line_start(const uint32_t* nl, uint64_t j) { return j ? nl[j - 1] + 1 : 0; }
+
+// First whitespace-separated token of [b, e): its start and length.
+__device__ __forceinline__ void first_token(const uint8_t* t, uint32_t b, uint32_t e, uint32_t* s, uint64_t* len) {
+    while (b < e && fx_ws(t[b])) ++b;
+    uint32_t x = b;
+    while (x < e && !fx_ws(t[x])) ++x;
+    *s = b;
+    *len = x - b;
+}
+
+__global__ void __launch_bounds__(kFxThreads) fx_count_kernel(const uint8_t* __restrict__ text,
+                                                              uint64_t* __restrict__ tile_cnt) {
+    using Reduce = hipcub::BlockReduce<uint32_t, kFxThreads>;
+    __shared__ typename Reduce::TempStorage tmp;
+    const uint8_t* p = text + (uint64_t)blockIdx.x * kFxTile + threadIdx.x * 16;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 v = *reinterpret_cast<const uint4*>(p + i * kFxRow);
+        c += __popc(nl_bits(v.x)) + __popc(nl_bits(v.y)) + __popc(nl_bits(v.z)) + __popc(nl_bits(v.w));
+    }
+    const uint32_t total = Reduce(tmp).Sum(c);
+    if (threadIdx.x == 0) tile_cnt[blockIdx.x] = total;
+}
+
+__global__ void __launch_bounds__(kFxThreads) fx_positions_kernel(const uint8_t* __restrict__ text,
+                                                                  const uint64_t* __restrict__ tile_ofs,
+                                                                  uint32_t* __restrict__ nl) {
+    using Scan = hipcub::BlockScan<uint32_t, kFxThreads>;
+    __shared__ typename Scan::TempStorage tmp;
+    uint64_t base = tile_ofs[blockIdx.x];
+    const uint32_t tile0 = blockIdx.x * (uint32_t)kFxTile;
+    for (int i = 0; i < 4; ++i) {
+        const uint32_t off = tile0 + i * kFxRow + threadIdx.x * 16;
+        const uint4 v = *reinterpret_cast<const uint4*>(text + off);
+        const uint32_t m[4] = {nl_bits(v.x), nl_bits(v.y), nl_bits(v.z), nl_bits(v.w)};
+        const uint32_t c = __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
+        uint32_t pre, total;
+        Scan(tmp).ExclusiveSum(c, pre, total);
+        uint64_t o = base + pre;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            uint32_t mm = m[w];
+            while (mm) {
+                const uint32_t bit = __ffs(mm) - 1;  // 7, 15, 23 or 31
+                nl[o++] = off + 4 * w + (bit >> 3);
+                mm &= mm - 1;
+            }
+        }
+        base += total;
+        __syncthreads();  // tmp is reused by the next row's scan
+    }
+}
+
+// FASTQ: record r = lines 4r .. 4r+3.  The checks are the host reader's
+// (parse_fastq, xs_fastx.cpp), narrowed to the layouts where four lines are
+// exactly one record; anything else sets *bad and the host parses the window.
+__global__ void __launch_bounds__(256) fq_records_kernel(const uint8_t* __restrict__ t,
+                                                         const uint32_t* __restrict__ nl, uint64_t n,
+                                                         FxRuns runs, uint32_t* __restrict__ bad) {
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s0 = line_start(nl, 4 * r), e0 = nl[4 * r];
+        const uint32_t s1 = e0 + 1, e1 = nl[4 * r + 1];
+        const uint32_t s2 = e1 + 1, e2 = nl[4 * r + 2];
+        const uint32_t s3 = e2 + 1, e3 = nl[4 * r + 3];
+        bool ok = e0 > s0 && t[s0] == '@';
+        const uint32_t tb = s0 + 1;
+        const uint32_t te = ok ? fx_rstrip(t, tb, e0) : tb;
+        // one sequence line, not empty, not itself a '+' line
+        const uint32_t se = fx_rstrip(t, s1, e1);
+        ok = ok && se > s1 && t[s1] != '+';
+        for (uint32_t p = s1; ok && p < se; ++p) ok = t[p] != ' ' && t[p] != '\t';
+        ok = ok && e2 > s2 && t[s2] == '+';
+        if (ok) {  // a caption, if any, repeats the title
+            const uint32_t cb = s2 + 1, ce = fx_rstrip(t, cb, e2);
+            if (ce > cb) {
+                ok = ce - cb == te - tb;
+                for (uint32_t i = 0; ok && i < ce - cb; ++i) ok = t[cb + i] == t[tb + i];
+            }
+        }
+        ok = ok && fx_rstrip(t, s3, e3) - s3 == se - s1;  // one quality line of the same length
+        if (!ok) {
+            *bad = 1;
+            runs.seq_len[r] = runs.id_len[r] = runs.desc_len[r] = 0;
+            runs.seq_src[r] = runs.id_src[r] = runs.desc_src[r] = 0;
+            continue;
+        }
+        runs.seq_src[r] = s1;
+        runs.seq_len[r] = se - s1;
+        runs.desc_src[r] = tb;
+        runs.desc_len[r] = te - tb;
+        first_token(t, tb, te, &runs.id_src[r], &runs.id_len[r]);
+    }
+}
+
+// FASTA pass 1: hdr[j] = line j is a header ('>' first).
+__global__ void __launch_bounds__(256) fa_headers_kernel(const uint8_t* __restrict__ t,
+                                                         const uint32_t* __restrict__ nl, uint64_t L,
+                                                         uint64_t* __restrict__ hdr) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < L;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = line_start(nl, j), e = nl[j];
+        hdr[j] = e > s && t[s] == '>';
+    }
+}
+
+// FASTA pass 2, with hofs = exclusive scan of hdr: a header line opens record
+// hofs[j] (its title and id); a sequence line after the first header keeps
+// its right-stripped bytes; lines before the first header are skipped.
+__global__ void __launch_bounds__(256) fa_lines_kernel(const uint8_t* __restrict__ t,
+                                                       const uint32_t* __restrict__ nl, uint64_t L,
+                                                       const uint64_t* __restrict__ hofs,
+                                                       uint32_t* __restrict__ line_src,
+                                                       uint64_t* __restrict__ line_len,
+                                                       uint32_t* __restrict__ rec_line, FxRuns runs,
+                                                       uint32_t* __restrict__ bad) {
+    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < L;
+         j += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = line_start(nl, j), e = nl[j];
+        line_src[j] = s;
+        if (e > s && t[s] == '>') {
+            const uint64_t r = hofs[j];
+            rec_line[r] = (uint32_t)j;
+            const uint32_t tb = s + 1, te = fx_rstrip(t, tb, e);
+            runs.desc_src[r] = tb;
+            runs.desc_len[r] = te - tb;
+            first_token(t, tb, te, &runs.id_src[r], &runs.id_len[r]);
+            line_len[j] = 0;
+        } else if (hofs[j] == 0) {
+            line_len[j] = 0;
+        } else {
+            const uint32_t se = fx_rstrip(t, s, e);
+            bool ok = true;
+            for (uint32_t p = s; ok && p < se; ++p) ok = t[p] != ' ' && t[p] != '\r';
+            if (!ok) *bad = 1;  // the host removes them inside the line
+            line_len[j] = se - s;
+        }
+    }
+}
+
+// FASTA pass 3: record r's sequence starts where its header line's output
+// does (a header keeps no bytes); lens[r] = its length.
+// The record count n = hofs[L] is read on the device (the grid covers L).
+__global__ void __launch_bounds__(256) fa_offsets_kernel(const uint32_t* __restrict__ rec_line,
+                                                         const uint64_t* __restrict__ line_ofs, uint64_t L,
+                                                         const uint64_t* __restrict__ n_dev,
+                                                         uint64_t* __restrict__ offs,
+                                                         uint64_t* __restrict__ lens) {
+    const uint64_t n = *n_dev;
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = line_ofs[rec_line[r]];
+        const uint64_t b = r + 1 < n ? line_ofs[rec_line[r + 1]] : line_ofs[L];
+        offs[r] = a;
+        lens[r] = b - a;
+        if (r == n - 1) offs[n] = line_ofs[L];
+    }
+}
+
+// Run i = src[i] .. + (dofs[i+1] - dofs[i]) bytes of t, to dst + dofs[i].
+__global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict__ t,
+                                                      const uint32_t* __restrict__ src,
+                                                      const uint64_t* __restrict__ dofs, uint64_t m,
+                                                      uint8_t* __restrict__ dst) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t i = wave; i < m; i += waves) {
+        const uint64_t o = dofs[i], len = dofs[i + 1] - o;
+        const uint8_t* s = t + src[i];
+        for (uint64_t x = (uint64_t)lane; x < len; x += 64) dst[o + x] = s[x];
+    }
+}
+
+}  // namespace
+
+size_t fx_temp_bytes(uint64_t n) {
+    size_t a = 0, b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n);
+    (void)hipcub::DeviceReduce::Max(nullptr, b, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)n);
+    return a > b ? a : b;
+}
+
+hipError_t launch_fx_count(const uint8_t* text, uint64_t tiles, uint64_t* tile_cnt, hipStream_t s) {
+    if (!tiles) return hipSuccess;
+    fx_count_kernel<<<(unsigned)tiles, kFxThreads, 0, s>>>(text, tile_cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_fx_positions(const uint8_t* text, uint64_t tiles, const uint64_t* tile_ofs, uint32_t* nl,
+                               hipStream_t s) {
+    if (!tiles) return hipSuccess;
+    fx_positions_kernel<<<(unsigned)tiles, kFxThreads, 0, s>>>(text, tile_ofs, nl);
+    return hipGetLastError();
+}
+
+hipError_t launch_fq_records(const uint8_t* text, const uint32_t* nl, uint64_t n, const FxRuns& runs,
+                             uint32_t* bad, hipStream_t s) {
+    if (!n) return hipSuccess;
+    fq_records_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(text, nl, n, runs, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_headers(const uint8_t* text, const uint32_t* nl, uint64_t L, uint64_t* hdr, hipStream_t s) {
+    if (!L) return hipSuccess;
+    fa_headers_kernel<<<grid_for(L, 256, 8192), 256, 0, s>>>(text, nl, L, hdr);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_lines(const uint8_t* text, const uint32_t* nl, uint64_t L, const uint64_t* hofs,
+                           uint32_t* line_src, uint64_t* line_len, uint32_t* rec_line, const FxRuns& runs,
+                           uint32_t* bad, hipStream_t s) {
+    if (!L) return hipSuccess;
+    fa_lines_kernel<<<grid_for(L, 256, 8192), 256, 0, s>>>(text, nl, L, hofs, line_src, line_len, rec_line, runs,
+                                                          bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_fa_offsets(const uint32_t* rec_line, const uint64_t* line_ofs, uint64_t L, const uint64_t* n_dev,
+                             uint64_t* offs, uint64_t* lens, hipStream_t s) {
+    if (!L) return hipSuccess;
+    fa_offsets_kernel<<<grid_for(L, 256, 8192), 256, 0, s>>>(rec_line, line_ofs, L, n_dev, offs, lens);
+    return hipGetLastError();
+}
+
+hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint8_t* dst,
+                          hipStream_t s) {
+    if (!m) return hipSuccess;
+    fx_copy_kernel<<<grid_for(m, 4, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
+    return hipGetLastError();
+}
+
+hipError_t launch_max_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t n, uint64_t* out,
+                          hipStream_t s) {
+    if (!n) return hipMemsetAsync(out, 0, sizeof(uint64_t), s);
+    return hipcub::DeviceReduce::Max(temp, temp_bytes, in, out, (int)n, s);
+}
+
+}  // namespace xs

@@ -205,6 +205,38 @@ hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hi
 hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
                                uint8_t* out, const uint64_t* out_offs, hipStream_t s);
 
+// ---- device-mode reader (xs_fastx_dev.hip) ----------------------------------
+// Text bytes per tile of the newline index (a window's device copy is padded
+// with zeros to a whole tile).
+constexpr uint64_t kFxTile = 16384;
+// Per record: where its sequence / id / title start in the window's text and
+// how long they are (the lengths, n+1 entries with [n] = 0, are scanned into
+// output offsets).
+struct FxRuns {
+    uint32_t* seq_src;
+    uint64_t* seq_len;
+    uint32_t* id_src;
+    uint64_t* id_len;
+    uint32_t* desc_src;
+    uint64_t* desc_len;
+};
+size_t fx_temp_bytes(uint64_t n);
+hipError_t launch_fx_count(const uint8_t* text, uint64_t tiles, uint64_t* tile_cnt, hipStream_t s);
+hipError_t launch_fx_positions(const uint8_t* text, uint64_t tiles, const uint64_t* tile_ofs, uint32_t* nl,
+                               hipStream_t s);
+hipError_t launch_fq_records(const uint8_t* text, const uint32_t* nl, uint64_t n, const FxRuns& runs,
+                             uint32_t* bad, hipStream_t s);
+hipError_t launch_fa_headers(const uint8_t* text, const uint32_t* nl, uint64_t L, uint64_t* hdr, hipStream_t s);
+hipError_t launch_fa_lines(const uint8_t* text, const uint32_t* nl, uint64_t L, const uint64_t* hofs,
+                           uint32_t* line_src, uint64_t* line_len, uint32_t* rec_line, const FxRuns& runs,
+                           uint32_t* bad, hipStream_t s);
+hipError_t launch_fa_offsets(const uint32_t* rec_line, const uint64_t* line_ofs, uint64_t L, const uint64_t* n_dev,
+                             uint64_t* offs, uint64_t* lens, hipStream_t s);
+hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint8_t* dst,
+                          hipStream_t s);
+hipError_t launch_max_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t n, uint64_t* out,
+                          hipStream_t s);
+
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
 

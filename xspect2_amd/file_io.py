@@ -17,8 +17,8 @@ from typing import Iterator
 
 import numpy as np
 
-from ._lib import (XS_ERR_FORMAT, XS_FASTX_FASTA, XS_FASTX_FASTQ, XS_FASTX_PINNED, FastxBatch, check,
-                   load)
+from ._lib import (XS_ERR_FORMAT, XS_FASTX_FASTA, XS_FASTX_FASTQ, XS_FASTX_PINNED, FastxBatch, FastxDBatch,
+                   check, load)
 from .packing import PackedReads
 
 FASTA_ENDINGS = ["fasta", "fna", "fa", "ffn", "frn"]  # definitions.py:6
@@ -112,6 +112,62 @@ class SeqBatch:
                 for i, rid in enumerate(self.ids())]
 
 
+class DeviceSeqBatch:
+    """One batch of the reader's device mode (xs_fastx_next_device): the
+    packed sequences and their offsets are in HBM (``seqs_ptr``,
+    ``offsets_ptr``; valid until the reader's second following call), ids,
+    titles and a copy of the offsets on the host.  ``Bank.query`` /
+    ``query_totals`` take it as they take a PackedReads, after ``check_valid``:
+    a batch whose reader was closed or has moved two batches on points at
+    device memory that is freed or reused."""
+
+    def __init__(self, fb: FastxDBatch, reader: "FastxReader"):
+        self._reader = reader
+        self._gen = reader._gen
+        n = int(fb.n)
+        self.n = n
+        self.seq_bytes = int(fb.seq_bytes)
+        self.seqs_ptr = int(fb.seqs or 0)
+        self.offsets_ptr = int(fb.offsets or 0)
+        self.max_len = int(fb.max_len)
+        self.parsed_on_device = bool(fb.parsed_on_device)
+        self.text_offset = int(fb.text_offset)
+        self.text_bytes = int(fb.text_bytes)
+        if n:
+            u64 = ctypes.POINTER(ctypes.c_uint64)
+            self.offsets = np.ctypeslib.as_array(ctypes.cast(fb.host_offsets, u64), (n + 1,)).copy()
+            ioffs = np.ctypeslib.as_array(ctypes.cast(fb.id_offsets, u64), (n + 1,))
+            self._ids_raw = ctypes.string_at(fb.ids, int(ioffs[n])) if ioffs[n] else b""
+            self._ioffs = ioffs.copy()
+            doffs = np.ctypeslib.as_array(ctypes.cast(fb.desc_offsets, u64), (n + 1,))
+            self._descs_raw = ctypes.string_at(fb.descs, int(doffs[n])) if doffs[n] else b""
+            self._doffs = doffs.copy()
+        else:
+            self.offsets = np.zeros(1, dtype=np.uint64)
+            self._ids_raw, self._ioffs = b"", np.zeros(1, dtype=np.uint64)
+            self._descs_raw, self._doffs = b"", np.zeros(1, dtype=np.uint64)
+
+    ids = SeqBatch.ids
+    descriptions = SeqBatch.descriptions
+
+    def lengths(self) -> np.ndarray:
+        return np.diff(self.offsets)
+
+    def check_valid(self) -> None:
+        rd = self._reader
+        if rd._h is None or rd._gen - self._gen > 1:
+            raise RuntimeError("device batch is no longer valid: its reader was closed or has read two batches "
+                               "since (the device buffers are freed or reused)")
+
+    def to_host(self) -> PackedReads:
+        """The sequences copied back from HBM (tests, diagnostics)."""
+        self.check_valid()
+        buf = np.zeros(self.seq_bytes + 1, dtype=np.uint8)
+        if self.seq_bytes:
+            check(load().xs_memcpy_to_host(buf.ctypes.data, self.seqs_ptr, self.seq_bytes))
+        return PackedReads(buf, self.offsets.copy())
+
+
 def fastx_format(path: Path) -> int:
     """XS_FASTX_* of a path by its ending (file_io.py:72-79), else ValueError."""
     ending = Path(path).suffix[1:]
@@ -127,27 +183,46 @@ class FastxReader:
 
     ``part``/``parts``: read only part ``part`` of ``parts`` byte ranges of the
     file, cut at record starts (xs_fastx_open_range): one rank's share of a
-    read-sharded job.  The parts' records in part order are the file's."""
+    read-sharded job.  The parts' records in part order are the file's.
 
-    def __init__(self, path: Path, threads: int = 0, pinned: bool = False, part: int = 0, parts: int = 1):
+    ``device``: a HIP device ordinal selects the device mode
+    (xs_fastx_open_device): each window's text goes to HBM and its records are
+    found on the GPU; batches are DeviceSeqBatch."""
+
+    def __init__(self, path: Path, threads: int = 0, pinned: bool = False, part: int = 0, parts: int = 1,
+                 device: int | None = None):
         self.path = Path(path)
         fmt = fastx_format(self.path)
         if not 0 <= part < parts:
             raise ValueError("part must be in [0, parts)")
         self._lib = load()
+        self._h = None
+        self._gen = 0  # batches read (device batches check their age against it)
+        self.device = device
         h = ctypes.c_void_p()
-        check(self._lib.xs_fastx_open_range(str(self.path).encode(), fmt, threads,
-                                            XS_FASTX_PINNED if pinned else 0, part, parts, ctypes.byref(h)))
+        if device is not None:
+            check(self._lib.xs_fastx_open_device(str(self.path).encode(), fmt, threads, device, part, parts,
+                                                 ctypes.byref(h)))
+        else:
+            check(self._lib.xs_fastx_open_range(str(self.path).encode(), fmt, threads,
+                                                XS_FASTX_PINNED if pinned else 0, part, parts, ctypes.byref(h)))
         self._h = h
 
     def next_batch(self, max_bytes: int = DEFAULT_BATCH_TEXT) -> SeqBatch:
         """Next batch (n == 0 at end of file).  Malformed records raise ValueError."""
-        fb = FastxBatch()
-        rc = self._lib.xs_fastx_next(self._h, max_bytes, ctypes.byref(fb))
+        if self._h is None:
+            raise ValueError("reader is closed")
+        self._gen += 1
+        if self.device is not None:
+            fb = FastxDBatch()
+            rc = self._lib.xs_fastx_next_device(self._h, max_bytes, ctypes.byref(fb))
+        else:
+            fb = FastxBatch()
+            rc = self._lib.xs_fastx_next(self._h, max_bytes, ctypes.byref(fb))
         if rc == XS_ERR_FORMAT:
             raise ValueError(self._lib.xs_last_error().decode())
         check(rc)
-        return SeqBatch(fb)
+        return DeviceSeqBatch(fb, self) if self.device is not None else SeqBatch(fb)
 
     def batches(self, max_bytes: int = DEFAULT_BATCH_TEXT) -> Iterator[SeqBatch]:
         while True:
@@ -175,17 +250,19 @@ class FastxReader:
 
 
 def read_batches(path: Path, max_bytes: int | None = None, threads: int = 0,
-                 pinned: bool = False, part: int = 0, parts: int = 1) -> Iterator[SeqBatch]:
+                 pinned: bool = False, part: int = 0, parts: int = 1,
+                 device: int | None = None) -> Iterator[SeqBatch]:
     """Batches of a FASTA/FASTQ file (or of its part ``part`` of ``parts``),
     parsing batch i+1 while the caller works on batch i (the native reader
     releases the GIL).  A yielded batch's buffers stay valid until the
     generator is advanced again.  max_bytes: file text per batch (None:
-    DEFAULT_BATCH_TEXT)."""
+    DEFAULT_BATCH_TEXT).  device: read in device mode on that GPU
+    (DeviceSeqBatch)."""
     from concurrent.futures import ThreadPoolExecutor
 
     max_bytes = DEFAULT_BATCH_TEXT if max_bytes is None else max_bytes
 
-    with FastxReader(path, threads, pinned, part, parts) as rd, ThreadPoolExecutor(1) as pool:
+    with FastxReader(path, threads, pinned, part, parts, device) as rd, ThreadPoolExecutor(1) as pool:
         fut = pool.submit(rd.next_batch, max_bytes)
         while True:
             b = fut.result()
