@@ -306,7 +306,9 @@ int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx
 int xs_fastx_open_range(const char* path, int format, int threads, int flags, uint32_t part, uint32_t parts,
                         xs_fastx** out);
 /* Parse the next batch: about max_text_bytes of file text, cut at a record
- * start (one record at least).  The batch's buffers stay valid until the
+ * start (one record at least).  Batches ramp up: for budgets of 64 MiB or
+ * more, the reader's k-th window takes at most 32 MiB << k, so a pipeline's
+ * first probe starts early.  The batch's buffers stay valid until the
  * SECOND following call, so batch i can be probed while batch i+1 is parsed.
  * Malformed records return XS_ERR_FORMAT with Biopython's message. */
 int xs_fastx_next(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_batch* out);

@@ -40,6 +40,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -355,12 +357,47 @@ struct Batch {
 };
 
 // ---- device mode -------------------------------------------------------------
-// Pinned host buffers outlive their reader in a small process-wide pool: a
-// hipHostMalloc of a few hundred MiB costs tens of ms, more than a window's
-// whole parse.
-std::mutex g_pin_mu;
-std::vector<std::pair<void*, size_t>> g_pin_pool;
-constexpr size_t kPinPoolMax = 4;
+// Pinned host and device buffers outlive their reader in a process-wide pool:
+// a hipHostMalloc of a few MiB costs milliseconds and a hipFree synchronises
+// the device, so a reader per input file would otherwise pay more for its
+// buffers than for its parse.  Reuse takes the smallest pooled buffer that
+// fits and is at most 4x the request.
+struct BufPool {
+    struct Entry {
+        void* p;
+        size_t cap;
+        int device;  // -1: pinned host memory
+    };
+    std::mutex mu;
+    std::vector<Entry> free_list;
+    size_t bytes = 0;
+    static constexpr size_t kMaxBytes = size_t(6) << 30;
+    static constexpr size_t kMaxEntries = 96;
+    void* take(size_t want, int device, size_t* cap) {
+        std::lock_guard<std::mutex> g(mu);
+        size_t best = free_list.size();
+        for (size_t i = 0; i < free_list.size(); ++i) {
+            const Entry& e = free_list[i];
+            if (e.device == device && e.cap >= want && e.cap / 4 <= want &&
+                (best == free_list.size() || e.cap < free_list[best].cap))
+                best = i;
+        }
+        if (best == free_list.size()) return nullptr;
+        void* p = free_list[best].p;
+        *cap = free_list[best].cap;
+        bytes -= *cap;
+        free_list.erase(free_list.begin() + (ptrdiff_t)best);
+        return p;
+    }
+    bool give(void* p, size_t cap, int device) {  // false: the caller frees it
+        std::lock_guard<std::mutex> g(mu);
+        if (bytes + cap > kMaxBytes || free_list.size() >= kMaxEntries) return false;
+        free_list.push_back({p, cap, device});
+        bytes += cap;
+        return true;
+    }
+};
+BufPool g_pool;
 
 struct PinBuf {
     char* p = nullptr;
@@ -368,19 +405,7 @@ struct PinBuf {
     int ensure(size_t bytes) {  // contents are not preserved
         if (bytes <= cap && p) return XS_OK;
         release();
-        {
-            std::lock_guard<std::mutex> g(g_pin_mu);
-            size_t best = g_pin_pool.size();
-            for (size_t i = 0; i < g_pin_pool.size(); ++i)
-                if (g_pin_pool[i].second >= bytes && (best == g_pin_pool.size() || g_pin_pool[i].second < g_pin_pool[best].second))
-                    best = i;
-            if (best < g_pin_pool.size()) {
-                p = static_cast<char*>(g_pin_pool[best].first);
-                cap = g_pin_pool[best].second;
-                g_pin_pool.erase(g_pin_pool.begin() + (ptrdiff_t)best);
-                return XS_OK;
-            }
-        }
+        if ((p = static_cast<char*>(g_pool.take(bytes, -1, &cap)))) return XS_OK;
         const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
         if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
             p = nullptr;
@@ -390,13 +415,7 @@ struct PinBuf {
         return XS_OK;
     }
     void release() {
-        if (!p) return;
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        if (g_pin_pool.size() < kPinPoolMax) {
-            g_pin_pool.emplace_back(p, cap);
-        } else {
-            (void)hipHostFree(p);
-        }
+        if (p && !g_pool.give(p, cap, -1)) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
     }
@@ -406,9 +425,11 @@ struct PinBuf {
 struct DBuf {
     void* p = nullptr;
     size_t cap = 0;
+    int device = 0;
     int ensure(size_t bytes) {  // contents are not preserved
         if (bytes <= cap && p) return XS_OK;
         release();
+        if ((p = g_pool.take(bytes, device, &cap))) return XS_OK;
         const size_t want = std::max<size_t>(bytes + bytes / 8, 4096);
         if (hipMalloc(&p, want) != hipSuccess) {
             p = nullptr;
@@ -418,7 +439,7 @@ struct DBuf {
         return XS_OK;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p && !g_pool.give(p, cap, device)) (void)hipFree(p);
         p = nullptr;
         cap = 0;
     }
@@ -430,16 +451,19 @@ struct DBuf {
 };
 
 constexpr size_t kPieceBytes = 4u << 20;  // pread + DMA unit of a window's text
+constexpr size_t kLoadThreads = 6;         // pread threads of a window load
 constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
 
 struct DevSide {
     int device = 0;
     hipStream_t stream = nullptr;  // parse kernels
     hipStream_t copy = nullptr;    // text DMA
-    hipEvent_t text_ev = nullptr;
-    PinBuf pin;         // the window's text
+    // Window text in two slots: the next window loads into one while the
+    // current one is parsed from the other.
+    hipEvent_t text_ev[2] = {nullptr, nullptr};
+    PinBuf pin[2];      // a window's text
     PinBuf status;      // small D2H results
-    DBuf text;          // the window's text, zero-padded to whole tiles
+    DBuf text[2];       // a window's text, zero-padded to whole tiles
     DBuf tiles, tile_ofs, nl, temp, flag;
     DBuf hdr, hofs, line_src, line_len, line_ofs, rec_line, lens, maxlen;
     DBuf seq_src, seq_len, id_src, id_len, desc_src, desc_len, id_ofs, desc_ofs, ids_d, descs_d;
@@ -450,14 +474,25 @@ struct DevSide {
     std::thread worker;
     bool pending = false;
     size_t pf_lo = 0, pf_hi = 0;
+    int pf_slot = 0;
+    int next_text = 0;  // text slot of the next inline load
     int pf_rc = XS_OK;
     std::string pf_err;
+    double load_ms[2] = {0, 0};  // each slot's last load_text: pread + DMA queueing
+    void set_device(int dev) {
+        device = dev;
+        for (DBuf* b : {&text[0], &text[1], &tiles, &tile_ofs, &nl, &temp, &flag, &hdr, &hofs, &line_src, &line_len, &line_ofs,
+                        &rec_line, &lens, &maxlen, &seq_src, &seq_len, &id_src, &id_len, &desc_src, &desc_len,
+                        &id_ofs, &desc_ofs, &ids_d, &descs_d, &seqs[0], &seqs[1], &offs[0], &offs[1]})
+            b->device = dev;
+    }
     ~DevSide() {
         if (worker.joinable()) worker.join();
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         if (copy) (void)hipStreamSynchronize(copy);
-        if (text_ev) (void)hipEventDestroy(text_ev);
+        for (hipEvent_t e : text_ev)
+            if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         if (copy) (void)hipStreamDestroy(copy);
     }
@@ -475,6 +510,7 @@ struct xs_fastx {
     size_t stop = 0;   // end of this reader's text (the file, or its part)
     size_t cur = 0;
     uint64_t records = 0;
+    uint64_t windows = 0;  // windows consumed (window_budget's ramp)
     Batch batch[2];
     int flip = 0;
     std::vector<Part> parts;
@@ -487,6 +523,17 @@ struct xs_fastx {
 };
 
 namespace {
+
+// Windows ramp up: the reader's k-th window takes at most kFirstWindow << k
+// bytes of text (for budgets of at least 2 * kFirstWindow), so the caller's
+// first probe starts after a small parse while the later, larger windows are
+// read behind it.
+constexpr size_t kFirstWindow = 32u << 20;
+size_t window_budget(uint64_t max_text_bytes, uint64_t k) {
+    const size_t b = std::max<uint64_t>(max_text_bytes, 1);
+    if (b < 2 * kFirstWindow || k >= 16) return b;
+    return std::min(b, kFirstWindow << k);
+}
 
 // End of the window that starts at lo: the first record start at or after
 // lo + budget (the whole rest if that is within budget; one record at least).
@@ -596,51 +643,81 @@ void fill_host_batch(const xs_fastx* r, const Batch& bt, xs_fastx_batch* out) {
     out->desc_offsets = reinterpret_cast<const uint64_t*>(bt.desc_offs.p);
 }
 
+// XSPECT2_AMD_FASTX_TRACE set: one line per device window on stderr with the
+// time of each phase (diagnostics of the device mode).
+bool fx_trace() {
+    static const bool on = getenv("XSPECT2_AMD_FASTX_TRACE") != nullptr;
+    return on;
+}
+double fx_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+struct FxTimes {
+    double load = 0, count = 0, records = 0, copy = 0;
+};
+thread_local FxTimes g_fx;
+
 #define FXCHK(expr)                                                                                     \
     do {                                                                                                \
         hipError_t _e = (expr);                                                                         \
         if (_e != hipSuccess) return xs::set_error(XS_ERR_HIP, hipGetErrorString(_e));                 \
     } while (0)
 
-// The text of [lo, hi) (file offsets) into d.pin and on to d.text (zero-padded
-// to whole tiles), piece by piece: host threads pread the pieces, the DMA of
-// each piece is queued on d.copy as soon as it is in.  d.text_ev marks the end.
-int load_text(xs_fastx* r, size_t lo, size_t hi) {
+// The text of [lo, hi) (file offsets) into d.pin[ts] and on to d.text[ts]
+// (zero-padded to whole tiles), piece by piece: host threads pread the pieces,
+// the DMA of each piece is queued on d.copy as soon as it is in.
+// d.text_ev[ts] marks the end.
+int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     DevSide& d = *r->dev;
+    const double t0 = fx_ms();
     FXCHK(hipSetDevice(d.device));
     const size_t span = hi - lo;
     const size_t tiles = std::max<size_t>(1, (span + xs::kFxTile - 1) / xs::kFxTile);
     const size_t padded = tiles * xs::kFxTile;
-    if (int rc = d.pin.ensure(span + 1)) return rc;
-    if (int rc = d.text.ensure(padded + 16)) return rc;
+    PinBuf& pin = d.pin[ts];
+    DBuf& text = d.text[ts];
+    if (int rc = pin.ensure(span + 1)) return rc;
+    if (int rc = text.ensure(padded + 16)) return rc;
     const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
-    const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)r->threads, pieces));
-    std::vector<std::atomic<int>> done(pieces);
-    for (auto& x : done) x.store(0);
-    std::atomic<bool> failed{false};
+    // pread outruns the DMA (~50 GB/s) with a few threads; more only burn the
+    // CPU share the caller's own threads need
+    const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, kLoadThreads, pieces}));
+    std::vector<uint8_t> done(pieces, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    bool failed = false;
     auto work = [&](int t) {
         for (size_t p = (size_t)t; p < pieces; p += (size_t)T) {
             size_t o = p * kPieceBytes;
             const size_t e = std::min(span, o + kPieceBytes);
+            bool bad = false;
             while (o < e) {
-                const ssize_t got = pread(r->fd, d.pin.p + o, e - o, (off_t)(lo + o));
+                const ssize_t got = pread(r->fd, pin.p + o, e - o, (off_t)(lo + o));
                 if (got <= 0) {
-                    failed.store(true);
+                    bad = true;
                     break;
                 }
                 o += (size_t)got;
             }
-            done[p].store(1, std::memory_order_release);
+            {
+                std::lock_guard<std::mutex> g(mu);
+                done[p] = 1;
+                failed |= bad;
+            }
+            cv.notify_one();
         }
     };
     std::vector<std::thread> th;
     for (int t = 0; t < T; ++t) th.emplace_back(work, t);
     int rc = XS_OK;
-    for (size_t p = 0; p < pieces; ++p) {
-        while (!done[p].load(std::memory_order_acquire)) std::this_thread::yield();
-        if (failed.load()) break;
+    for (size_t p = 0; p < pieces; ++p) {  // queue each piece's DMA as soon as it is in
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return done[p] != 0; });
+            if (failed) break;
+        }
         const size_t o = p * kPieceBytes, n = std::min(span, o + kPieceBytes) - o;
-        hipError_t e = hipMemcpyAsync(d.text.as<char>() + o, d.pin.p + o, n, hipMemcpyHostToDevice, d.copy);
+        hipError_t e = hipMemcpyAsync(text.as<char>() + o, pin.p + o, n, hipMemcpyHostToDevice, d.copy);
         if (e != hipSuccess) {
             rc = xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
             break;
@@ -648,49 +725,56 @@ int load_text(xs_fastx* r, size_t lo, size_t hi) {
     }
     for (auto& x : th) x.join();
     if (rc) return rc;
-    if (failed.load()) return xs::set_error(XS_ERR_IO, "read failed while loading the window's text");
-    FXCHK(hipMemsetAsync(d.text.as<char>() + span, 0, padded + 16 - span, d.copy));
-    FXCHK(hipEventRecord(d.text_ev, d.copy));
+    if (failed) return xs::set_error(XS_ERR_IO, "read failed while loading the window's text");
+    FXCHK(hipMemsetAsync(text.as<char>() + span, 0, padded + 16 - span, d.copy));
+    FXCHK(hipEventRecord(d.text_ev[ts], d.copy));
+    d.load_ms[ts] = fx_ms() - t0;
     return XS_OK;
 }
 
-void start_prefetch(xs_fastx* r, size_t lo, size_t hi) {
+// Load [lo, hi) into text slot ts on a worker thread.
+void start_prefetch(xs_fastx* r, size_t lo, size_t hi, int ts) {
     DevSide& d = *r->dev;
     d.pending = true;
     d.pf_lo = lo;
     d.pf_hi = hi;
-    d.worker = std::thread([r, lo, hi] {
+    d.pf_slot = ts;
+    d.next_text = ts ^ 1;
+    d.worker = std::thread([r, lo, hi, ts] {
         DevSide& dd = *r->dev;
-        dd.pf_rc = load_text(r, lo, hi);
+        dd.pf_rc = load_text(r, lo, hi, ts);
         if (dd.pf_rc) dd.pf_err = xs_last_error();
     });
 }
 
-// Wait for the text of [lo, hi) to be queued for d.text (loading it now if no
-// prefetch of exactly that window is pending).
-int text_for(xs_fastx* r, size_t lo, size_t hi) {
+// Wait for the text of [lo, hi) to be queued for its slot (loading it now if
+// no prefetch of exactly that window is pending); *ts = the slot.
+int text_for(xs_fastx* r, size_t lo, size_t hi, int* ts) {
     DevSide& d = *r->dev;
     if (d.pending) {
         d.worker.join();
         d.pending = false;
         if (d.pf_lo == lo && d.pf_hi == hi) {
+            *ts = d.pf_slot;
             if (d.pf_rc) return xs::set_error(d.pf_rc, d.pf_err.c_str());
             return XS_OK;
         }
     }
-    return load_text(r, lo, hi);
+    *ts = d.next_text;
+    d.next_text ^= 1;
+    return load_text(r, lo, hi, *ts);
 }
 
 // Record finding on the device for the window [lo, hi) whose text is queued
 // for d.text.  *ok = false: the window needs the host parser (nothing of the
 // batch is kept).  On success the batch is in slot `slot` and `out` is filled.
-int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fastx_dbatch* out) {
+int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* ok, xs_fastx_dbatch* out) {
     DevSide& d = *r->dev;
     *ok = false;
     const size_t span = hi - lo;
     if (span == 0 || span >= (1ull << 31) - xs::kFxTile) return XS_OK;  // u32 positions, int scan sizes
     const hipStream_t s = d.stream;
-    FXCHK(hipStreamWaitEvent(s, d.text_ev, 0));
+    FXCHK(hipStreamWaitEvent(s, d.text_ev[ts], 0));
     const uint64_t tiles = (span + xs::kFxTile - 1) / xs::kFxTile;
     if (int rc = d.tiles.ensure((tiles + 1) * 8)) return rc;
     if (int rc = d.tile_ofs.ensure((tiles + 1) * 8)) return rc;
@@ -699,11 +783,14 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fa
     size_t tb = xs::fx_temp_bytes(tiles + 1);
     if (int rc = d.temp.ensure(tb)) return rc;
     auto* st = reinterpret_cast<uint64_t*>(d.status.p);
-    FXCHK(xs::launch_fx_count(d.text.as<uint8_t>(), tiles, d.tiles.as<uint64_t>(), s));
+    FXCHK(xs::launch_fx_count(d.text[ts].as<uint8_t>(), tiles, d.tiles.as<uint64_t>(), s));
     FXCHK(hipMemsetAsync(d.tiles.as<uint64_t>() + tiles, 0, 8, s));
     FXCHK(xs::launch_scan(d.temp.p, tb, d.tiles.as<uint64_t>(), d.tile_ofs.as<uint64_t>(), tiles + 1, s));
+    const double t0 = fx_ms();
     FXCHK(hipMemcpyAsync(st, d.tile_ofs.as<uint64_t>() + tiles, 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipStreamSynchronize(s));
+    const double t1 = fx_ms();
+    g_fx.count = t1 - t0;
     const uint64_t newlines = st[0];
     const bool tail = r->base[hi - 1] != '\n';  // a last line without '\n' ends at hi
     const uint64_t L = newlines + (tail ? 1 : 0);
@@ -713,7 +800,8 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fa
     if (int rc = d.nl.ensure(L * 4 + 4)) return rc;
     tb = xs::fx_temp_bytes((fasta ? L : nmax) + 1);
     if (int rc = d.temp.ensure(tb)) return rc;
-    FXCHK(xs::launch_fx_positions(d.text.as<uint8_t>(), tiles, d.tile_ofs.as<uint64_t>(), d.nl.as<uint32_t>(), s));
+    FXCHK(xs::launch_fx_positions(d.text[ts].as<uint8_t>(), tiles, d.tile_ofs.as<uint64_t>(), d.nl.as<uint32_t>(),
+                                  s));
     if (tail) FXCHK(hipMemsetD32Async(d.nl.as<uint32_t>() + newlines, (int)span, 1, s));
     FXCHK(hipMemsetAsync(d.flag.p, 0, 4, s));
     for (DBuf* b : {&d.seq_src, &d.id_src, &d.desc_src})
@@ -725,7 +813,7 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fa
     const xs::FxRuns runs{d.seq_src.as<uint32_t>(), d.seq_len.as<uint64_t>(), d.id_src.as<uint32_t>(),
                           d.id_len.as<uint64_t>(), d.desc_src.as<uint32_t>(), d.desc_len.as<uint64_t>()};
     uint64_t* offs = d.offs[slot].as<uint64_t>();
-    const uint8_t* text = d.text.as<uint8_t>();
+    const uint8_t* text = d.text[ts].as<uint8_t>();
     const uint32_t* nl = d.nl.as<uint32_t>();
     // status: [0] bad, [1] records, [2] sequence bytes, [3] id bytes, [4] title bytes, [5] longest record
     if (fasta) {
@@ -770,6 +858,8 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fa
     FXCHK(hipMemcpyAsync(st, d.flag.p, 4, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(st + 5, d.maxlen.p, 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipStreamSynchronize(s));
+    const double t2 = fx_ms();
+    g_fx.records = t2 - t1;
     if ((uint32_t)st[0]) return XS_OK;
     const uint64_t n = st[1], sbytes = st[2], ibytes = st[3], dbytes = st[4];
     if (int rc = d.seqs[slot].ensure(sbytes + kDevPad)) return rc;
@@ -793,6 +883,7 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, bool* ok, xs_fa
     FXCHK(hipMemcpyAsync(d.desc_offs[slot].p, d.desc_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(d.hoffs[slot].p, offs, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipStreamSynchronize(s));
+    g_fx.copy = fx_ms() - t2;
     *ok = true;
     out->n = n;
     out->seq_bytes = sbytes;
@@ -910,14 +1001,15 @@ int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
     r->flip ^= 1;
     bt.n = bt.seq_bytes = 0;
     const char* end = r->base + r->stop;
-    const size_t budget = std::max<uint64_t>(max_text_bytes, 1);
     int nparts = 0;
     // a window can hold no record (text before the first one): go on until
     // records are found or the file ends
     for (;;) {
         const char* lo = r->base + r->cur;
+        const size_t budget = window_budget(max_text_bytes, r->windows);
         nparts = 0;
         if (lo < end) {
+            ++r->windows;
             if (r->format == XS_FASTX_FASTQ && r->wrapped) {
                 // sequential: the parser itself stops at the first record past the budget
                 Part& pt = r->parts[0];
@@ -945,16 +1037,22 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
     if (int rc = xs_fastx_open_range(path, format, threads, 0, part, parts, out)) return rc;
     xs_fastx* r = *out;
     r->dev = new DevSide();
-    r->dev->device = device;
+    r->dev->set_device(device);
     auto fail = [&](hipError_t e) {
         xs_fastx_close(r);
         *out = nullptr;
         return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
     };
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->stream, hipStreamNonBlocking);
+    // The parse kernels are short and sit between the caller's probes of the
+    // previous batch: a high-priority stream lets their workgroups in as soon
+    // as the probe frees a slot, instead of after the whole probe.
+    int least = 0, greatest = 0;
+    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&r->dev->text_ev, hipEventDisableTiming);
+    for (hipEvent_t& ev : r->dev->text_ev)
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
     if (e != hipSuccess) return fail(e);
     return XS_OK;
 }
@@ -976,7 +1074,6 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
         return XS_OK;
     }
     const char* end = r->base + r->stop;
-    const size_t budget = std::max<uint64_t>(max_text_bytes, 1);
     for (;;) {
         if (r->cur >= r->stop) {
             if (d.pending) {
@@ -988,11 +1085,31 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
             return XS_OK;
         }
         const char* lo = r->base + r->cur;
-        const char* hi = window_end(r, lo, end, budget);
+        const char* hi = window_end(r, lo, end, window_budget(max_text_bytes, r->windows));
         const size_t flo = (size_t)(lo - r->base), fhi = (size_t)(hi - r->base);
-        if (int rc = text_for(r, flo, fhi)) return rc;
+        const double t0 = fx_ms();
+        const bool prefetched = d.pending && d.pf_lo == flo && d.pf_hi == fhi;
+        int ts = 0;
+        if (int rc = text_for(r, flo, fhi, &ts)) return rc;
+        const double t1 = fx_ms();
+        r->cur = fhi;
+        ++r->windows;
+        // the next window's text loads into the other slot while this one is
+        // parsed and the caller works on the batch
+        if (r->cur < r->stop) {
+            const char* nlo = r->base + r->cur;
+            const size_t nb = window_budget(max_text_bytes, r->windows);
+            start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, nb) - r->base), ts ^ 1);
+        }
         bool ok = false;
-        if (int rc = parse_on_device(r, flo, fhi, slot, &ok, out)) return rc;
+        g_fx = FxTimes{};
+        if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
+        if (fx_trace())
+            fprintf(stderr,
+                    "[fastx-device] t=%.2f window %zu+%zu: text %s load %.2f ms, wait %.2f ms | count %.2f records %.2f "
+                    "copy %.2f ms | %s\n",
+                    t0, flo, fhi - flo, prefetched ? "prefetched" : "inline", d.load_ms[ts], t1 - t0, g_fx.count,
+                    g_fx.records, g_fx.copy, ok ? "device" : "host parser");
         if (!ok) {  // the host parser's batch for exactly this window
             int nparts = 0;
             if (int rc = parse_window(r, lo, hi, &nparts)) return rc;
@@ -1003,12 +1120,6 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
             memset(&hb, 0, sizeof(hb));
             fill_host_batch(r, bt, &hb);
             if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
-        }
-        r->cur = fhi;
-        // the next window's text loads while the caller works on this batch
-        if (r->cur < r->stop) {
-            const char* nlo = r->base + r->cur;
-            start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, budget) - r->base));
         }
         if (out->n) {
             r->records += out->n;

@@ -115,17 +115,17 @@ class SeqBatch:
 class DeviceSeqBatch:
     """One batch of the reader's device mode (xs_fastx_next_device): the
     packed sequences and their offsets are in HBM (``seqs_ptr``,
-    ``offsets_ptr``; valid until the reader's second following call), ids,
-    titles and a copy of the offsets on the host.  ``Bank.query`` /
-    ``query_totals`` take it as they take a PackedReads, after ``check_valid``:
-    a batch whose reader was closed or has moved two batches on points at
-    device memory that is freed or reused."""
+    ``offsets_ptr``), ids, titles and a copy of the offsets in the reader's
+    pinned host buffers, copied out on first use.  All of them are valid until
+    the reader's second following batch: ``check_valid`` (run by every access
+    and by ``Bank.query`` / ``query_totals``, which take the batch as they take
+    a PackedReads) raises for a batch whose reader was closed or has moved two
+    batches on, whose memory is freed or reused."""
 
     def __init__(self, fb: FastxDBatch, reader: "FastxReader"):
         self._reader = reader
         self._gen = reader._gen
-        n = int(fb.n)
-        self.n = n
+        self.n = int(fb.n)
         self.seq_bytes = int(fb.seq_bytes)
         self.seqs_ptr = int(fb.seqs or 0)
         self.offsets_ptr = int(fb.offsets or 0)
@@ -133,31 +133,44 @@ class DeviceSeqBatch:
         self.parsed_on_device = bool(fb.parsed_on_device)
         self.text_offset = int(fb.text_offset)
         self.text_bytes = int(fb.text_bytes)
-        if n:
-            u64 = ctypes.POINTER(ctypes.c_uint64)
-            self.offsets = np.ctypeslib.as_array(ctypes.cast(fb.host_offsets, u64), (n + 1,)).copy()
-            ioffs = np.ctypeslib.as_array(ctypes.cast(fb.id_offsets, u64), (n + 1,))
-            self._ids_raw = ctypes.string_at(fb.ids, int(ioffs[n])) if ioffs[n] else b""
-            self._ioffs = ioffs.copy()
-            doffs = np.ctypeslib.as_array(ctypes.cast(fb.desc_offsets, u64), (n + 1,))
-            self._descs_raw = ctypes.string_at(fb.descs, int(doffs[n])) if doffs[n] else b""
-            self._doffs = doffs.copy()
-        else:
-            self.offsets = np.zeros(1, dtype=np.uint64)
-            self._ids_raw, self._ioffs = b"", np.zeros(1, dtype=np.uint64)
-            self._descs_raw, self._doffs = b"", np.zeros(1, dtype=np.uint64)
-
-    ids = SeqBatch.ids
-    descriptions = SeqBatch.descriptions
-
-    def lengths(self) -> np.ndarray:
-        return np.diff(self.offsets)
+        self._host = (fb.host_offsets, fb.ids, fb.id_offsets, fb.descs, fb.desc_offsets)
+        self._offsets = self._ids_raw = self._descs_raw = None
 
     def check_valid(self) -> None:
         rd = self._reader
         if rd._h is None or rd._gen - self._gen > 1:
             raise RuntimeError("device batch is no longer valid: its reader was closed or has read two batches "
                                "since (the device buffers are freed or reused)")
+
+    def _u64(self, ptr) -> np.ndarray:
+        return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint64)), (self.n + 1,)).copy()
+
+    @property
+    def offsets(self) -> np.ndarray:
+        if self._offsets is None:
+            self.check_valid()
+            self._offsets = self._u64(self._host[0]) if self.n else np.zeros(1, dtype=np.uint64)
+        return self._offsets
+
+    def _text(self, which: int):
+        self.check_valid()
+        if not self.n:
+            return b"", np.zeros(1, dtype=np.uint64)
+        o = self._u64(self._host[which + 1])
+        return (ctypes.string_at(self._host[which], int(o[-1])) if o[-1] else b""), o
+
+    def ids(self) -> list[str]:
+        if self._ids_raw is None:
+            self._ids_raw, self._ioffs = self._text(1)
+        return SeqBatch.ids(self)
+
+    def descriptions(self) -> list[str]:
+        if self._descs_raw is None:
+            self._descs_raw, self._doffs = self._text(3)
+        return SeqBatch.descriptions(self)
+
+    def lengths(self) -> np.ndarray:
+        return np.diff(self.offsets)
 
     def to_host(self) -> PackedReads:
         """The sequences copied back from HBM (tests, diagnostics)."""
