@@ -32,6 +32,8 @@ probe from profiles/r02_traffic.json.  cpu_baseline: the C oracle (oracle/libora
 OpenMP) on a bounded sample of the same reads and bank (rank 0, N=1 only);
 its hits are also compared with the GPU's; plus the reference's per-read loop
 shape on one core.  host_path: the same step from host buffers (PCIe).
+end_to_end (species/genus, N=1): SURVEY.md §8(d) time (ii), the same reads as
+a FASTQ file -> totals / hit matrix through the library's file path.
 """
 from __future__ import annotations
 
@@ -90,6 +92,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host-buffer runs (profiling: only full-size probe launches)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end legs (the bench's reads as a FASTQ file -> totals / hit matrix)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r02_traffic.json"))
@@ -419,6 +423,9 @@ def main():
         except Exception:
             lookup_l2 = None
     host = None if args.no_host_path else host_path(wl, args)
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e and args.workload in ("species", "genus"):
+        e2e = end_to_end(wl, args)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -469,6 +476,7 @@ def main():
         },
         "cpu_baseline": cpu,
         "host_path": host,
+        "end_to_end": e2e,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -582,6 +590,54 @@ def host_path(wl, args, reps=3):
                    "buffer (xs_query_hits); hits_u32_pageable: xs_query's uint32 matrix into a fresh pageable "
                    "array; totals: D+1 counters.  The headline value starts with the reads in HBM")
     return out
+
+
+def end_to_end(wl, args, reps=3):
+    """SURVEY.md §8(d) time (ii), end to end from a file: the bench's reads
+    written as a FASTQ (ids r<i>, quality 'I'), then file -> per-doc totals
+    and file -> hit matrix (narrowest exact type) through the library's file
+    path (file_io.read_batches + Bank.query_totals / Bank.query, as
+    predict_columnar streams a file), with the native reader in device mode
+    (text to HBM, records found on the GPU; the models' default) and in host
+    mode.  The file is in the page cache (just written): disk time is not in
+    it.  Best of `reps` passes; never the headline value."""
+    import shutil
+    import tempfile
+    from xspect2_amd.file_io import read_batches
+
+    tmp = Path(tempfile.mkdtemp(prefix="xs_bench_e2e_"))
+    try:
+        fq = tmp / "reads.fastq"
+        qual = b"I" * args.read_len
+        with open(fq, "wb") as fh:
+            for lo in range(0, wl.n, 100_000):
+                fh.write(b"".join(b"@r%d\n%s\n+\n%s\n" % (i, wl.reads[i].tobytes(), qual)
+                                  for i in range(lo, min(wl.n, lo + 100_000))))
+        size = fq.stat().st_size
+        out = {"file_bytes": size, "reads": wl.n}
+        for mode, dev in (("device_reader", wl.dev.index), ("host_reader", None)):
+            for name, fn in (("totals", lambda b, pb: b.query_totals(pb, step=args.step)),
+                             ("hits", lambda b, pb: b.query(pb, step=args.step, hit_dtype="auto"))):
+                ts = []
+                for _ in range(reps):
+                    t = time.perf_counter()
+                    n = 0
+                    for batch in read_batches(fq, device=dev):
+                        for b in wl.banks:
+                            fn(b, batch if dev is not None else batch.packed)
+                        n += batch.n
+                    ts.append(time.perf_counter() - t)
+                assert n == wl.n
+                dt = min(ts)
+                out[f"{mode}_{name}"] = {"ms": dt * 1e3, "first_ms": ts[0] * 1e3,
+                                         "probes_per_s": wl.probes_per_step() / wl.world / dt,
+                                         "file_GBps": size / dt / 1e9}
+        out["note"] = ("file (page cache) -> parse -> probe -> totals (D+1 counters) or the n x D hit matrix in the "
+                       "narrowest exact type, on host; device_reader: xs_fastx_open_device (the models' default "
+                       "for file inputs), host_reader: xs_fastx_open + H2D of packed batches")
+        return out
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def reference_style_baseline(wl, args, obanks, m=10_000):

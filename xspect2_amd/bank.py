@@ -159,6 +159,10 @@ class Bank:
         return self.info.kind
 
     @property
+    def device(self) -> int:
+        return int(self.info.device)
+
+    @property
     def num_docs(self) -> int:
         return int(self.info.num_docs)
 

@@ -358,7 +358,7 @@ def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: b
     from host buffers and gathered through the host."""
     import torch
     from .bank import narrowest_count_dtype
-    from .file_io import check_input_path, read_batches
+    from .file_io import check_input_path, file_reader_device, read_batches
     from .result import MatrixResult
 
     dist = _dist()
@@ -370,23 +370,29 @@ def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: b
     labels = [lab for part in labels_all for lab in part]
     on_device = collective_device().type == "cuda"
     ids, hits, nks = [], [], []
-    for batch in read_batches(input_file):
+    rdev = file_reader_device(model.index) if on_device else None  # text straight to HBM
+    for batch in read_batches(input_file, device=rdev):
         L = batch.lengths()
         if (L <= model.k).any():
             raise ValueError("Invalid sequence, must be longer than k")
-        pr = batch.packed
         mx = int(((L - model.k) // step + 1).max()) if batch.n else 0
         if on_device:
-            dev = torch.device("cuda", model.index.info.device)
-            d_seq = torch.from_numpy(pr.buf[:max(pr.nbytes, 1)]).to(dev)
-            d_off = torch.from_numpy(pr.offsets.view(np.int64)).to(dev)
-            g, d_nk = docs_sharded_hits_device(model.index, d_seq, pr.nbytes, d_off, pr.n, step)
+            if rdev is not None:
+                batch.check_valid()
+                d_seq, nbytes, d_off = batch.seqs_ptr, batch.seq_bytes, batch.offsets_ptr
+            else:
+                pr = batch.packed
+                dev = torch.device("cuda", model.index.info.device)
+                d_seq = torch.from_numpy(pr.buf[:max(pr.nbytes, 1)]).to(dev)
+                d_off = torch.from_numpy(pr.offsets.view(np.int64)).to(dev)
+                nbytes = pr.nbytes
+            g, d_nk = docs_sharded_hits_device(model.index, d_seq, nbytes, d_off, batch.n, step)
             dt = narrowest_count_dtype(mx)
             h = g.to({np.uint8: torch.uint8, np.uint16: torch.int16}.get(dt, torch.int32)).cpu().numpy()
             h = h.view(np.uint16) if dt == np.uint16 else h.view(np.uint8) if dt == np.uint8 else h.view(np.uint32)
             nk = d_nk.cpu().numpy().view(np.uint64)
         else:
-            hl, nk = model._query(pr, step)
+            hl, nk = model._query(batch.packed, step)
             t = torch.from_numpy(np.ascontiguousarray(hl).astype(np.int32))
             h = gather_doc_shards(t, mx).numpy().view(np.uint32)  # every rank reads the same batches
         ids += batch.ids()

@@ -27,6 +27,20 @@ FASTQ_ENDINGS = ["fastq", "fq"]                       # definitions.py:7
 DEFAULT_BATCH_TEXT = 256 << 20
 
 
+def file_reader_device(index) -> int | None:
+    """The device a model's file inputs are read on (the reader's device mode,
+    text straight to HBM, records found there), or None for the host reader:
+    device mode when the index is a GPU bank (bank.Bank), unless
+    XSPECT2_AMD_READER=host."""
+    import os
+
+    from .bank import Bank
+
+    if os.environ.get("XSPECT2_AMD_READER", "device").strip().lower() == "host":
+        return None
+    return index.device if isinstance(index, Bank) else None
+
+
 @dataclass
 class Record:
     id: str

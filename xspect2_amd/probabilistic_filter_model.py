@@ -19,8 +19,8 @@ import numpy as np
 
 from .bank import Bank, cobs_signature_size
 from ._lib import XS_BANK_COBS_CLASSIC
-from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, FileShard, check_input_path, get_record_iterator,
-                      is_record, read_batches, seq_text)
+from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, FileShard, check_input_path, file_reader_device,
+                      get_record_iterator, is_record, read_batches, seq_text)
 from .packing import PackedReads, pack_sequences
 from .result import MatrixResult, ModelResult
 from .util import default_device, slugify
@@ -162,8 +162,9 @@ class ProbabilisticFilterModel:
         self.index = bank
 
     # ------------------------------------------------------------ queries
-    def _query(self, packed: PackedReads, step: int):
-        """(hits, num_kmers) of one batch; the hit matrix comes back in the
+    def _query(self, packed, step: int):
+        """(hits, num_kmers) of one batch (PackedReads or a device-mode reader
+        batch); the hit matrix comes back in the
         narrowest integer type that holds the batch's largest k-mer count."""
         if self.index is None:
             raise ValueError("The model has not been trained yet")
@@ -219,17 +220,20 @@ class ProbabilisticFilterModel:
         """A FASTA/FASTQ file (or its part ``part`` of ``parts``, FileShard)
         streamed through the native reader: batch i+1 is parsed while batch i
         is probed, and no per-record objects are built (the reference iterates
-        Bio.SeqIO records, :316-330)."""
+        Bio.SeqIO records, :316-330).  On a GPU bank the reader runs in device
+        mode (file_io.file_reader_device): the window's text goes to HBM and
+        the probe reads the records there."""
         check_input_path(path)
         if self.index is None:
             raise ValueError("The model has not been trained yet")
         ids: list[str] = []
         lens, hits, nks = [], [], []
-        for batch in read_batches(path, part=part, parts=parts):
+        dev = file_reader_device(self.index)
+        for batch in read_batches(path, part=part, parts=parts, device=dev):
             L = batch.lengths()
             if (L <= self.k).any():
                 raise ValueError("Invalid sequence, must be longer than k")
-            h, n = self._query(batch.packed, step)
+            h, n = self._query(batch if dev is not None else batch.packed, step)
             ids += batch.ids()
             lens.append(L)
             hits.append(h)
