@@ -31,5 +31,5 @@ echo "== mlst"
 timeout -k 10 600 python -u bench.py --workload mlst > $F/mlst.json 2> $F/mlst.err || { tail -30 $F/mlst.err; exit 32; }
 cut -c1-300 $F/mlst.json
 echo "== kernel trace (species, no host path)"
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $F/trace -o run -- python bench.py --steps 10 --warmup 2 --no-host-path --no-cpu-baseline --no-e2e > $F/trace_bench.json 2> $F/trace.err || { tail -30 $F/trace.err; exit 33; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $F/trace -o run -- python bench.py --steps 10 --warmup 2 --no-host-path --no-cpu-baseline --no-e2e > $F/trace_bench.json 2> $F/trace.err || { tail -30 $F/trace.err; exit 33; }
 find $F/trace -name "*kernel_stats.csv" | head -3

@@ -202,6 +202,40 @@ class MatrixResult:
         n_all = self.job_total_kmers if self.job_total_hits is not None else int(self.num_kmers.sum())
         return {label: round(v / n_all, 2) for label, v in self.get_total_hits().items()}
 
+    def get_filter_mask(self, label: str, filter_threshold: float) -> dict[str, bool]:
+        """ModelResult.get_filter_mask (result.py:92-123) over the matrix:
+        {read id: round(h / n, 2) >= threshold} for `label`'s column, or with
+        threshold -1 whether `label`'s rounded score is the read's largest.
+        Python's round is applied to each distinct (h, n) pair, so every
+        decision is the reference's."""
+        if filter_threshold < 0 and not filter_threshold == -1 or filter_threshold > 1:
+            raise ValueError("The filter threshold must be between 0 and 1.")
+        if self._needs_dicts():
+            return self.to_model_result().get_filter_mask(label, filter_threshold)
+        if not self.ids:
+            raise IndexError("list index out of range")  # get_scores -> get_total_hits, as the reference
+        docs = self.docs.tolist()
+        col = next((d for d in docs if self.labels[d] == label), None)
+        if col is None:
+            raise KeyError(label)  # score[label] in the reference
+        n = self.num_kmers.astype(np.uint64)
+        h = self.hits[:, col].astype(np.uint64)
+        if filter_threshold == -1:
+            hmax = self.hits[:, self.docs].max(axis=1).astype(np.uint64)
+            keys = np.concatenate([(h << np.uint64(32)) | n, (hmax << np.uint64(32)) | n])
+        else:
+            keys = (h << np.uint64(32)) | n
+        uniq, inv = np.unique(keys, return_inverse=True)
+        score = np.fromiter((round(int(k >> 32) / int(k & 0xFFFFFFFF), 2) for k in uniq.tolist()),
+                            dtype=np.float64, count=uniq.size)[inv]
+        m = len(self.ids)
+        keep = score[:m] == score[m:] if filter_threshold == -1 else score >= filter_threshold
+        return dict(zip(self.ids, keep.tolist()))
+
+    def get_filtered_subsequence_labels(self, label: str, filter_threshold: float = 0.7) -> list[str]:
+        """ModelResult.get_filtered_subsequence_labels (result.py:125-149)."""
+        return [rid for rid, keep in self.get_filter_mask(label, filter_threshold).items() if keep]
+
     def best(self) -> tuple[np.ndarray, np.ndarray]:
         """(best doc or XS_BEST_AMBIGUOUS, max hits) per read, over the kept docs."""
         docs = self.docs
