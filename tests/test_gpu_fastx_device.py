@@ -229,3 +229,64 @@ def test_stale_device_batches_are_refused(tmp_path):
     with pytest.raises(RuntimeError, match="no longer valid"):
         b1.to_host()
     gb.close()
+
+
+def _outcome(path, max_bytes, device):
+    """The batches of a reader mode, or ('error', message) where it raises."""
+    try:
+        return _batches(path, max_bytes, device)
+    except ValueError as e:
+        return ("error", str(e))
+
+
+def _mutate(rng, text: bytes) -> bytes:
+    """One of: truncation at a random byte, random bytes spliced in (record
+    markers, whitespace, CR, bases), a blank line inserted, a line dropped."""
+    if not text:
+        return text
+    kind = int(rng.integers(0, 4))
+    pos = int(rng.integers(0, len(text)))
+    if kind == 0:
+        return text[:pos]
+    if kind == 1:
+        junk = _pick(rng, b"\n@+> \r\tACGTN", int(rng.integers(1, 6)))
+        return text[:pos] + junk + text[pos:]
+    nl = text.find(b"\n", pos)
+    if nl < 0:
+        return text
+    if kind == 2:
+        return text[:nl + 1] + b"\n" + text[nl + 1:]
+    nxt = text.find(b"\n", nl + 1)
+    return text[:nl + 1] + (text[nxt + 1:] if nxt >= 0 else b"")
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_fuzz_device_equals_host(tmp_path, seed):
+    """Malformed and well-formed inputs (the host sanitizer sweep's kinds:
+    truncations, spliced bytes, blank lines, dropped lines) in both formats
+    and at several window sizes: the device mode gives the host mode's batches,
+    or raises the host mode's error."""
+    rng = np.random.default_rng(1000 + seed)
+    kind = ["fq", "fasta", "fq_plain"][seed % 3]
+    n = int(rng.integers(1, 400))
+    if kind == "fasta":
+        text, ext = _fasta_text(rng, n, wrap=bool(seed % 2), crlf=seed % 4 == 1), "fasta"
+    elif kind == "fq":
+        text, ext = _fastq_text(rng, n, crlf=seed % 4 == 0, blank=seed % 5 == 0), "fq"
+    else:
+        text, ext = _plain_fastq(rng, n, crlf=seed % 2 == 1, tail_newline=seed % 3 != 0), "fastq"
+    for _ in range(int(rng.integers(0, 4))):
+        text = _mutate(rng, text)
+    p = tmp_path / f"f.{ext}"
+    p.write_bytes(text)
+    for mb in (int(rng.integers(1, 3000)), 50_000, 1 << 30):
+        host = _outcome(p, mb, None)
+        dev = _outcome(p, mb, 0)
+        if isinstance(host, tuple):
+            assert dev == host, (mb, host, dev if isinstance(dev, tuple) else "batches")
+            continue
+        assert not isinstance(dev, tuple), (mb, dev)
+        assert len(dev) == len(host)
+        for h, d in zip(host, dev):
+            for key in ("n", "offsets", "seqs", "ids", "descs", "text_offset"):
+                assert d[key] == h[key], (mb, key)
