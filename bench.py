@@ -28,7 +28,7 @@ filter word (h or K per k-mer).  The direct kernels: one 128-byte L2 line fill p
 k-mer and doc group; rbloom: K dwords per k-mer; MLST: the 64-byte rows
 themselves, its banks being Infinity-Cache resident).  Both + the read bytes,
 hit matrix and per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per
-probe from profiles/r02_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
+probe from profiles/r03_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
 OpenMP) on a bounded sample of the same reads and bank (rank 0, N=1 only);
 its hits are also compared with the GPU's; plus the reference's per-read loop
 shape on one core.  host_path: the same step from host buffers (PCIe).
@@ -96,7 +96,7 @@ def parse():
                     help="skip the end-to-end legs (the bench's reads as a FASTQ file -> totals / hit matrix)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r02_traffic.json"))
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r03_traffic.json"))
     return ap.parse_args()
 
 
@@ -411,14 +411,14 @@ def main():
         # the dominant pass against its own ceiling: L2 requests per launch (PMC,
         # scaled to this call's k-mers) over the lookup's live HIP-event time
         try:
-            pmc = json.loads((ROOT / "profiles" / "r02_pmc_cobspart.json").read_text())["kernels"]
+            pmc = json.loads((ROOT / "profiles" / "r03_pmc_cobspart.json").read_text())["kernels"]
             key = next(k for k in pmc if k.startswith("xs::cobs_lookup_kernel"))
             req = pmc[key]["TCC_REQ_sum"] * wl.kmers / (1_000_000 * 130)
             ach = req / (pass_ms["lookup"] * 1e-3)
             lookup_l2 = {"kernel": key, "bound": "l2_requests", "achieved": ach, "peak": L2_GATHER_PEAK_REQ,
                          "unit": "req/s", "frac": ach / L2_GATHER_PEAK_REQ, "requests_per_launch": req,
                          "lookup_ms_avg": pass_ms["lookup"],
-                         "source": "TCC_REQ_sum per dispatch from profiles/r02_pmc_cobspart.json (1 M reads; "
+                         "source": "TCC_REQ_sum per dispatch from profiles/r03_pmc_cobspart.json (1 M reads; "
                                    "scaled by k-mers); peak = pure L2 gathers, profiles/r02_l2gather.txt"}
         except Exception:
             lookup_l2 = None
