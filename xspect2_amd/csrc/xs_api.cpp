@@ -168,6 +168,8 @@ struct xs_bank {
     PinnedBuf stage[2];             // D2H staging ring for large host outputs
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
+    PinnedBuf small_h;              // small host calls: the whole request and its results (query_small)
+    DevBuf small_d;
     hipEvent_t hstage_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr, d2h_stream = nullptr;
     std::vector<hipEvent_t> chunk_ev;  // probe of batch chunk i done
@@ -813,6 +815,137 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     return XS_OK;
 }
 
+// ---- small host calls ------------------------------------------------------------
+// A request of a few reads (a serving loop's request, the per-read drop-in
+// `search` of INTEGRATION.md §2) costs its launches, copies and syncs, not its
+// probe: query_host's unit pipeline (units, scan, scatter), staging ring and
+// three streams take 150-200 us for one read.  Here the host builds the unit
+// map and packs the whole request into one pinned buffer: one H2D copy, the
+// same direct probe kernel as query_host's gather path, one D2H copy of the
+// per-block partials and the hit rows, one sync.  k-mer counts are the host's
+// own (the formula of units_kernel), totals the sum of the partials.
+constexpr uint64_t kSmallReads = 4096;
+constexpr uint64_t kSmallBytes = 1u << 20;  // sequence bytes of the request
+constexpr uint64_t kSmallUnits = 8192;
+constexpr uint64_t kSmallUnitsPerBlock = 4;  // 4 waves taking 1 unit per grab (ReadView::grab)
+
+size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+// XSPECT2_AMD_SMALL=0 sends every call through query_host (A/B, tests).
+bool small_enabled() {
+    const char* e = getenv("XSPECT2_AMD_SMALL");
+    return !e || atoi(e) != 0;
+}
+
+// *done = false: the call does not qualify (nothing was enqueued).  Hit rows
+// go to hits_host as hit_bytes-wide counts (the caller checked the width).
+int query_small(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
+                void* hits_host, int hit_bytes, uint64_t* nk_host, uint64_t* tot_host, bool* done) {
+    *done = false;
+    if (b->profiling || n == 0 || n > kSmallReads || !small_enabled()) return XS_OK;
+    const uint64_t base = offsets[0];
+    for (uint64_t r = 0; r < n; ++r)
+        if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    const uint64_t bytes = offsets[n] - base;
+    if (bytes > kSmallBytes) return XS_OK;
+    const bool bloom = b->kind == XS_BANK_RBLOOM;
+    const uint64_t cols = bloom ? 1 : b->D;
+    const uint64_t pcols = cols + 1;
+    std::vector<uint64_t> nk(n), uofs(n + 1);
+    uint64_t U = 0;
+    bool zero_rows = false;  // rows the probe does not store whole (no k-mers, or several units)
+    for (uint64_t r = 0; r < n; ++r) {
+        const uint64_t len = offsets[r + 1] - offsets[r];
+        nk[r] = len >= b->k ? (len - b->k) / step + 1 : 0;
+        const uint64_t s = (nk[r] + kSegKmers - 1) / kSegKmers;
+        zero_rows |= s != 1;
+        uofs[r] = U;
+        U += s;
+    }
+    uofs[n] = U;
+    if (U > kSmallUnits) return XS_OK;
+    // only where query_host would take the direct / gather probe as well (a forced
+    // or member-rich partitioned path keeps its own pipeline)
+    if (bloom) {
+        if (b->bloom_pending && hipEventQuery(b->bloom_ev) == hipSuccess) {  // as run_query
+            const uint64_t* t = static_cast<const uint64_t*>(b->bloom_tot_h.p);
+            if (t[1]) b->member_frac = (double)t[0] / (double)t[1];
+            b->bloom_pending = false;
+        }
+        (void)hipGetLastError();  // hipErrorNotReady is not an error here
+        BloomPartPlan plan;
+        if (bloom_part_plan(b->bloom_view(), n, bytes, step, b->member_frac, &plan)) return XS_OK;
+    } else {
+        CobsPartPlan plan;
+        if (cobs_part_plan(b->cobs_view(), b->k, n, bytes, step, &plan)) return XS_OK;
+    }
+    const int blocks = (int)std::min<uint64_t>((uint64_t)probe_grid(b), std::max<uint64_t>(1, (U + kSmallUnitsPerBlock - 1) / kSmallUnitsPerBlock));
+    // device / pinned layout: [queue | offsets | unit_ofs | unit_read | seqs] [partials | hits]
+    const size_t o_off = 16, o_uofs = o_off + align16((n + 1) * 8), o_uread = o_uofs + align16((n + 1) * 8);
+    const size_t o_seq = o_uread + align16(U * 4 + 4);
+    const size_t in_bytes = o_seq + align16(bytes + kPad);
+    const size_t o_part = in_bytes, part_bytes = align16((size_t)blocks * pcols * 8);
+    const size_t o_hits = o_part + part_bytes;
+    const size_t out_bytes = part_bytes + (hits_host ? n * cols * 4 : 0);
+    if (int rc = b->small_h.ensure(in_bytes + out_bytes)) return rc;
+    if (int rc = b->small_d.ensure(in_bytes + out_bytes)) return rc;
+    char* h = static_cast<char*>(b->small_h.p);
+    char* d = static_cast<char*>(b->small_d.p);
+    auto* q = reinterpret_cast<uint64_t*>(h);
+    q[0] = U;
+    q[1] = 0;
+    auto* ho = reinterpret_cast<uint64_t*>(h + o_off);
+    for (uint64_t r = 0; r <= n; ++r) ho[r] = offsets[r] - base;
+    memcpy(h + o_uofs, uofs.data(), (n + 1) * 8);
+    auto* ur = reinterpret_cast<uint32_t*>(h + o_uread);
+    for (uint64_t r = 0; r < n; ++r)
+        for (uint64_t u = uofs[r]; u < uofs[r + 1]; ++u) ur[u] = (uint32_t)r;
+    if (bytes) memcpy(h + o_seq, seqs + base, bytes);
+    memset(h + o_seq + bytes, 0, kPad);
+    const hipStream_t s = b->stream;
+    HIPCHK(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, s));
+    uint32_t* d_hits = hits_host ? reinterpret_cast<uint32_t*>(d + o_hits) : nullptr;
+    if (d_hits && zero_rows) HIPCHK(hipMemsetAsync(d_hits, 0, n * cols * 4, s));
+    ReadView rv;
+    rv.seq = reinterpret_cast<const uint8_t*>(d + o_seq);
+    rv.seq_bytes = bytes;
+    rv.offs = reinterpret_cast<const uint64_t*>(d + o_off);
+    rv.unit_read = reinterpret_cast<const uint32_t*>(d + o_uread);
+    rv.unit_ofs = reinterpret_cast<const uint64_t*>(d + o_uofs);
+    rv.queue = reinterpret_cast<uint64_t*>(d);
+    rv.n = n;
+    rv.k = b->k;
+    rv.step = step;
+    rv.grab = 1;
+    auto* d_part = reinterpret_cast<uint64_t*>(d + o_part);
+    if (bloom) HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, d_part, blocks, s));
+    else HIPCHK(launch_probe_cobs(rv, b->cobs_view(), d_hits, d_part, blocks, s));
+    HIPCHK(hipMemcpyAsync(h + o_part, d + o_part, out_bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    b->last_path = XS_PATH_GATHER;
+    const auto* part = reinterpret_cast<const uint64_t*>(h + o_part);
+    std::vector<uint64_t> tot(pcols, 0);
+    for (int i = 0; i < blocks; ++i)
+        for (uint64_t c = 0; c < pcols; ++c) tot[c] += part[(uint64_t)i * pcols + c];
+    if (bloom) {  // the next query's path choice follows this one's member fraction
+        if (tot[1]) b->member_frac = (double)tot[0] / (double)tot[1];
+        b->bloom_pending = false;
+    }
+    if (tot_host) memcpy(tot_host, tot.data(), pcols * 8);
+    if (nk_host) memcpy(nk_host, nk.data(), n * 8);
+    if (hits_host) {
+        const auto* hr = reinterpret_cast<const uint32_t*>(h + o_hits);
+        const uint64_t m = n * cols;
+        if (hit_bytes == 4) memcpy(hits_host, hr, m * 4);
+        else if (hit_bytes == 2)
+            for (uint64_t i = 0; i < m; ++i) static_cast<uint16_t*>(hits_host)[i] = (uint16_t)hr[i];
+        else
+            for (uint64_t i = 0; i < m; ++i) static_cast<uint8_t*>(hits_host)[i] = (uint8_t)hr[i];
+    }
+    *done = true;
+    return XS_OK;
+}
+
 xs_bank* new_bank(int device, int kind) {
     xs_bank* b = new xs_bank();
     b->device = device;
@@ -1078,6 +1211,9 @@ static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uin
     std::lock_guard<std::mutex> lk(b->mu);
     HIPCHK(hipSetDevice(b->device));
     if (n == 0) return XS_OK;
+    bool done = false;
+    if (int rc = query_small(b, seqs, offsets, n, step, hits_out, hit_bytes, num_kmers_out, nullptr, &done)) return rc;
+    if (done) return XS_OK;
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     uint32_t* d_hits = nullptr;
     uint64_t* d_nk = nullptr;
@@ -1174,6 +1310,31 @@ int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_
         if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
         return XS_OK;
     }
+    if (n <= kSmallReads) {  // the per-read call of a small request, made on the host from its hit rows
+        std::vector<uint32_t> rows(n * cols);
+        std::vector<uint64_t> tot(cols + 1);
+        bool done = false;
+        if (int rc = query_small(b, seqs, offsets, n, step, rows.data(), 4, num_kmers_out, tot.data(), &done)) return rc;
+        if (done) {
+            for (uint64_t r = 0; r < n; ++r) {  // best_doc_kernel's rule: a unique maximum, else ambiguous
+                const uint32_t* row = rows.data() + r * cols;
+                uint32_t m = 0, arg = 0, cnt = 0;
+                for (uint64_t c = 0; c < cols; ++c) {
+                    if (cnt == 0 || row[c] > m) {
+                        m = row[c];
+                        arg = (uint32_t)c;
+                        cnt = 1;
+                    } else if (row[c] == m) {
+                        ++cnt;
+                    }
+                }
+                best_doc[r] = cnt == 1 ? arg : kBestAmbiguous;
+                if (best_hits) best_hits[r] = m;
+            }
+            if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
+            return XS_OK;
+        }
+    }
     if (int rc = b->hits.ensure(n * cols * 4)) return rc;
     if (int rc = b->nk.ensure(n * 8)) return rc;
     if (int rc = b->best.ensure(n * 8)) return rc;
@@ -1223,7 +1384,10 @@ int xs_query_totals(xs_bank* b, const char* seqs, const uint64_t* offsets, uint6
         return XS_OK;
     }
     std::vector<uint64_t> t(cols + 1);
-    if (int rc = query_host(b, seqs, offsets, n, step, nullptr, nullptr, nullptr, t.data())) return rc;
+    bool done = false;
+    if (int rc = query_small(b, seqs, offsets, n, step, nullptr, 4, nullptr, t.data(), &done)) return rc;
+    if (!done)
+        if (int rc = query_host(b, seqs, offsets, n, step, nullptr, nullptr, nullptr, t.data())) return rc;
     memcpy(totals_out, t.data(), cols * 8);
     if (total_kmers_out) *total_kmers_out = t[cols];
     return XS_OK;

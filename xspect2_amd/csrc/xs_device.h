@@ -387,12 +387,11 @@ __device__ __forceinline__ uint64_t num_kmers(uint64_t len, uint32_t k, uint32_t
     return len >= k ? (len - k + step) / step : 0;  // ceil((len-k+1)/step)
 }
 
-// Hand out kGrab units per atomic to balance ragged reads across waves.
-constexpr uint32_t kGrab = 4;
-
-__device__ __forceinline__ uint64_t grab_units(uint64_t* queue, int lane) {
+// Hand out `grab` units per atomic (ReadView::grab: 4 balances ragged reads
+// across waves; a small request takes 1, so every unit gets a wave).
+__device__ __forceinline__ uint64_t grab_units(uint64_t* queue, int lane, uint32_t grab) {
     uint64_t base = 0;
-    if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long*>(queue + 1), (unsigned long long)kGrab);
+    if (lane == 0) base = atomicAdd(reinterpret_cast<unsigned long long*>(queue + 1), (unsigned long long)grab);
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
     return ((uint64_t)hi << 32) | lo;

@@ -65,6 +65,7 @@ struct ReadView {
     uint64_t n;
     uint32_t k;
     uint32_t step;
+    uint32_t grab = 4;         // units a wave takes from the queue per atomic (small calls: 1)
 };
 
 // ---- launchers (xs_kernels.hip) -------------------------------------------

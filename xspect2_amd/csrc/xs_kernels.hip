@@ -104,9 +104,9 @@ __global__ void __launch_bounds__(kProbeThreads) probe_bloom_kernel(ReadView rv,
     uint64_t hit_total = 0, kmer_total = 0, rows_total = 0;
 
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];
@@ -167,9 +167,9 @@ __global__ void __launch_bounds__(kProbeThreads) build_cobs_kernel(ReadView rv,
     const uint32_t h = HT ? HT : bv.h;
     const uint64_t U = rv.queue[0];
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];
@@ -205,9 +205,9 @@ __global__ void __launch_bounds__(kProbeThreads) build_bloom_kernel(ReadView rv,
     const uint32_t k = KT ? KT : rv.k;
     const uint64_t U = rv.queue[0];
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];

@@ -6,7 +6,7 @@ namespace xs {
 // ------------------------------------------------------------------ COBS probe (fast)
 // Classic bank with D <= 128 docs: one 16-byte row per hash, counters in
 // registers.  One wavefront per unit (<= kSegKmers k-mers of one read), one
-// lane per k-mer; units are handed out kGrab at a time.
+// lane per k-mer; units are handed out rv.grab at a time.
 struct FastBank {
     const uint8_t* rows;
     uint64_t sig, magic;
@@ -48,9 +48,9 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
     uint64_t kmer_total = 0;
 
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];

@@ -30,9 +30,9 @@ __global__ void __launch_bounds__(kProbeThreads) probe_cobs_kernel(ReadView rv, 
     uint64_t kmer_total = 0;
 
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];

@@ -62,9 +62,9 @@ __global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_
     uint64_t kmer_total = 0;
 
     for (;;) {
-        const uint64_t base = grab_units(rv.queue, lane);
+        const uint64_t base = grab_units(rv.queue, lane, rv.grab);
         if (base >= U) break;
-        const uint64_t uend = min(base + kGrab, U);
+        const uint64_t uend = min(base + rv.grab, U);
         for (uint64_t u = base; u < uend; ++u) {
             const uint32_t r = rv.unit_read[u];
             const uint64_t seg = u - rv.unit_ofs[r];
