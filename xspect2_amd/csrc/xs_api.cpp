@@ -1310,7 +1310,7 @@ int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_
         if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
         return XS_OK;
     }
-    if (n <= kSmallReads) {  // the per-read call of a small request, made on the host from its hit rows
+    if (n <= kSmallReads && n * cols <= (1u << 16)) {  // a small request: the per-read call made on the host
         std::vector<uint32_t> rows(n * cols);
         std::vector<uint64_t> tot(cols + 1);
         bool done = false;
