@@ -271,6 +271,16 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
                              const uint64_t* total_hits, uint64_t total_kmers, const uint32_t* total_order_row,
                              int threads);
 
+/* ---- Packed read ids (ASCII only; a byte >= 0x80 is XS_ERR_ARG and the caller
+ * falls back to Python).  xs_ids_json_quote: json.dumps(id) of every id (the
+ * "hits"/"scores"/"num_kmers" keys ModelResult.save writes, result.py:191-202),
+ * packed with n+1 offsets; out_cap >= 6 * offs[n] + 2 * n.
+ * xs_ids_has_duplicates: whether two ids are equal (the reference's hits dict
+ * keeps the last record of a repeated id, probabilistic_filter_model.py:310). */
+int xs_ids_json_quote(const char* buf, const uint64_t* offs, uint64_t n, char* out, uint64_t out_cap,
+                      uint64_t* out_offs);
+int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int* has_dup);
+
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
  * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path
  * probabilistic_filter_model.py:316-330).  Records come out packed the way

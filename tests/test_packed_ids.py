@@ -1,0 +1,80 @@
+"""PackedIds (read ids kept as the reader's buffer + offsets) against the
+list-of-strings semantics it replaces (CPU): json.dumps quoting
+(xs_ids_json_quote), duplicate detection (xs_ids_has_duplicates),
+membership, slicing, concatenation, and MatrixResult.save writing the same
+bytes with packed or listed ids (result.py:151-202 via json.dumps)."""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+import pytest
+
+from xspect2_amd.packing import PackedIds
+from xspect2_amd.result import MatrixResult, _json_packed
+
+
+def _ids(rng, n, alphabet):
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(0, 12))
+        out.append("".join(rng.choice(alphabet, L)))
+    return out
+
+
+ASCII = list("abcXYZ019_-.:|/ ") + ['"', "\\", "\n", "\r", "\t", "\b", "\f", "\x00", "\x01", "\x1f", "\x7f"]
+
+
+@pytest.mark.parametrize("seed", range(5))
+def test_json_quote_and_duplicates_match_python(seed):
+    rng = np.random.default_rng(seed)
+    ids = _ids(rng, 3000, ASCII)
+    if seed % 2:
+        ids = list(dict.fromkeys(ids))  # no repeats
+    p = PackedIds.of(ids)
+    assert p.is_ascii and p == ids and len(p) == len(ids)
+    assert p.json_packed()[0] == _json_packed(ids)[0]
+    assert np.array_equal(p.json_packed()[1], _json_packed(ids)[1])
+    assert p.has_duplicates() == (len(set(ids)) != len(ids))
+
+
+def test_non_ascii_ids_fall_back_to_python():
+    ids = ["r1", "é", "ü∑", "r1x", "\U0001F600"]
+    p = PackedIds.of(ids)
+    assert not p.is_ascii and p.tolist() == ids
+    assert p.json_packed()[0] == b"".join(json.dumps(s).encode() for s in ids)
+    assert not p.has_duplicates() and PackedIds.of(ids + ["é"]).has_duplicates()
+    raw = PackedIds(b"a\xffb\xfe", np.array([0, 2, 4], dtype=np.uint64))  # invalid UTF-8: replacement chars
+    assert raw.tolist() == [b"a\xff".decode("utf-8", "replace"), b"b\xfe".decode("utf-8", "replace")]
+
+
+def test_membership_slicing_concat():
+    ids = ["total1", "xtotal", "tot", "al", "total", "", "r7"]
+    p = PackedIds.of(ids)
+    for s in ids + ["otal", "totalx", "to", "r", "7", "missing"]:
+        assert (s in p) == (s in ids), s
+    assert "total" not in PackedIds.of(["total1", "xtotal", "tota", "ltotal"])
+    assert "" not in PackedIds.of(["a", "b"]) and "" in PackedIds.of(["a", "", "b"])
+    assert p[2:5] == ids[2:5] and p[::2] == ids[::2] and p[-1] == ids[-1] and list(p) == ids
+    q = PackedIds.concat([p[0:3], p[3:], PackedIds.of(["z"])])
+    assert q == ids + ["z"] and q.json_packed()[0] == _json_packed(ids + ["z"])[0]
+    assert PackedIds.concat([PackedIds.of([])]) == []
+
+
+@pytest.mark.parametrize("dup", [False, True])
+def test_matrix_result_with_packed_ids_writes_the_same_json(tmp_path, dup):
+    rng = np.random.default_rng(3)
+    n, D = 500, 7
+    ids = [f"read_{i % 300 if dup else i}\t\"q\"" for i in range(n)]
+    hits = rng.integers(0, 50, (n, D)).astype(np.uint8)
+    nk = rng.integers(50, 60, n).astype(np.uint64)
+    labels = [f"L{d}" for d in range(D)]
+    a = MatrixResult("slug", ids, labels, hits, nk, input_source="x.fq")
+    b = MatrixResult("slug", PackedIds.of(ids), labels, hits, nk, input_source="x.fq")
+    assert isinstance(b.ids, PackedIds) != dup  # repeated ids collapse through the list path
+    a.save(tmp_path / "a.json")
+    b.save(tmp_path / "b.json")
+    assert (tmp_path / "a.json").read_bytes() == (tmp_path / "b.json").read_bytes()
+    assert b.get_filter_mask("L3", 0.5) == a.get_filter_mask("L3", 0.5)
+    with pytest.raises(ValueError, match="reserved"):
+        MatrixResult("slug", PackedIds.of(["a", "total"]), ["x"], np.zeros((2, 1), np.uint8), np.ones(2))

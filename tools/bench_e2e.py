@@ -10,6 +10,8 @@ bench's config-2 bank), then times:
              (H2D, probe, D2H of the n x D hit matrix), parse overlapped
   e2e_tot    same, but per-doc totals only (xs_query_totals, no hit matrix)
   e2e_best   read_batches -> Bank.query_best (per-read best doc on the device)
+  classify   ProbabilisticFilterModel.predict_columnar(file) + MatrixResult.save of
+             the whole file (the product's classify path, device-mode reader)
   json       MatrixResult.save (native writer) of the first 200k reads' result, and
              the per-read-dict ModelResult.save on a 20k-read sample, scaled
   py_parse   the pure-Python restatement of Bio.SeqIO (oracle/fastx.py) on a
@@ -246,6 +248,19 @@ def main():
     res["pipeline_kept_reads"] = outf["filtered"][0].read_bytes().count(b">") if outf["filtered"] else 0
     res["pipeline_identical"] = all(a.read_bytes() == b.read_bytes() for key in ("genus", "filtered", "species")
                                     for a, b in zip(outf[key], outr[key]))
+    # the product's classify path on the whole file: predict_columnar (device-mode
+    # reader, narrow hit rows back) then MatrixResult.save (the reference's JSON)
+    t = time.perf_counter()
+    cres = species.predict_columnar(fq)
+    res["classify_predict_s"] = time.perf_counter() - t
+    cres.input_source = fq.name
+    t = time.perf_counter()
+    cres.save(tmp / "classify.json")
+    res["classify_save_s"] = time.perf_counter() - t
+    res["classify_json_bytes"] = (tmp / "classify.json").stat().st_size
+    res["classify_reads"] = len(cres.ids)
+    (tmp / "classify.json").unlink()
+    del cres
     import shutil
     shutil.rmtree(tmp / "fused")
     shutil.rmtree(tmp / "three_pass")

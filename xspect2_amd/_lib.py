@@ -138,6 +138,8 @@ SIGNATURES = {
     "xs_bank_close": (None, [_vp]),
     "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _int, _vp, ctypes.c_char_p, _vp,
                                         ctypes.c_char_p, _vp, _vp, _vp, _u64, _vp, _int]),
+    "xs_ids_json_quote": (_int, [ctypes.c_char_p, _vp, _u64, _vp, _u64, _vp]),
+    "xs_ids_has_duplicates": (_int, [ctypes.c_char_p, _vp, _u64, ctypes.POINTER(_int)]),
     "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
     "xs_fastx_open_range": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),

@@ -317,3 +317,84 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
 }
 
 }  // extern "C"
+
+// ---- packed read ids ------------------------------------------------------------
+// The reader hands ids over as one byte buffer + offsets; a result of 10^6..10^7
+// reads keeps them that way (MatrixResult with PackedIds) instead of building
+// Python strings.  Both helpers take ASCII ids only (the caller checks; other
+// ids go through Python's own decoding and json.dumps).
+
+// json.dumps(id) with ensure_ascii (Python's json encoder, py_encode_basestring_ascii):
+// '"' and '\\' escaped, \n \r \t \b \f short forms, other bytes outside ' '..'~'
+// (< 0x20, 0x7f) as \u00xx (lower-case hex); everything else as is.
+int xs_ids_json_quote(const char* buf, const uint64_t* offs, uint64_t n, char* out, uint64_t out_cap,
+                      uint64_t* out_offs) {
+    if ((!buf && n && offs[n]) || !offs || (!out && n) || !out_offs) return xs::set_error(XS_ERR_ARG, "null argument");
+    static const char hex[] = "0123456789abcdef";
+    uint64_t o = 0;
+    out_offs[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
+        const uint64_t len = offs[i + 1] - offs[i];
+        if (o + 2 + 6 * len > out_cap) return xs::set_error(XS_ERR_ARG, "output buffer too small");
+        out[o++] = '"';
+        const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+        for (uint64_t j = 0; j < len; ++j) {
+            const unsigned char c = s[j];
+            if (c >= 0x80) return xs::set_error(XS_ERR_ARG, "non-ASCII id");
+            if (c == '"' || c == '\\') {
+                out[o++] = '\\';
+                out[o++] = (char)c;
+            } else if (c >= 0x20 && c < 0x7f) {
+                out[o++] = (char)c;
+            } else if (c == '\n' || c == '\r' || c == '\t' || c == '\b' || c == '\f') {
+                out[o++] = '\\';
+                out[o++] = c == '\n' ? 'n' : c == '\r' ? 'r' : c == '\t' ? 't' : c == '\b' ? 'b' : 'f';
+            } else {
+                out[o++] = '\\';
+                out[o++] = 'u';
+                out[o++] = '0';
+                out[o++] = '0';
+                out[o++] = hex[c >> 4];
+                out[o++] = hex[c & 15];
+            }
+        }
+        out[o++] = '"';
+        out_offs[i + 1] = o;
+    }
+    return XS_OK;
+}
+
+// *has_dup = 1 when two of the n ids are equal (byte for byte).  Open addressing
+// over a 64-bit FNV-1a of each id; equal hashes are compared in full.
+int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int* has_dup) {
+    if ((!buf && n && offs[n]) || !offs || !has_dup) return xs::set_error(XS_ERR_ARG, "null argument");
+    *has_dup = 0;
+    if (n < 2) return XS_OK;
+    uint64_t cap = 16;
+    while (cap < 2 * n) cap <<= 1;
+    std::vector<uint64_t> slot(cap, ~0ull);  // id index + 1 of the occupant, ~0 = empty
+    std::vector<uint64_t> hv(cap);
+    for (uint64_t i = 0; i < n; ++i) {
+        const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+        const uint64_t len = offs[i + 1] - offs[i];
+        uint64_t hsh = 1469598103934665603ull;
+        for (uint64_t j = 0; j < len; ++j) hsh = (hsh ^ s[j]) * 1099511628211ull;
+        hsh ^= hsh >> 29;
+        for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
+            if (slot[p] == ~0ull) {
+                slot[p] = i;
+                hv[p] = hsh;
+                break;
+            }
+            if (hv[p] == hsh) {
+                const uint64_t k = slot[p];
+                if (offs[k + 1] - offs[k] == len && memcmp(buf + offs[k], s, len) == 0) {
+                    *has_dup = 1;
+                    return XS_OK;
+                }
+            }
+        }
+    }
+    return XS_OK;
+}

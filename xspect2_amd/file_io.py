@@ -19,7 +19,7 @@ import numpy as np
 
 from ._lib import (XS_ERR_FORMAT, XS_FASTX_FASTA, XS_FASTX_FASTQ, XS_FASTX_PINNED, FastxBatch, FastxDBatch,
                    check, load)
-from .packing import PackedReads
+from .packing import PackedIds, PackedReads
 
 FASTA_ENDINGS = ["fasta", "fna", "fa", "ffn", "frn"]  # definitions.py:6
 FASTQ_ENDINGS = ["fastq", "fq"]                       # definitions.py:7
@@ -100,6 +100,10 @@ class SeqBatch:
             return [s[o[i]:o[i + 1]] for i in range(self.n)]
         return [raw[o[i]:o[i + 1]].decode("utf-8", errors="replace") for i in range(self.n)]
 
+    def ids_packed(self) -> PackedIds:
+        """The ids as one buffer + offsets (no Python string per read)."""
+        return PackedIds(self._ids_raw, self._ioffs)
+
     def descriptions(self) -> list[str]:
         """Record titles (header line without '>'/'@', right-stripped)."""
         raw, o = self._descs_raw, self._doffs.tolist()
@@ -177,6 +181,11 @@ class DeviceSeqBatch:
         if self._ids_raw is None:
             self._ids_raw, self._ioffs = self._text(1)
         return SeqBatch.ids(self)
+
+    def ids_packed(self) -> PackedIds:
+        if self._ids_raw is None:
+            self._ids_raw, self._ioffs = self._text(1)
+        return PackedIds(self._ids_raw, self._ioffs)
 
     def descriptions(self) -> list[str]:
         if self._descs_raw is None:

@@ -21,7 +21,7 @@ from .bank import Bank, cobs_signature_size
 from ._lib import XS_BANK_COBS_CLASSIC
 from .file_io import (FASTA_ENDINGS, FASTQ_ENDINGS, FileShard, check_input_path, file_reader_device,
                       get_record_iterator, is_record, read_batches, seq_text)
-from .packing import PackedReads, pack_sequences
+from .packing import PackedIds, PackedReads, pack_sequences
 from .result import MatrixResult, ModelResult
 from .util import default_device, slugify
 
@@ -226,7 +226,7 @@ class ProbabilisticFilterModel:
         check_input_path(path)
         if self.index is None:
             raise ValueError("The model has not been trained yet")
-        ids: list[str] = []
+        ids: list[PackedIds] = []
         lens, hits, nks = [], [], []
         dev = file_reader_device(self.index)
         for batch in read_batches(path, part=part, parts=parts, device=dev):
@@ -234,13 +234,13 @@ class ProbabilisticFilterModel:
             if (L <= self.k).any():
                 raise ValueError("Invalid sequence, must be longer than k")
             h, n = self._query(batch if dev is not None else batch.packed, step)
-            ids += batch.ids()
+            ids.append(batch.ids_packed())  # the reader's id buffer: no string per read
             lens.append(L)
             hits.append(h)
             nks.append(n)
         hits_m, nk = _stack(list(zip(hits, nks)), self.index.num_docs)
-        lens_l = np.concatenate(lens).tolist() if lens else []
-        return ids, lens_l, hits_m, nk
+        lens_a = np.concatenate(lens) if lens else np.zeros(0, dtype=np.uint64)
+        return PackedIds.concat(ids) if ids else [], lens_a, hits_m, nk
 
     def _collect(self, sequence_input) -> list:
         if is_record(sequence_input):

@@ -13,6 +13,8 @@ from pathlib import Path
 
 import numpy as np
 
+from .packing import PackedIds
+
 
 class ModelResult:
     """Hits per subsequence and label, plus the k-mer count of each subsequence."""
@@ -119,7 +121,9 @@ class MatrixResult:
     Per-read labels follow COBS result order (count descending, ties by doc
     index); ``doc_mask`` drops excluded docs (predict's exclude_ids).
     Duplicate read ids collapse as they do in the reference's dictionaries:
-    the first position, the last record's values.
+    the first position, the last record's values.  ``ids`` may be a
+    ``PackedIds`` (the reader's id buffer, as ``predict_columnar`` of a file
+    passes it): no Python string per read is made unless a caller reads one.
 
     ``hits`` may be uint8 / uint16 / uint32: a matrix narrowed on the device
     (counts never exceed a read's k-mer count) is kept narrow, and widened
@@ -128,7 +132,7 @@ class MatrixResult:
     the whole job's, all-reduced over the ranks (xspect2_amd.distributed).
     """
 
-    def __init__(self, model_slug: str, ids: list[str], labels: list[str], hits: np.ndarray,
+    def __init__(self, model_slug: str, ids: list[str] | PackedIds, labels: list[str], hits: np.ndarray,
                  num_kmers: np.ndarray, sparse_sampling_step: int = 1, prediction: str | None = None,
                  input_source: str | None = None, doc_mask: np.ndarray | None = None):
         if "total" in ids:
@@ -140,13 +144,15 @@ class MatrixResult:
         if hits.ndim != 2 or hits.shape[0] != len(ids) or hits.shape[1] != len(labels) or \
                 num_kmers.shape != (len(ids),):
             raise ValueError("hits must be [len(ids), len(labels)] and num_kmers [len(ids)]")
-        if len(set(ids)) != len(ids):
+        packed = isinstance(ids, PackedIds)
+        if (ids.has_duplicates() if packed else len(set(ids)) != len(ids)):
+            ids = list(ids)
             last = {rid: i for i, rid in enumerate(ids)}
             first_order = list(dict.fromkeys(ids))
             rows = np.array([last[rid] for rid in first_order], dtype=np.int64)
             ids, hits, num_kmers = first_order, hits[rows], num_kmers[rows]
         self.model_slug = model_slug
-        self.ids = list(ids)
+        self.ids = ids if isinstance(ids, PackedIds) else list(ids)
         self.labels = list(labels)
         self.hits = hits
         self.num_kmers = num_kmers
@@ -267,7 +273,7 @@ class MatrixResult:
             dumps("model_slug"), dumps(self.model_slug), dumps("sparse_sampling_step"),
             dumps(self.sparse_sampling_step))
         path.write_text(head, encoding="utf-8")
-        ids_b, ids_off = _json_packed(self.ids)
+        ids_b, ids_off = self.ids.json_packed() if isinstance(self.ids, PackedIds) else _json_packed(self.ids)
         lab_b, lab_off = _json_packed(self.labels)
         mask = self.doc_mask
         vp = ctypes.c_void_p
