@@ -84,6 +84,12 @@ int xs_device_count(int* count);
 
 /* Open a bank file and make it resident on `device`.  kind = XS_BANK_*. */
 int xs_bank_open(const char* path, int kind, int device, xs_bank** out);
+/* A classic COBS index with only docs [doc_lo, doc_hi) resident: each row's
+ * byte columns of those docs (doc_lo and doc_hi multiples of 8, or doc_hi the
+ * doc count).  One bank column-split over ranks (SURVEY.md §8(e) config 5,
+ * option b): every rank hashes every k-mer and reads its slice of each row;
+ * the per-read hit columns are then all-gathered (xspect2_amd.distributed). */
+int xs_bank_open_docs(const char* path, int device, uint64_t doc_lo, uint64_t doc_hi, xs_bank** out);
 
 /* Create an empty COBS bank (classic: num_groups = 1 and page_size =
  * ceil(num_docs/8); compact: num_groups groups of 8*page_size docs each, the

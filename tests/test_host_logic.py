@@ -231,3 +231,27 @@ def test_bench_metric_is_baseline_metric():
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.METRIC == json.loads((root / "BASELINE.json").read_text())["metric"]
+
+
+def test_doc_slices_cover_the_bank_in_byte_columns(tmp_path):
+    """distributed.doc_slice: contiguous, in order, bounds multiples of 8 (the
+    last ends at D), every rank non-empty; too many ranks refused.
+    cobs_classic_docs reads the document count of the restated file layout."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+    import oracle
+    from xspect2_amd.distributed import cobs_classic_docs, doc_slice
+    for D in (1, 8, 9, 13, 100, 128, 129, 2000, 2100):
+        R = (D + 7) // 8
+        for world in range(1, min(R, 9) + 1):
+            sl = [doc_slice(D, r, world) for r in range(world)]
+            assert sl[0][0] == 0 and sl[-1][1] == D
+            assert all(a[1] == b[0] for a, b in zip(sl, sl[1:]))
+            assert all(lo < hi and lo % 8 == 0 and (hi % 8 == 0 or hi == D) for lo, hi in sl)
+        with pytest.raises(ValueError):
+            doc_slice(D, 0, R + 1)
+    names = [f"d{i}" for i in range(13)]
+    p = tmp_path / "index.cobs_classic"
+    p.write_bytes(oracle.cobs_classic_file(names, 21, 7, 11, np.zeros((11, 2), dtype=np.uint8)))
+    assert cobs_classic_docs(p) == 13

@@ -11,6 +11,11 @@ Config 5 (docs sharded; one genus model per rank, every read on every rank):
     torchrun --nproc-per-node N tools/sharded_classify.py docs-shard --root DIR
     python tools/sharded_classify.py docs-check  --root DIR
 
+Config 5 with ONE bank column-split over the ranks (the `setup` model):
+    python tools/sharded_classify.py bank-single --root DIR        # predict_columnar -> bank_single.json
+    torchrun --nproc-per-node N tools/sharded_classify.py bank-shard --root DIR
+    python tools/sharded_classify.py bank-check  --root DIR
+
 `shard` runs xspect2_amd.classify.classify_species_sharded: each rank parses
 its byte range of reads.fq, the D+1 totals are all-reduced (RCCL, or gloo
 with XSPECT_SHARE_GPU=1 when the ranks share one GPU), rank 0 forms the SVM
@@ -82,7 +87,7 @@ def docs_setup(root: Path, n_reads: int, world: int) -> None:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("cmd", choices=["setup", "single", "shard", "check", "docs-setup", "docs-single", "docs-shard",
-                                    "docs-check"])
+                                    "docs-check", "bank-single", "bank-shard", "bank-check"])
     ap.add_argument("--root", required=True)
     ap.add_argument("--reads", type=int, default=200_000)
     ap.add_argument("--world", type=int, default=2)
@@ -145,6 +150,40 @@ def main() -> int:
             res.save(root / "docs_sharded.json")
         dist.barrier()
         dist.destroy_process_group()
+    elif a.cmd == "bank-single":
+        from xspect2_amd import classify
+        from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+        res = ProbabilisticFilterSVMModel.load(classify.species_model_path(GENUS)).predict_columnar(
+            root / "reads.fq", step=a.step)
+        res.input_source = "reads.fq"
+        res.save(root / "bank_single.json")
+    elif a.cmd == "bank-shard":
+        import torch
+        import torch.distributed as dist
+        from xspect2_amd import classify, distributed
+        from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+        share = os.environ.get("XSPECT_SHARE_GPU") == "1"
+        local = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
+        os.environ["XSPECT2_AMD_DEVICE"] = str(local)
+        torch.cuda.set_device(local)
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        model = distributed.load_docs_slice(ProbabilisticFilterSVMModel, classify.species_model_path(GENUS))
+        print(f"rank {dist.get_rank()}: docs {model.index.num_docs}", file=sys.stderr)
+        res = distributed.predict_bank_sharded(model, root / "reads.fq", step=a.step)
+        if dist.get_rank() == 0:
+            res.save(root / "bank_sharded.json")
+        dist.barrier()
+        dist.destroy_process_group()
+    elif a.cmd == "bank-check":
+        a_ = (root / "bank_single.json").read_bytes()
+        b_ = (root / "bank_sharded.json").read_bytes()
+        d = json.loads(a_)
+        print(json.dumps({"docs": len(d["scores"]["total"]), "reads": len(d["hits"]), "equal_bytes": a_ == b_,
+                          "prediction": d.get("prediction"), "json_bytes": len(a_)}))
+        return 0 if a_ == b_ else 1
     elif a.cmd == "docs-check":
         a_ = (root / "docs_single.json").read_bytes()
         b_ = (root / "docs_sharded.json").read_bytes()

@@ -104,6 +104,7 @@ SIGNATURES = {
     "xs_last_error": (ctypes.c_char_p, []),
     "xs_device_count": (_int, [ctypes.POINTER(_int)]),
     "xs_bank_open": (_int, [ctypes.c_char_p, _int, _int, _pp]),
+    "xs_bank_open_docs": (_int, [ctypes.c_char_p, _int, _u64, _u64, _pp]),
     "xs_bank_create_cobs": (_int, [_int, _int, _u32, _u32, _u64, _u64, _u64, _vp, _vp, _pp]),
     "xs_bank_create_bloom": (_int, [_int, _u32, _u64, _u32, _pp]),
     "xs_bank_build": (_int, [_vp, _vp, _vp, _vp, _u64]),

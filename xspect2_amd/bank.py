@@ -97,11 +97,20 @@ class Bank:
 
     # ------------------------------------------------------------ creation
     @classmethod
-    def open(cls, path: str | Path, kind: int, device: int = 0, term_size: int | None = None) -> "Bank":
+    def open(cls, path: str | Path, kind: int, device: int = 0, term_size: int | None = None,
+             docs: tuple[int, int] | None = None) -> "Bank":
+        """Load an index file.  docs=(lo, hi): a classic COBS index with only
+        docs [lo, hi) resident (lo, hi multiples of 8 or hi = the doc count):
+        one rank's column slice of a docs-sharded bank (xs_bank_open_docs)."""
         path = Path(path)
         if not path.exists():
             raise FileNotFoundError(f"Index file not found at {path}")
         h = ctypes.c_void_p()
+        if docs is not None:
+            if kind != XS_BANK_COBS_CLASSIC:
+                raise ValueError("only classic COBS banks open as doc slices")
+            check(load().xs_bank_open_docs(str(path).encode(), device, int(docs[0]), int(docs[1]), ctypes.byref(h)))
+            return cls(h)
         check(load().xs_bank_open(str(path).encode(), kind, device, ctypes.byref(h)))
         bank = cls(h)
         if kind == XS_BANK_RBLOOM and term_size is not None:

@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -1025,6 +1026,54 @@ int xs_bank_open(const char* path, int kind, int device, xs_bank** out) {
         return rc;
     }
     *out = b;
+    return XS_OK;
+}
+
+int xs_bank_open_docs(const char* path, int device, uint64_t doc_lo, uint64_t doc_hi, xs_bank** out) {
+    if (!path || !out) return fail(XS_ERR_ARG, "null argument");
+    *out = nullptr;
+    Reader rd;
+    rd.f.open(path, std::ios::binary);
+    if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
+    rd.f.seekg(0, std::ios::end);
+    const uint64_t fsize = (uint64_t)rd.f.tellg();
+    rd.f.seekg(0);
+    xs_bank* full = new_bank(device, XS_BANK_COBS_CLASSIC);
+    std::unique_ptr<xs_bank> keep_full(full);
+    if (int rc = read_cobs_header(full, rd, path)) return rc;
+    const uint64_t D = full->D, R = full->page, S = full->sig[0];
+    if (doc_lo % 8 || doc_lo >= doc_hi || doc_hi > D || (doc_hi % 8 && doc_hi != D))
+        return fail(XS_ERR_ARG, "doc range [%llu, %llu) of %llu docs: bounds must be multiples of 8 (or the end)",
+                    (unsigned long long)doc_lo, (unsigned long long)doc_hi, (unsigned long long)D);
+    const uint64_t pos = (uint64_t)rd.f.tellg();
+    if (fsize - pos != S * R)
+        return fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
+                    (unsigned long long)(fsize - pos), (unsigned long long)(S * R));
+    xs_bank* b = new_bank(device, XS_BANK_COBS_CLASSIC);
+    std::unique_ptr<xs_bank> keep(b);
+    b->k = full->k;
+    b->h = full->h;
+    b->canonicalize = full->canonicalize;
+    b->D = doc_hi - doc_lo;
+    b->G = 1;
+    b->page = (b->D + 7) / 8;
+    b->sig.assign(1, S);
+    b->names.assign(full->names.begin() + (ptrdiff_t)doc_lo, full->names.begin() + (ptrdiff_t)doc_hi);
+    if (int rc = validate_geometry(b)) return rc;
+    if (int rc = alloc_image(b)) return rc;
+    // the rows' byte columns [doc_lo / 8, + page), read in pieces of rows
+    const uint64_t c0 = doc_lo / 8, P = b->page;
+    std::vector<uint8_t> payload(S * P);
+    constexpr uint64_t kRows = 1u << 20;
+    std::vector<uint8_t> piece(std::min(S, kRows) * R);
+    for (uint64_t r0 = 0; r0 < S; r0 += kRows) {
+        const uint64_t m = std::min(kRows, S - r0);
+        rd.f.read(reinterpret_cast<char*>(piece.data()), (std::streamsize)(m * R));
+        if (!rd.f) return fail(XS_ERR_IO, "%s: short read", path);
+        for (uint64_t r = 0; r < m; ++r) memcpy(payload.data() + (r0 + r) * P, piece.data() + r * R + c0, P);
+    }
+    if (int rc = upload_payload(b, payload.data(), payload.size())) return rc;
+    *out = keep.release();
     return XS_OK;
 }
 

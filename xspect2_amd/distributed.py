@@ -30,7 +30,7 @@ from typing import Callable
 
 import numpy as np
 
-from .packing import PackedReads
+from .packing import PackedIds, PackedReads
 
 
 def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
@@ -356,6 +356,56 @@ def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: b
     and only the gathered matrix, narrowed to the reads' count width, comes
     back.  Under gloo (CPU tests, shared-GPU rehearsal) the rows are probed
     from host buffers and gathered through the host."""
+    return _predict_doc_columns(model, input_file, step, display_name, "multi-genus-docs-sharded")
+
+
+def cobs_classic_docs(index_path: Path) -> int:
+    """Document count of a classic COBS index, from its header (magic, u32
+    version, u32 docs; the layout xs_bank_open reads)."""
+    with open(index_path, "rb") as fh:
+        head = fh.read(26)
+    if not head.startswith(b"COBS:CLASSIC_INDEX") or len(head) < 26:
+        raise ValueError(f"{index_path}: not a classic COBS index")
+    return int.from_bytes(head[22:26], "little")
+
+
+def doc_slice(num_docs: int, rank: int, world: int) -> tuple[int, int]:
+    """Docs [lo, hi) of rank `rank` when one bank is column-split over `world`
+    ranks (option b): the rows' byte columns are
+    dealt out evenly, so lo and hi are multiples of 8 (hi = num_docs last)."""
+    R = (num_docs + 7) // 8
+    if not 0 <= rank < world or world > R:
+        raise ValueError(f"a bank of {num_docs} docs ({R} row bytes) cannot be split over {world} ranks")
+    return R * rank // world * 8, min(num_docs, R * (rank + 1) // world * 8)
+
+
+def load_docs_slice(cls, json_path: Path, rank: int | None = None, world: int | None = None):
+    """This rank's slice of ONE species model: `cls.load(json_path)` with only
+    docs doc_slice(D, rank, world) of its bank on this rank's GPU (the model's
+    metadata, display names and SVM stay whole)."""
+    dist = _dist()
+    rank = dist.get_rank() if rank is None else rank
+    world = dist.get_world_size() if world is None else world
+    from .util import slugify
+    meta = json.loads(Path(json_path).read_text(encoding="utf-8"))  # the index lies where load() finds it
+    index = Path(json_path).parent / slugify(meta["model_display_name"] + "-" + str(meta["model_type"])) / \
+        "index.cobs_classic"
+    return cls.load(json_path, docs=doc_slice(cobs_classic_docs(index), rank, world))
+
+
+def predict_bank_sharded(model, input_file: Path, step: int = 1, display_name: bool = False):
+    """Config 5 with ONE bank column-split over the ranks (each rank's model
+    from load_docs_slice): every rank hashes every k-mer and reads its slice of
+    each row; the gathered MatrixResult is the whole model's prediction (labels
+    in doc order, the model's slug; an SVM model's label formed from the
+    gathered totals, probabilistic_filter_svm_model.py:175-223)."""
+    res = _predict_doc_columns(model, input_file, step, display_name, model.slug())
+    if hasattr(model, "_get_svm") and len(res.ids):
+        res.prediction = str(model._get_svm(None).predict([[v for _, v in sorted(res.get_total_scores().items())]])[0])
+    return res
+
+
+def _predict_doc_columns(model, input_file: Path, step: int, display_name: bool, slug: str):
     import torch
     from .bank import narrowest_count_dtype
     from .file_io import check_input_path, file_reader_device, read_batches
@@ -395,9 +445,10 @@ def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: b
             hl, nk = model._query(batch.packed, step)
             t = torch.from_numpy(np.ascontiguousarray(hl).astype(np.int32))
             h = gather_doc_shards(t, mx).numpy().view(np.uint32)  # every rank reads the same batches
-        ids += batch.ids()
+        ids.append(batch.ids_packed())
         hits.append(h)
         nks.append(nk)
+    ids = PackedIds.concat(ids) if ids else []
     D = len(labels)
     if hits:
         dt = max((h.dtype for h in hits), key=lambda t: t.itemsize)
@@ -405,6 +456,6 @@ def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: b
         nk = np.concatenate(nks)
     else:
         hm, nk = np.zeros((0, D), np.uint8), np.zeros(0, np.uint64)
-    res = MatrixResult("multi-genus-docs-sharded", ids, labels, hm, nk, sparse_sampling_step=step)
+    res = MatrixResult(slug, ids, labels, hm, nk, sparse_sampling_step=step)
     res.input_source = input_file.name
     return res

@@ -317,21 +317,23 @@ class ProbabilisticFilterModel:
         json_path.write_text(json.dumps(self.to_dict(), indent=4), encoding="utf-8")
 
     @staticmethod
-    def load(path: Path) -> "ProbabilisticFilterModel":
+    def load(path: Path, docs: tuple[int, int] | None = None) -> "ProbabilisticFilterModel":
+        """Reference :351-391.  docs=(lo, hi): only those docs of the bank resident
+        (one rank's slice of a docs-sharded bank, distributed.load_docs_slice)."""
         meta = json.loads(Path(path).read_text(encoding="utf-8"))
         model = ProbabilisticFilterModel(
             meta["k"], meta["model_display_name"], meta["author"], meta["author_email"],
             meta["model_type"], Path(path).parent, meta["fpr"], meta["num_hashes"],
             meta["training_accessions"])
         model.display_names = meta["display_names"]
-        model._open_index()
+        model._open_index(docs)
         return model
 
-    def _open_index(self) -> None:
+    def _open_index(self, docs: tuple[int, int] | None = None) -> None:
         index_path = Path(self.get_cobs_index_path())
         if not index_path.exists():
             raise FileNotFoundError(f"Index file not found at {index_path}")
-        self.index = Bank.open(index_path, XS_BANK_COBS_CLASSIC, device=self.device)
+        self.index = Bank.open(index_path, XS_BANK_COBS_CLASSIC, device=self.device, docs=docs)
 
     def close(self) -> None:
         if self.index is not None:

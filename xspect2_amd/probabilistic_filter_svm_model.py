@@ -13,8 +13,6 @@ import csv
 import json
 from pathlib import Path
 
-from ._lib import XS_BANK_COBS_CLASSIC
-from .bank import Bank
 from .file_io import FASTA_ENDINGS, FASTQ_ENDINGS
 from .probabilistic_filter_model import ProbabilisticFilterModel
 from .result import MatrixResult, ModelResult
@@ -121,7 +119,7 @@ class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
         return svm
 
     @staticmethod
-    def load(path: Path) -> "ProbabilisticFilterSVMModel":
+    def load(path: Path, docs: tuple[int, int] | None = None) -> "ProbabilisticFilterSVMModel":
         meta = json.loads(Path(path).read_text(encoding="utf-8"))
         model = ProbabilisticFilterSVMModel(
             meta["k"], meta["model_display_name"], meta["author"], meta["author_email"],
@@ -129,8 +127,5 @@ class ProbabilisticFilterSVMModel(ProbabilisticFilterModel):
             num_hashes=meta["num_hashes"], training_accessions=meta["training_accessions"],
             svm_accessions=meta["svm_accessions"])
         model.display_names = meta["display_names"]
-        index_path = Path(model.get_cobs_index_path())
-        if not index_path.exists():
-            raise FileNotFoundError(f"Index file not found at {index_path}")
-        model.index = Bank.open(index_path, XS_BANK_COBS_CLASSIC, device=model.device)
+        model._open_index(docs)
         return model
