@@ -84,7 +84,9 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
 @pytest.mark.parametrize("ck,ws_mb,lookup,pad", [("1024", None, None, None), ("2048", None, None, None),
                                                  ("4096", None, None, None), ("2048", "1", None, None),
                                                  ("1024", "2", None, None), ("2048", None, "1", None),
-                                                 ("2048", None, None, "1"), ("4096", "2", "1", "1")])
+                                                 ("2048", None, None, "1"), ("4096", "2", "1", "1"),
+                                                 ("2048", None, "5", None), ("1024", "2", "5", None),
+                                                 ("4096", None, "5", "1")])
 def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup,
                                                   pad):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
@@ -97,7 +99,7 @@ def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D
     monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    if lookup:  # the register-gather lookup instead of LDS-DMA
+    if lookup:  # 1: the register-gather lookup instead of LDS-DMA; 5: LDS entry -> block map
         monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
     if pad:  # runs not padded to 64-B row pieces
         monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)
@@ -305,10 +307,15 @@ def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
     gb2.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "3"])
+@pytest.mark.parametrize("mode", ["0", "3", "3s"])
 @pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
 def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode):
-    """mode 0: direct probe; mode 3: partitioned probe with small partitions."""
+    """mode 0: direct probe; mode 3: partitioned probe with small partitions
+    (lookup with the LDS entry -> block map); 3s: the same with the lookup's
+    shuffle binary search (XSPECT2_AMD_BL_LOOKUP=0)."""
+    if mode == "3s":
+        mode = "3"
+        monkeypatch.setenv("XSPECT2_AMD_BL_LOOKUP", "0")
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)

@@ -3,5 +3,5 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out/ldsl
-timeout -k 10 240 ./tools/ldslookup > gpurun_out/ldsl/out.txt 2>&1 || { cat gpurun_out/ldsl/out.txt; exit 5; }
+timeout -k 10 240 ./tools/ldslookup ${LDSL_ARGS:-} > gpurun_out/ldsl/out.txt 2>&1 || { cat gpurun_out/ldsl/out.txt; exit 5; }
 cat gpurun_out/ldsl/out.txt

@@ -207,6 +207,87 @@ __global__ void __launch_bounds__(256) lookup_l2(const uint4* __restrict__ bank,
     }
 }
 
+// A2: today's lookup with the entry -> block map built in LDS per window of W
+// entries (each lane writes its block's position base over its run's slots,
+// then every entry reads its base) instead of a 6-step shuffle binary search
+// per entry: ~2 LDS operations per 64 entries instead of 8 shuffles.
+template <int W>
+__global__ void __launch_bounds__(256) lookup_l2_own(const uint4* __restrict__ bank, uint32_t P, uint64_t nblk,
+                                                     const uint32_t* __restrict__ ent,
+                                                     const uint16_t* __restrict__ tbl, uint4* __restrict__ out,
+                                                     uint32_t* qctr, uint64_t stride) {
+    constexpr int U = 6;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    __shared__ uint4 s_rows[4][U][64];
+    __shared__ uint32_t s_base[4][W];
+    const uint32_t xcd = blockIdx.x & 7;
+    for (uint64_t p = xcd; p < P; p += 8) {
+        const uint4* prow = bank + (p << SHIFT);
+        const uint16_t* t0 = tbl + p * nblk;
+        const uint16_t* t1 = t0 + nblk;
+        for (;;) {
+            uint32_t grp = 0;
+            if (lane == 0) grp = atomicAdd(&qctr[p * kQ], 1u);
+            const uint64_t b0 = (uint64_t)__builtin_amdgcn_readfirstlane(grp) * 64;
+            if (b0 >= nblk) break;
+            const uint64_t b = b0 + lane;
+            uint32_t s = 0, len = 0;
+            if (b < nblk) {
+                s = t0[b];
+                len = (uint32_t)t1[b] - s;
+            }
+            uint32_t inc = len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+                if (lane >= d) inc += t;
+            }
+            const uint32_t pre = inc - len;
+            const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
+            // position of entry i of this group = base of its block + i (u32: the workspace
+            // holds < 2^32 entries)
+            const uint32_t base = (uint32_t)(b * stride + s - pre);
+            for (uint32_t w0 = 0; w0 < total; w0 += W) {
+                const uint32_t lo = max(pre, w0), hi = min(pre + len, w0 + W);
+                for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
+                __builtin_amdgcn_wave_barrier();
+                const uint32_t wend = min(total, w0 + W);
+                for (uint32_t i0 = w0; i0 < wend; i0 += 64 * U) {
+                    uint32_t pos[U], e[U];
+                    uint4 v[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = i0 + u * 64 + lane;
+                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        e[u] = i0 + u * 64 + lane < wend ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (i0 + u * 64 + lane < wend && e[u] != PAD_ENTRY) {
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            __builtin_amdgcn_global_load_lds(prow + (e[u] >> IDB), &s_rows[wid][u][0], 16, 0, 0);
+                        }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int u = 0; u < U; ++u) v[u] = s_rows[wid][u][lane];
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (e[u] == PAD_ENTRY) {
+                            v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                            e[u] = pos[u] & (CK - 1);
+                        }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (i0 + u * 64 + lane < wend) store_row(out, pos[u], v[u], e[u]);
+                }
+                __builtin_amdgcn_wave_barrier();  // the window's bases are read before the next overwrite
+            }
+        }
+    }
+}
+
 // B: fine partition f (8192 rows) in LDS; the workgroup's waves take groups of
 // 64 blocks from an LDS counter and copy f's rows for their sub-runs.
 template <int U, int WT>
@@ -378,12 +459,32 @@ int main(int argc, char** argv) {
     CHK(hipMemset(outB, 0, nblk * stride * 16));
     run("A: L2 partitions (today)", [&] { lookup_l2<<<2 * ncu, 256>>>(bank, P, nblk, ent, tbl, outA, qctr, stride); },
         qctr, (size_t)P * kQ * 4);
+    unsigned long long nb = 0;
+    auto compare = [&](const char* what) {
+        CHK(hipMemset(bad, 0, 8));
+        cmp_kernel<<<4096, 256>>>(outA, outB, nblk * stride, bad);
+        CHK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
+        printf("row slots differing between A and %s: %llu\n", what, nb);
+        if (nb) exit(2);
+        CHK(hipMemset(outB, 0, nblk * stride * 16));
+    };
+    run("A2: owner map W=1024", [&] { lookup_l2_own<1024><<<2 * ncu, 256>>>(bank, P, nblk, ent, tbl, outB, qctr, stride); },
+        qctr, (size_t)P * kQ * 4);
+    compare("A2");
+    run("A2: owner map W=2048", [&] { lookup_l2_own<2048><<<2 * ncu, 256>>>(bank, P, nblk, ent, tbl, outB, qctr, stride); },
+        qctr, (size_t)P * kQ * 4);
+    compare("A2 W=2048");
+    run("A: L2 partitions (today), again", [&] { lookup_l2<<<2 * ncu, 256>>>(bank, P, nblk, ent, tbl, outA, qctr, stride); },
+        qctr, (size_t)P * kQ * 4);
+    run("A2: owner map W=1024, again", [&] { lookup_l2_own<1024><<<2 * ncu, 256>>>(bank, P, nblk, ent, tbl, outB, qctr, stride); },
+        qctr, (size_t)P * kQ * 4);
+    compare("A2 again");
+    if (argc > 3) return 0;  // owner-map A/B only
     run("B: LDS fine partitions, 1024 thr U4",
         [&] { lookup_lds<4, 1024><<<ncu, 1024>>>(bank, sig, P, PF, nblk, ent, tbl, ftbl, outB, qx, stride); }, qx,
         8 * kQ * 4);
     CHK(hipMemset(bad, 0, 8));
     cmp_kernel<<<4096, 256>>>(outA, outB, nblk * stride, bad);
-    unsigned long long nb = 0;
     CHK(hipMemcpy(&nb, bad, 8, hipMemcpyDeviceToHost));
     printf("row slots differing between A and B: %llu\n", nb);
     CHK(hipMemset(outB, 0, nblk * stride * 16));

@@ -188,13 +188,20 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
 // sits on its own 128-B line (a line's atomics are serialised at the memory
 // side).  Every lane keeps kLookupUnroll entries in flight.
 
-template <int kLookupUnroll>
+// W > 0: each group's entry -> block map is built in LDS per window of W
+// entries, as in cobs_lookup_kernel (xs_probe_cobspart.hip), instead of a
+// shuffle binary search per entry.
+template <int kLookupUnroll, int W = 0>
 __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const uint64_t* __restrict__ kofs,
                                                            uint64_t n, uint32_t K, uint32_t shift, uint32_t P,
                                                            uint64_t tstride, const uint32_t* __restrict__ eoff,
                                                            const uint16_t* __restrict__ tbl,
                                                            uint8_t* __restrict__ emiss, uint32_t* qctr) {
     const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    __shared__ uint32_t s_base[W > 0 ? 4 : 1][W > 0 ? W : 1];  // entry -> position base (host: < 2^32 entries)
+    (void)wid;
+    (void)s_base;
     const uint64_t nblk = (kofs[n] + kTK - 1) / kTK;
     const uint64_t cap = (uint64_t)kTK * K;
     const uint32_t xcd = blockIdx.x & 7;
@@ -222,31 +229,45 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
             }
             const uint32_t pre = inc - len;
             const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-            for (uint32_t i0 = 0; i0 < total; i0 += 64 * kLookupUnroll) {
+            const uint32_t base = (uint32_t)(b * cap + s) - pre;  // entry i sits at base + i (mod 2^32)
+            for (uint32_t w0 = 0; w0 < total; w0 += (W > 0 ? W : total)) {
+            const uint32_t wend = W > 0 ? min(total, w0 + W) : total;
+            if constexpr (W > 0) {
+                const uint32_t lo = max(pre, w0), hi = min(pre + len, wend);
+                for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
+                __builtin_amdgcn_wave_barrier();
+            }
+            for (uint32_t i0 = w0; i0 < wend; i0 += 64 * kLookupUnroll) {
                 uint64_t pos[kLookupUnroll];
                 uint32_t off[kLookupUnroll], w[kLookupUnroll];
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u) {
                     const uint32_t i = i0 + u * 64 + lane;
-                    int j = 0;
+                    if constexpr (W > 0) {
+                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
+                    } else {
+                        int j = 0;
 #pragma unroll
-                    for (int st = 32; st; st >>= 1) {
-                        const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
-                        if (pv <= i) j += st;
+                        for (int st = 32; st; st >>= 1) {
+                            const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
+                            if (pv <= i) j += st;
+                        }
+                        const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
+                        const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
+                        pos[u] = (b0 + j) * cap + sj + (i - pj);
                     }
-                    const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
-                    const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
-                    pos[u] = (b0 + j) * cap + sj + (i - pj);
                 }
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
-                    off[u] = i0 + u * 64 + lane < total ? eoff[pos[u]] : 0u;
+                    off[u] = i0 + u * 64 + lane < wend ? eoff[pos[u]] : 0u;
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
-                    w[u] = i0 + u * 64 + lane < total ? pb[off[u] >> 5] : ~0u;
+                    w[u] = i0 + u * 64 + lane < wend ? pb[off[u] >> 5] : ~0u;
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
                     if (!((w[u] >> (off[u] & 31)) & 1u)) emiss[pos[u]] = 1;
+            }
+            if constexpr (W > 0) __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
             }
         }
         }
@@ -349,6 +370,11 @@ static int part_env() {
     return e ? atoi(e) : 1;
 }
 
+static int env_int_bl(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : dflt;
+}
+
 // Partition shift for a filter of `mbits` bits: 2^24-bit (2 MiB) partitions
 // (2 MiB: 8.92 ms per config-2 step; 1 MiB 9.31, 512 KiB 10.86, 4 MiB 10.00),
 // halved down to 2^20 bits while that leaves fewer than 64 partitions (8 per
@@ -441,8 +467,14 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
     pass_mark(rec, kPassBucket, s);
-    bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                plan.tstride, eoff, ws.tbl, emiss, qctr);
+    // XSPECT2_AMD_BL_LOOKUP: 1 (default) the LDS entry -> block map, 0 the shuffle binary search
+    // (round 2); u32 positions need < 2^32 entries
+    if (env_int_bl("XSPECT2_AMD_BL_LOOKUP", 1) == 1 && ne < (1ull << 32))
+        bloom_lookup_kernel<kUnroll, 1024><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                         plan.tstride, eoff, ws.tbl, emiss, qctr);
+    else
+        bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
+                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr);
     pass_mark(rec, kPassLookup, s);
     bloom_resolve_kernel<<<(unsigned)plan.tstride, 256, 0, s>>>(ws.kofs, rv.n, bv.K, eid, emiss, ws.miss);
     bloom_count_kernel<<<blocks, 256, 0, s>>>(rv, ws.kofs, ws.miss, bv.K, hits, partials, bv.rows_read);

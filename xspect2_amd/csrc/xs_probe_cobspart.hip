@@ -217,7 +217,12 @@ constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
 // registers.  Rows go back with non-temporal dword stores (7.8 vs 10.1 ms for
 // one plain dwordx4 in tools/partgather.hip; the other store and load cache
 // policies measured no better: profiles/r02_cobspart_ab.txt item 9).
-template <int kUnroll, bool EMB, int CK, int DMA>
+// W > 0: the entry -> block map of a group is built in LDS per window of W
+// entries (each lane writes its block's position base over its run's slots,
+// then every entry reads its base: ~2 LDS operations per 64 entries) instead
+// of a 6-step shuffle binary search per entry (8 shuffles per 64 entries);
+// 6.37 -> 6.01 ms on tools/ldslookup.hip's config-2 entries at W = 1024.
+template <int kUnroll, bool EMB, int CK, int DMA, int W = 0>
 __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
                                                           uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
@@ -229,7 +234,9 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     __shared__ uint4 s_rows[DMA > 0 ? 4 : 1][DMA > 0 ? kUnroll : 1][64];  // LDS-DMA landing slots
+    __shared__ uint32_t s_base[W > 0 ? 4 : 1][W > 0 ? W : 1];  // entry -> position base (host: range < 2^32 entries)
     (void)wid;
+    (void)s_base;
     // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
     // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
     const uint64_t last = min(b_end, (kofs[n] + CK - 1) / CK);
@@ -258,29 +265,43 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
             }
             const uint32_t pre = inc - len;
             const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-            for (uint32_t i0 = 0; i0 < total; i0 += 64 * kUnroll) {
+            // entry i of the group sits at its block's base + i (mod 2^32: the range's
+            // workspace holds < 2^32 entries when W > 0)
+            const uint32_t base = (uint32_t)(b * stride + s) - pre;
+            for (uint32_t w0 = 0; w0 < total; w0 += (W > 0 ? W : total)) {
+            const uint32_t wend = W > 0 ? min(total, w0 + W) : total;
+            if constexpr (W > 0) {
+                const uint32_t lo = max(pre, w0), hi = min(pre + len, wend);
+                for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
+                __builtin_amdgcn_wave_barrier();
+            }
+            for (uint32_t i0 = w0; i0 < wend; i0 += 64 * kUnroll) {
                 uint64_t pos[kUnroll];
                 uint32_t e[kUnroll];
                 uint4 v[kUnroll];
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u) {
                     const uint32_t i = i0 + u * 64 + lane;
-                    int j = 0;
+                    if constexpr (W > 0) {
+                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
+                    } else {
+                        int j = 0;
 #pragma unroll
-                    for (int st = 32; st; st >>= 1) {
-                        const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
-                        if (pv <= i) j += st;
+                        for (int st = 32; st; st >>= 1) {
+                            const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
+                            if (pv <= i) j += st;
+                        }
+                        const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
+                        const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
+                        pos[u] = (b0 + j) * stride + sj + (i - pj);
                     }
-                    const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
-                    const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
-                    pos[u] = (b0 + j) * stride + sj + (i - pj);
                 }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    e[u] = i0 + u * 64 + lane < total ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
+                    e[u] = i0 + u * 64 + lane < wend ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    if (i0 + u * 64 + lane < total && e[u] != kCobsPadEntry) {
+                    if (i0 + u * 64 + lane < wend && e[u] != kCobsPadEntry) {
                         if constexpr (DMA > 0) {  // the row lands in this wave's slot u
 #if defined(__HIP_DEVICE_COMPILE__)  // a device-only builtin: the host pass must not see it
                             // DMA 1: one row gather in flight per wave (each waits for the one before);
@@ -310,7 +331,7 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                     }
 #pragma unroll
                 for (int u = 0; u < kUnroll; ++u)
-                    if (i0 + u * 64 + lane < total) {
+                    if (i0 + u * 64 + lane < wend) {
                         if constexpr (EMB) v[u].w = (v[u].w & (0xFFFFFFFFu >> IDB)) | (e[u] << (32 - IDB));
                         uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
                         __builtin_nontemporal_store(v[u].x, o);
@@ -318,6 +339,8 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                         __builtin_nontemporal_store(v[u].z, o + 2);
                         __builtin_nontemporal_store(v[u].w, o + 3);
                     }
+            }
+            if constexpr (W > 0) __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
             }
         }
     }
@@ -573,7 +596,7 @@ static int cobs_lookup_grid(int per_cu_want) {
     return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
 }
 
-template <int U, int CK, int DMA>
+template <int U, int CK, int DMA, int W = 0>
 static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
                           const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
                           uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
@@ -581,11 +604,11 @@ static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t
     const uint64_t waves = (uint64_t)grid / 8 * 4;
     const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
     if (emb)
-        cobs_lookup_kernel<U, true, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                 ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
+        cobs_lookup_kernel<U, true, CK, DMA, W><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+                                                                    ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
     else
-        cobs_lookup_kernel<U, false, CK, DMA><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                  ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
+        cobs_lookup_kernel<U, false, CK, DMA, W><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
+                                                                     ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
 }
 
 // Ranges of plan.rblk bucket blocks, one after the other on stream s, each
@@ -604,11 +627,16 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
     pass_mark(rec, kPassPrep, s);
     const bool emb = pb.D <= emb_max_docs<CK>();
-    // lookup: 0 (default) LDS-DMA row gathers of 6 entries per lane, one gather in
-    // flight per wave at a time, 2 workgroups per CU; 1 register gathers, 8 in
-    // flight, 3 per CU (the first build); 2 LDS-DMA with all 6 in flight.
+    // lookup: 5 (default) LDS-DMA row gathers of 6 entries per lane, one gather in
+    // flight per wave at a time, 2 workgroups per CU, entry -> block map in LDS
+    // (lookup 6.33 -> 6.06-6.10 ms, step 11.49 -> 11.23-11.28 ms interleaved on
+    // one box, profiles/r03_lookup_ownermap.txt); 0 the same with the shuffle
+    // binary search (round 2's default); 1 register gathers, 8 in flight, 3 per
+    // CU (the first build); 2 LDS-DMA with all 6 in flight.
     // XSPECT2_AMD_CP_PERCU overrides the workgroups per CU.
-    const int var = env_int("XSPECT2_AMD_CP_LOOKUP", 0);
+    int var = env_int("XSPECT2_AMD_CP_LOOKUP", 5);
+    // 5: the LDS entry -> block map (u32 positions: ranges of < 2^32 entries)
+    if (var == 5 && plan.rblk * plan.stride >= (1ull << 32)) var = 0;
     const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", var == 1 ? 3 : 2));
     for (uint64_t b0 = 0; b0 < plan.nblk; b0 += plan.rblk) {
         const uint64_t b1 = std::min(plan.nblk, b0 + plan.rblk);
@@ -630,6 +658,7 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             case 2: lookup_launch<6, CK, 2>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             case 3: lookup_launch<6, CK, 3>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             case 4: lookup_launch<6, CK, 4>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 5: lookup_launch<6, CK, 1, 1024>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             default: lookup_launch<6, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         pass_mark(rec, kPassLookup, s);
