@@ -86,7 +86,7 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
                                                  ("1024", "2", None, None), ("2048", None, "1", None),
                                                  ("2048", None, None, "1"), ("4096", "2", "1", "1"),
                                                  ("2048", None, "5", None), ("1024", "2", "5", None),
-                                                 ("4096", None, "5", "1")])
+                                                 ("4096", None, "5", "1"), ("2048", None, "6", None)])
 def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup,
                                                   pad):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
@@ -99,7 +99,7 @@ def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D
     monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    if lookup:  # 1: the register-gather lookup instead of LDS-DMA; 5: LDS entry -> block map
+    if lookup:  # 1: the register-gather lookup instead of LDS-DMA; 5, 6: LDS entry -> block map
         monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
     if pad:  # runs not padded to 64-B row pieces
         monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)

@@ -467,9 +467,12 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
     pass_mark(rec, kPassBucket, s);
-    // XSPECT2_AMD_BL_LOOKUP: 1 (default) the LDS entry -> block map, 0 the shuffle binary search
-    // (round 2); u32 positions need < 2^32 entries
-    if (env_int_bl("XSPECT2_AMD_BL_LOOKUP", 1) == 1 && ne < (1ull << 32))
+    // XSPECT2_AMD_BL_LOOKUP: 1 (default) the LDS entry -> block map over 1024-entry windows,
+    // 0 the shuffle binary search (round 2); u32 positions need < 2^32 entries.  Lookup
+    // 5.27 -> 5.02-5.05 ms; 2048 / 512-entry windows 5.13 / 5.51, 24 / 12 entries per lane
+    // 5.09 / 5.21 (profiles/r03_lookup_ownermap.txt)
+    const int blv = ne < (1ull << 32) ? env_int_bl("XSPECT2_AMD_BL_LOOKUP", 1) : 0;
+    if (blv == 1)
         bloom_lookup_kernel<kUnroll, 1024><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
                                                                          plan.tstride, eoff, ws.tbl, emiss, qctr);
     else

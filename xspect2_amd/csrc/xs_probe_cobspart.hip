@@ -627,16 +627,18 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
     pass_mark(rec, kPassPrep, s);
     const bool emb = pb.D <= emb_max_docs<CK>();
-    // lookup: 5 (default) LDS-DMA row gathers of 6 entries per lane, one gather in
+    // lookup: 5 (default) LDS-DMA row gathers of 8 entries per lane, one gather in
     // flight per wave at a time, 2 workgroups per CU, entry -> block map in LDS
-    // (lookup 6.33 -> 6.06-6.10 ms, step 11.49 -> 11.23-11.28 ms interleaved on
-    // one box, profiles/r03_lookup_ownermap.txt); 0 the same with the shuffle
-    // binary search (round 2's default); 1 register gathers, 8 in flight, 3 per
-    // CU (the first build); 2 LDS-DMA with all 6 in flight.
+    // over windows of 2048 entries; 6 the same with 6 entries per lane and
+    // 1024-entry windows (the map alone: lookup 6.33 -> 6.06-6.10 ms; 8 per lane
+    // 5.87-5.91, 10 / 12 / 14 per lane 6.08 / 6.55 / 6.78 ms, interleaved,
+    // profiles/r03_lookup_ownermap.txt); 0 6 per lane with the shuffle binary
+    // search (round 2's default); 1 register gathers, 8 in flight, 3 per CU
+    // (the first build); 2 LDS-DMA with all 6 in flight.
     // XSPECT2_AMD_CP_PERCU overrides the workgroups per CU.
     int var = env_int("XSPECT2_AMD_CP_LOOKUP", 5);
-    // 5: the LDS entry -> block map (u32 positions: ranges of < 2^32 entries)
-    if (var == 5 && plan.rblk * plan.stride >= (1ull << 32)) var = 0;
+    // 5, 6: the LDS entry -> block map (u32 positions: ranges of < 2^32 entries)
+    if (var >= 5 && plan.rblk * plan.stride >= (1ull << 32)) var = 0;
     const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", var == 1 ? 3 : 2));
     for (uint64_t b0 = 0; b0 < plan.nblk; b0 += plan.rblk) {
         const uint64_t b1 = std::min(plan.nblk, b0 + plan.rblk);
@@ -658,7 +660,8 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             case 2: lookup_launch<6, CK, 2>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             case 3: lookup_launch<6, CK, 3>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             case 4: lookup_launch<6, CK, 4>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 5: lookup_launch<6, CK, 1, 1024>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 5: lookup_launch<8, CK, 1, 2048>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
+            case 6: lookup_launch<6, CK, 1, 1024>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
             default: lookup_launch<6, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
         }
         pass_mark(rec, kPassLookup, s);
