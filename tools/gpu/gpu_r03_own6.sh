@@ -1,0 +1,18 @@
+# Batched LDS reads of the lookups' entry map: parity, then species and genus lines (twice each).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+F=gpurun_out/r03own6; mkdir -p $F
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
+  tests/test_gpu_parity.py > $F/parity.log 2>&1 || { tail -40 $F/parity.log; exit 12; }
+tail -1 $F/parity.log
+run() {  # label, workload, env...
+  local lab=$1 wl=$2; shift 2
+  env "$@" timeout -k 10 300 python bench.py --workload $wl --steps 10 --warmup 3 --no-cpu-baseline --no-host-path --no-e2e > $F/ab_$lab.json 2> $F/ab_$lab.err || { tail -20 $F/ab_$lab.err; exit 13; }
+  python3 -c "import json;d=json.load(open('$F/ab_$lab.json'));r=d['roofline'];print('$lab', round(d['ms_per_step'],3), round(r['probe_ms_avg'],3), {k: round(v,3) for k,v in r.get('pass_ms_avg',{}).items()})"
+}
+for rep in 1 2; do
+  run s_$rep species
+  run s0_$rep species XSPECT2_AMD_CP_LOOKUP=0
+  run g_$rep genus
+done
