@@ -1,4 +1,4 @@
-"""Config 3 and config 5 end to end over gloo on CPU (world 2 and 3).
+"""Config 3 and config 5 end to end over gloo on CPU (world 2, 3 and 8).
 
 * Config 3: ``distributed.classify_species_sharded`` — every rank parses only
   its byte range of one FASTQ file, probes it, the D+1 totals are
@@ -116,7 +116,7 @@ def _worker(rank: int, world: int, port: int, tmp: str, n_reads: int, svm: bool)
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n_reads,svm", [(2, 600, False), (3, 600, True), (3, 2, True)])
+@pytest.mark.parametrize("world,n_reads,svm", [(2, 600, False), (3, 600, True), (3, 2, True), (8, 1000, True)])
 def test_classify_species_sharded_equals_single_process(tmp_path, world, n_reads, svm):
     import torch.multiprocessing as mp
     from xspect2_amd import distributed
@@ -182,7 +182,7 @@ def _genera(oracle, world):
     return banks, reads
 
 
-@pytest.mark.parametrize("world", [3])
+@pytest.mark.parametrize("world", [3, 8])
 def test_multigenus_docs_sharded_over_100_docs(tmp_path, world):
     import torch.multiprocessing as mp
     sys.path.insert(0, str(ROOT / "oracle"))
