@@ -33,7 +33,8 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 GENUS = "Acinetobacter"
-GENERA = ["Acinetobacter", "Pseudomonas", "Klebsiella", "Escherichia"]
+GENERA = ["Acinetobacter", "Pseudomonas", "Klebsiella", "Escherichia", "Salmonella", "Enterobacter",
+          "Staphylococcus", "Streptococcus"]
 
 
 def setup(root: Path, n_reads: int) -> None:
