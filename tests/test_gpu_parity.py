@@ -106,6 +106,39 @@ def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
 
 
+def _random_partitioned_configs(n=16, seed=20261017):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        D = int(rng.integers(1, 129))
+        k = int(rng.integers(5, 33))
+        h = int(rng.integers(1, 9))
+        sig = int(rng.integers(1_000, 200_001))
+        ck = str(int(rng.choice([1024, 2048, 4096])))
+        lookup = str(int(rng.choice([0, 5, 6])))
+        ws_mb = [None, "1", "2"][int(rng.integers(0, 3))]
+        pad = [None, "1"][int(rng.integers(0, 2))]
+        out.append((D, k, h, sig, ck, lookup, ws_mb, pad))
+    return out
+
+
+@pytest.mark.parametrize("D,k,h,sig,ck,lookup,ws_mb,pad", _random_partitioned_configs())
+def test_partitioned_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, lookup, ws_mb, pad):
+    """Seeded random configurations of the partitioned COBS probe (docs 1-128,
+    k 5-32, h 1-8, 1 k-200 k rows in partitions down to 1024 rows, every
+    bucket block size, the entry-map lookups (5, 6) and the binary-search one
+    (0), small workspaces that force block ranges, padded and unpadded runs):
+    same hits, k-mer counts and totals as the oracle at steps 1, 2 and 7."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
+    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
+    monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
+    if ws_mb:
+        monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
+    if pad:
+        monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)
+    _classic_case(xs, oracle_mod, D, k, h, [sig], want_path=1)
+
+
 @pytest.mark.parametrize("shift,D", [("10", 100), ("11", 100), ("10", 117), ("11", 128), ("12", 64)])
 def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, shift, D):
     """A 1 M-row bank cut into 1024-row partitions (977 of them: more than
