@@ -106,7 +106,7 @@ def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
 
 
-def _random_partitioned_configs(n=16, seed=20261017):
+def _random_partitioned_configs(n=48, seed=20261017):
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(n):
@@ -365,6 +365,39 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
         got_h, got_n = gb.query(reads, step=step)
         assert np.array_equal(got_n, want_n)
         assert np.array_equal(got_h[:, 0], want_h)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+    gb.close()
+
+
+def _random_bloom_configs(n=24, seed=1017):
+    rng = np.random.default_rng(seed)
+    return [(int(rng.integers(5, 33)), int(rng.integers(1_000, 2_000_001)), int(rng.integers(1, 9)),
+             str(int(rng.integers(0, 2))), int(rng.integers(0, 1_000_000))) for _ in range(n)]
+
+
+@pytest.mark.parametrize("k,nbytes,K,bl_lookup,seed", _random_bloom_configs())
+def test_bloom_partitioned_random_configs(xs, oracle_mod, monkeypatch, k, nbytes, K, bl_lookup, seed):
+    """Seeded random rbloom filters (k 5-32, 1 kB-2 MB, K 1-8 bit indices)
+    through the partitioned probe with small partitions, entry-map (1) and
+    binary-search (0) lookups; mixed-case / IUPAC reads: same hits, counts
+    and totals as the oracle at steps 1 and 3."""
+    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
+    monkeypatch.setenv("XSPECT2_AMD_BL_LOOKUP", bl_lookup)
+    rng = np.random.default_rng(seed)
+    genome = _reads(rng, 8, k, alphabet="ACGTacgtN", min_len=k, max_len=5000)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.build(genome)
+    assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
+    reads = _reads(rng, 400, k, alphabet="ACGTacgtNRY") + [g[:300] for g in genome] + [genome[0] * 2]
+    for step in (1, 3):
+        want_h, want_n = bf.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h[:, 0], want_h)
+        assert gb.probe_path() == 1
         tot, nk = gb.query_totals(reads, step=step)
         assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
     gb.close()
