@@ -481,8 +481,10 @@ struct Inputs {
 };
 
 // Unit decomposition (k-mer counts, units, unit -> read map) for n device-resident reads.
+// units = false (the partitioned COBS probe, which maps k-mers to reads itself and
+// zeroes the hit matrix): only the per-read k-mer counts, when the caller wants them.
 int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, uint32_t* hits_zero,
-                  uint64_t zero_cols, hipStream_t s, ReadView* rv) {
+                  uint64_t zero_cols, hipStream_t s, ReadView* rv, bool units = true) {
     if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->unit_ofs.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
@@ -490,12 +492,14 @@ int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, u
     if (int rc = b->unit_read.ensure(unit_bound * 4)) return rc;
     const size_t tb = scan_temp_bytes(in.n ? in.n : 1);
     if (int rc = b->scan_tmp.ensure(tb)) return rc;
-    HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(), s));
-    HIPCHK(launch_scan(b->scan_tmp.p, b->scan_tmp.cap, b->nseg.as<uint64_t>(),
-                       b->unit_ofs.as<uint64_t>(), in.n, s));
-    HIPCHK(launch_scatter_units(b->nseg.as<uint64_t>(), b->unit_ofs.as<uint64_t>(), in.n,
-                                b->unit_read.as<uint32_t>(), b->n_units.as<uint64_t>(), hits_zero,
-                                zero_cols, s));
+    if (units || d_nk) HIPCHK(launch_units(in.offs, in.n, b->k, step, d_nk, b->nseg.as<uint64_t>(), s));
+    if (units) {
+        HIPCHK(launch_scan(b->scan_tmp.p, b->scan_tmp.cap, b->nseg.as<uint64_t>(),
+                           b->unit_ofs.as<uint64_t>(), in.n, s));
+        HIPCHK(launch_scatter_units(b->nseg.as<uint64_t>(), b->unit_ofs.as<uint64_t>(), in.n,
+                                    b->unit_read.as<uint32_t>(), b->n_units.as<uint64_t>(), hits_zero,
+                                    zero_cols, s));
+    }
     rv->seq = in.seqs;
     rv->seq_bytes = in.seq_bytes;
     rv->offs = in.offs;
@@ -521,12 +525,22 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     if (in.n >= (1ull << 31)) return fail(XS_ERR_ARG, "at most 2^31-1 reads per call");
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     if (int rc = ws_enter(b, s)) return rc;
+    const bool bloom = b->kind == XS_BANK_RBLOOM;
+    // the COBS path is chosen first: the partitioned probe needs no unit map
+    CobsPartPlan cplan;
+    bool cobs_part = false;
+    if (!bloom) {
+        cobs_part = cobs_part_plan(b->cobs_view(), b->k, in.n, in.seq_bytes, step, &cplan) &&
+                    !(b->pk_nkc.ensure(cplan.nkc_bytes) || b->pk_kofs.ensure(cplan.nkc_bytes) ||
+                      b->pk_scan.ensure(cplan.scan_bytes) || b->pk_entries.ensure(cplan.entry_bytes) ||
+                      b->pk_tbl.ensure(cplan.tbl_bytes) || b->pk_aux.ensure(cplan.aux_bytes));
+        (void)hipGetLastError();  // a workspace that did not fit: the direct probe
+    }
     ReadView rv;
-    if (int rc = prepare_units(b, in, step, d_nk, d_hits, cols, s, &rv)) return rc;
+    if (int rc = prepare_units(b, in, step, d_nk, d_hits, cols, s, &rv, !cobs_part)) return rc;
     const int blocks = probe_grid(b);
     uint64_t* partials = nullptr;
     const uint64_t pcols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
-    const bool bloom = b->kind == XS_BANK_RBLOOM;
     if (d_totals || bloom) {  // rbloom always: its totals steer the next query's path
         if (int rc = b->partials.ensure((size_t)blocks * pcols * 8)) return rc;
         partials = b->partials.as<uint64_t>();
@@ -574,18 +588,13 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         HIPCHK(launch_probe_bloom(rv, b->bloom_view(), d_hits, partials, blocks, s));
     } else {
         const CobsView cv = b->cobs_view();
-        CobsPartPlan cplan;
-        if (cobs_part_plan(cv, b->k, in.n, in.seq_bytes, step, &cplan) &&
-            !(b->pk_nkc.ensure(cplan.nkc_bytes) || b->pk_kofs.ensure(cplan.nkc_bytes) ||
-              b->pk_scan.ensure(cplan.scan_bytes) || b->pk_entries.ensure(cplan.entry_bytes) ||
-              b->pk_tbl.ensure(cplan.tbl_bytes) || b->pk_aux.ensure(cplan.aux_bytes))) {
+        if (cobs_part) {
             path = XS_PATH_PARTITIONED;
             const PartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                             b->pk_entries.p, b->pk_tbl.as<uint16_t>(), b->pk_aux.as<uint32_t>()};
             PassRecorder rec{&b->pass_ev, &b->pass_tag, &b->pass_used};
             HIPCHK(launch_probe_cobs_part(rv, cv, cplan, ws, d_hits, partials, blocks, s, b->profiling ? &rec : nullptr));
         } else {
-            (void)hipGetLastError();  // a workspace that did not fit: the direct probe
             HIPCHK(launch_probe_cobs(rv, cv, d_hits, partials, blocks, s));
         }
     }
