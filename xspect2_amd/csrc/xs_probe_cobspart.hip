@@ -503,6 +503,30 @@ __global__ void __launch_bounds__(resolve_threads<CK>()) cobs_resolve_kernel(Rea
     }
 }
 
+// The hit rows cobs_resolve_kernel does not store whole are zeroed here, so the
+// n x D matrix needs no memset: rows of reads without k-mers, of reads whose
+// k-mers span two bucket blocks (added atomically by each), and of every read
+// of a block with more reads than its LDS counter rows (all added atomically).
+template <int CK>
+__global__ void part_zero_rows_kernel(const uint64_t* __restrict__ kofs, uint64_t n,
+                                      const uint32_t* __restrict__ blk_read, uint32_t D,
+                                      uint32_t* __restrict__ hits) {
+    const uint64_t Nk = kofs[n];
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
+         r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t a = kofs[r], e = kofs[r + 1];
+        bool zero = a == e;
+        if (!zero) {
+            const uint64_t b0 = a / CK, b1 = (e - 1) / CK;
+            const uint64_t lo = blk_read[b0];
+            const uint64_t hi = (b0 + 1) * CK < Nk ? blk_read[b0 + 1] : n - 1;
+            zero = b0 != b1 || hi - lo + 1 > cnt_reads<CK>();
+        }
+        if (zero)
+            for (uint32_t d = 0; d < D; ++d) hits[r * D + d] = 0;
+    }
+}
+
 }  // namespace
 
 // XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
@@ -625,6 +649,8 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
     uint16_t* tbm = ws.tbl + (uint64_t)(plan.P + 1) * plan.rblk;  // block-major copy
     uint32_t* qctr = ws.aux + (plan.nblk + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     part_map_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read);
+    if (hits)
+        part_zero_rows_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read, pb.D, hits);
     pass_mark(rec, kPassPrep, s);
     const bool emb = pb.D <= emb_max_docs<CK>();
     // lookup: 5 (default) LDS-DMA row gathers of 8 entries per lane, one gather in
@@ -689,7 +715,7 @@ hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const 
     pb.D = (uint32_t)bv.D;
     pb.nwords = (uint32_t)((bv.D + 31) / 32);
     hipError_t e;
-    if (hits && (e = hipMemsetAsync(hits, 0, rv.n * bv.D * sizeof(uint32_t), s)) != hipSuccess) return e;
+    // (the hit rows the resolve does not store are zeroed by part_zero_rows_kernel)
     if (partials && (e = hipMemsetAsync(partials, 0, (size_t)blocks * (bv.D + 1) * sizeof(uint64_t), s)) != hipSuccess)
         return e;
     part_counts_kernel<<<grid_for(rv.n + 1, 256, 4096), 256, 0, s>>>(rv.offs, rv.n, rv.k, rv.step, ws.nkc);
