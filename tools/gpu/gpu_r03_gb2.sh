@@ -1,0 +1,17 @@
+# COBS lookup groups of up to 128 blocks with the entry map (XSPECT2_AMD_CP_GB 64 / 96 / 128): parity, interleaved lines.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+F=gpurun_out/r03gb2; mkdir -p $F
+for g in 64 128 96; do
+XSPECT2_AMD_CP_GB=$g timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -k "partitioned or padding or entry_width or mixed_streams" >> $F/parity.log 2>&1 || { tail -30 $F/parity.log; exit 12; }
+done
+grep passed $F/parity.log
+run() {  # label, env...
+  local lab=$1; shift
+  env "$@" timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-path --no-e2e > $F/ab_$lab.json 2> $F/ab_$lab.err || { tail -20 $F/ab_$lab.err; exit 13; }
+  python3 -c "import json;d=json.load(open('$F/ab_$lab.json'));r=d['roofline'];print('$lab', round(d['ms_per_step'],3), round(r['probe_ms_avg'],3), {k: round(v,3) for k,v in r.get('pass_ms_avg',{}).items()})"
+}
+for rep in 1 2; do
+  for g in 64 96 128; do run gb${g}_$rep XSPECT2_AMD_CP_GB=$g; done
+done
