@@ -3,6 +3,14 @@
     python bench.py [--gpus N --steps K --warmup W] [--workload species|genus|mlst|multigenus]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
+With --gpus N > 1 and no WORLD_SIZE in the environment (no torchrun around
+it), bench.py starts the N ranks itself (launch_ranks: one child process per
+GPU, started before anything touches the GPU) and prints rank 0's line; under
+torchrun it is one of the ranks.  Either way the line carries the process
+group's backend and size (dist_backend, rccl_world), every rank's GPU (PCI
+address; two ranks on one device is an error outside the shared-GPU
+rehearsal) and every rank's timed region and probe time (per_rank).
+
 Default workload = BASELINE.json configs[1] / SURVEY.md §8(d) config 2: 1M
 synthetic 150 bp reads per GPU against a D=100 species COBS classic bank
 (k=21, h=7, fpr=0.01; 38.4M rows, 0.5 GB file / 0.61 GB in HBM, larger than
@@ -15,8 +23,9 @@ Other workloads (SURVEY.md §8(d) configs 4/5 and the genus path):
   genus       rbloom filter over all 100 genomes (k=21, fpr=0.01), D=1
   mlst        7 loci x 1430 alleles, COBS compact (k=31, h=1, fpr=0.001,
               64-byte pages = 512 alleles per doc group); one step probes all loci
-  multigenus  each rank holds a different 100-species bank, reads replicated,
-              per-read hit vectors all-gathered over RCCL (docs sharded)
+  multigenus  each rank holds a different 100-species bank, reads replicated;
+              rank q ends with every bank's hit columns for its 1/N of the
+              reads (one RCCL all-to-all; docs sharded, output by reads)
 
 metric = k-mer x filter probes/s = sum(ceil((L-k+1)/step)) x docs / second,
 whole job.  roofline prices the probe alone (HIP events on its launch
@@ -97,7 +106,81 @@ def parse():
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r03_traffic.json"))
+    ap.add_argument("--launch-timeout", type=float, default=1800.0,
+                    help="self-launched N>1 runs: seconds before the parent kills every rank")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    """A TCP port on 127.0.0.1 that nothing listens on right now."""
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, cmd: list[str], timeout: float, env: dict | None = None, poll_s: float = 0.2) -> int:
+    """One child process per rank (the reference's only fan-out is one process
+    per input, scripts/benchmark/classify/main.nf:1-22; here one per GPU).
+
+    Each child gets RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1 and a free MASTER_PORT, as torchrun would set them.
+    The parent touches no GPU and never execs: it starts the children, copies
+    rank 0's stdout to its own (the one JSON line), lets every rank's stderr
+    through, and waits.  If a child fails, or the whole run outlives
+    `timeout`, the remaining children are killed and the parent returns
+    non-zero (the first failing child's code, 124 on timeout)."""
+    import subprocess
+    import threading
+
+    base = dict(os.environ if env is None else env)
+    base.update(WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
+                MASTER_PORT=str(free_port()))
+    procs = []
+    try:
+        for r in range(n):
+            e = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+            procs.append(subprocess.Popen(cmd, env=e, stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    except BaseException:
+        for p in procs:
+            p.kill()
+        raise
+
+    def forward(stream):
+        for line in iter(stream.readline, b""):
+            sys.stdout.buffer.write(line)
+            sys.stdout.flush()
+
+    fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
+    fwd.start()
+    deadline = time.monotonic() + timeout
+    code = 0
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            r, code = bad[0]
+            print(f"bench launcher: rank {r} exited with {code}; stopping the other ranks", file=sys.stderr, flush=True)
+            break
+        if all(c == 0 for c in codes):
+            break
+        if time.monotonic() > deadline:
+            print(f"bench launcher: ranks still running after {timeout:.0f}s; stopping them", file=sys.stderr,
+                  flush=True)
+            code = 124
+            break
+        time.sleep(poll_s)
+    for p in procs:
+        if p.poll() is None:
+            p.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            p.wait()
+    fwd.join(timeout=10)
+    return code if code >= 0 else 128 - code  # a signal -s becomes 128 + s, as a shell reports it
 
 
 def log(rank, *a):
@@ -184,9 +267,12 @@ class Workload:
             # for 150 bp reads), narrowed and widened on the device; the layout
             # (docs per rank, wire type) is agreed once, as a serving loop would
             from xspect2_amd.distributed import doc_shard_layout
+            from xspect2_amd.distributed import shard_range
             self.layout = doc_shard_layout(self.docs[0], self.nk_read)
-            self.config["gather_dtype"] = str(self.layout[1]).replace("torch.", "")
-            self.config["gathered_docs"] = sum(self.layout[0])
+            self.counts = [b - a for a, b in (shard_range(self.n, q, world) for q in range(world))]
+            self.config["exchange_dtype"] = str(self.layout[1]).replace("torch.", "")
+            self.config["exchanged_docs"] = sum(self.layout[0])
+            self.config["reads_out_per_rank"] = self.counts
 
     def _mlst(self, args, dev, s):
         import torch
@@ -253,8 +339,10 @@ class Workload:
         if self.world > 1:
             from xspect2_amd import distributed
             if self.args.workload == "multigenus":
-                # docs sharded: hit vectors of every rank's bank over xGMI -> [n, sum D_r]
-                self.gathered = distributed.gather_doc_shards(self.d_hits[0], layout=self.layout)
+                # docs sharded, output sharded by reads: every rank's hit columns of
+                # rank q's 1/N of the reads go to rank q over xGMI (one all-to-all in
+                # the narrowest exact type) -> [n/N, sum D_r] per rank
+                self.exchanged = distributed.exchange_doc_columns(self.d_hits[0], self.counts, *self.layout)
             else:
                 for t in self.d_tot:
                     distributed.allreduce_(t)  # per-doc totals + k-mer total over all ranks
@@ -283,8 +371,28 @@ class Workload:
         return sum(per_bank) / len(per_bank)
 
 
+def check_distinct_devices(dev) -> list[str]:
+    """PCI address of every rank's GPU (all-gathered); raises if two ranks
+    drive the same device, which would make an N-GPU line an N-rank-on-one-GPU
+    line.  Skipped (addresses still returned) in the shared-GPU rehearsal."""
+    import torch
+    import torch.distributed as dist
+    p = torch.cuda.get_device_properties(dev)
+    mine = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    addrs: list = [None] * dist.get_world_size()
+    dist.all_gather_object(addrs, mine)
+    if not SHARE_GPU and len(set(addrs)) != len(addrs):
+        raise RuntimeError(f"ranks share a GPU (PCI addresses by rank: {addrs}); one rank per GPU is required")
+    return addrs
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start one process per GPU ourselves, before
+        # anything here touches the GPU (torch.cuda is not imported yet)
+        sys.exit(launch_ranks(args.gpus, [sys.executable, str(Path(__file__).resolve()), *sys.argv[1:]],
+                              args.launch_timeout))
     import torch
     import torch.distributed as dist
 
@@ -297,11 +405,16 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    dist_info = {"dist_backend": None, "rccl_world": None, "rank_devices": None}
     if world > 1:
         if SHARE_GPU:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+        dist_info = {"dist_backend": dist.get_backend(), "rccl_world": dist.get_world_size(),
+                     "rank_devices": check_distinct_devices(dev)}
+        if dist_info["rccl_world"] != world:
+            raise RuntimeError(f"process group has {dist_info['rccl_world']} ranks, WORLD_SIZE={world}")
     stream = torch.cuda.current_stream(dev)
     t_setup = time.time()
     wl = Workload(args, rank, world, dev, stream)
@@ -340,11 +453,16 @@ def main():
         probe_ms_total += tot_ms
         probe_ms_max = max(probe_ms_max, mx)
     probe_ms = probe_ms_total / max(1, launches)
+    per_rank = None
     if world > 1:
-        from xspect2_amd.distributed import allreduce_
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        allreduce_(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # every rank's own timed region and probe time; the line's time is the max
+        mine = torch.tensor([elapsed, probe_ms], dtype=torch.float64, device=dev if not SHARE_GPU else "cpu")
+        parts = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        el = [float(p[0].item()) for p in parts]
+        pm = [float(p[1].item()) for p in parts]
+        elapsed = max(el)
+        per_rank = {"elapsed_s": el, "probe_ms_avg": pm, "probe_ms_min": min(pm), "probe_ms_max": max(pm)}
 
     # sanity of the last step: whole-job k-mer totals
     for t in wl.d_tot:
@@ -407,22 +525,26 @@ def main():
             traffic = None
     pass_ms = {name: ms / max(1, launches) for name, (ms, cnt) in passes.items() if cnt}
     lookup_l2 = None
-    if wl.partitioned == "cobs" and "lookup" in pass_ms:
+    if wl.partitioned and "lookup" in pass_ms:
         # the dominant pass against its own ceiling: L2 requests per launch (PMC,
         # scaled to this call's k-mers) over the lookup's live HIP-event time
+        pmc_file, prefix = (("r03_pmc_cobspart.json", "xs::cobs_lookup_kernel") if wl.partitioned == "cobs" else
+                            ("r04_pmc_bloompart.json", "xs::bloom_lookup_kernel"))
         try:
-            pmc = json.loads((ROOT / "profiles" / "r03_pmc_cobspart.json").read_text())["kernels"]
-            key = next(k for k in pmc if k.startswith("xs::cobs_lookup_kernel"))
+            pmc = json.loads((ROOT / "profiles" / pmc_file).read_text())["kernels"]
+            key = next(k for k in pmc if k.startswith(prefix))
             req = pmc[key]["TCC_REQ_sum"] * wl.kmers / (1_000_000 * 130)
             ach = req / (pass_ms["lookup"] * 1e-3)
             lookup_l2 = {"kernel": key, "bound": "l2_requests", "achieved": ach, "peak": L2_GATHER_PEAK_REQ,
                          "unit": "req/s", "frac": ach / L2_GATHER_PEAK_REQ, "requests_per_launch": req,
                          "lookup_ms_avg": pass_ms["lookup"],
-                         "source": "TCC_REQ_sum per dispatch from profiles/r03_pmc_cobspart.json (1 M reads; "
+                         "l2_hit_rate": pmc[key].get("l2_hit_rate"),
+                         "source": f"TCC_REQ_sum per dispatch from profiles/{pmc_file} (1 M reads; "
                                    "scaled by k-mers); peak = pure L2 gathers, profiles/r02_l2gather.txt"}
         except Exception:
             lookup_l2 = None
-    host = None if args.no_host_path else host_path(wl, args)
+    # the PCIe-inclusive legs are a per-GPU figure: measured at N=1 only
+    host = None if args.no_host_path or world > 1 else host_path(wl, args)
     e2e = None
     if rank == 0 and world == 1 and not args.no_e2e and args.workload in ("species", "genus"):
         e2e = end_to_end(wl, args)
@@ -439,16 +561,19 @@ def main():
     names = {"species": f"{species_cfg}: {nr}/GPU vs D={args.docs} COBS classic species bank",
              "genus": f"genus path: {nr}/GPU vs rbloom filter over {args.docs} genomes",
              "mlst": f"config4: {nr}/GPU vs 7 loci x 1430 alleles (COBS compact)",
-             "multigenus": f"config5: {nr} vs one {args.docs}-species bank per GPU, hits all-gathered"}
+             "multigenus": f"config5: {nr} vs one {args.docs}-species bank per GPU, hit columns exchanged to the reads' ranks"}
     par = {"species": f"reads sharded x{world}, bank replicated, RCCL all-reduce of D+1 totals",
            "genus": f"reads sharded x{world}, filter replicated, RCCL all-reduce of totals",
            "mlst": f"reads sharded x{world}, loci banks replicated, RCCL all-reduce of totals",
-           "multigenus": f"docs sharded x{world} (one bank per GPU), reads replicated, RCCL all-gather of hit rows in the narrowest exact integer type"}
+           "multigenus": f"docs sharded x{world} (one bank per GPU), reads replicated, output sharded by reads: RCCL "
+                         "all-to-all of hit columns in the narrowest exact integer type"}
     line = {
         "metric": METRIC,
         "value": value,
         "unit": "probes/s",
         "n_gpus": world,
+        **dist_info,
+        "per_rank": per_rank,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
@@ -468,6 +593,10 @@ def main():
             "bound": "mall" if args.workload == "mlst" else "hbm", "achieved": achieved, "peak": peak,
             "unit": "GB/s", "frac": achieved / peak, "traffic": traffic,
             "traffic_frac": (traffic / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            "frac_basis": ("frac = SURVEY.md §8(d)-priced algorithmic bytes / probe time / peak; traffic_frac = "
+                           "PMC-measured HBM bytes of the same probe (traffic) / probe time / 8 TB/s: the bytes "
+                           "the pipeline really moves, intermediates included" if traffic else
+                           "frac = algorithmic bytes / probe time / peak"),
             "kernel": wl.kernel,
             "probe_ms_avg": probe_ms, "probe_ms_max": probe_ms_max, "probe_launches": launches,
             "pass_ms_avg": pass_ms or None, "lookup_l2": lookup_l2,

@@ -157,6 +157,10 @@ int xs_query_hits_device(xs_bank* bank, const void* d_seqs, uint64_t seq_bytes, 
  * sequences, for checks). */
 int xs_memcpy_to_host(void* host, const void* dev, uint64_t bytes);
 
+/* Device -> device copy of `bytes`, asynchronous on `stream` (e.g. a device
+ * reader batch's sequences into a caller's buffer for a collective). */
+int xs_memcpy_device(void* dst, const void* src, uint64_t bytes, void* stream);
+
 /* Pinned (page-locked) host memory for outputs the caller reuses across calls:
  * results land there by DMA, with no page faults on a fresh pageable buffer. */
 int xs_host_alloc(uint64_t bytes, void** out);
@@ -286,6 +290,12 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
 int xs_ids_json_quote(const char* buf, const uint64_t* offs, uint64_t n, char* out, uint64_t out_cap,
                       uint64_t* out_offs);
 int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int* has_dup);
+/* out[2i], out[2i+1] = XXH64 of id i with seeds 0 and 0x27D4EB2F165667C5: the
+ * 128-bit key by which the ranks of a read-sharded job find ids repeated
+ * across their shards (the reference keeps the last record of a repeated id,
+ * probabilistic_filter_model.py:310, and sums totals over that dict,
+ * result.py:76-90).  Any bytes (not only ASCII). */
+int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* out);
 
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
  * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path

@@ -14,7 +14,7 @@ HEADER = ROOT / "include" / "xspect_hip.h"
 def declared_functions() -> list[str]:
     text = HEADER.read_text()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(xs_[a-z_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(xs_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_parses_and_lists_entry_points():
@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
     lib = _lib.load()
     out = subprocess.run(["nm", "-D", "--defined-only", str(_lib.SO_PATH)], capture_output=True,
                          text=True, check=True).stdout
-    exported = set(re.findall(r"\bT (xs_[a-z_]+)\b", out))
+    exported = set(re.findall(r"\bT (xs_[a-z0-9_]+)\b", out))
     for name in declared_functions():
         assert name in exported, f"{name} not exported"
         assert hasattr(lib, name)

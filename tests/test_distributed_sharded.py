@@ -55,7 +55,7 @@ class OracleIndex:
         return h.astype(hit_dtype), nk
 
 
-def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True):
+def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int = 0, short_at: int = -1):
     """A species model over 6 synthetic genomes (oracle bank), its reads as a
     FASTQ file (written by the parent before the ranks start: a rank must not
     rewrite a file another rank is reading)."""
@@ -89,9 +89,9 @@ def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True):
     reads = []
     for i in range(n_reads):
         g = genomes[i % 6] if i % 7 else acgt[rng.integers(0, 4, 3000)].tobytes()
-        L = int(rng.integers(K + 1, 200))
+        L = int(rng.integers(K + 1, 200)) if i != short_at else K  # len <= k: the reference raises
         s = int(rng.integers(0, len(g) - L))
-        reads.append((f"read_{i}", g[s:s + L].decode()))
+        reads.append((f"read_{i % id_mod if id_mod else i}", g[s:s + L].decode()))
     fq = tmp / "reads.fq"
     if write:
         fq.write_text("".join(f"@{rid} x\n{s}\n+\n{'I' * len(s)}\n" for rid, s in reads))
@@ -139,6 +139,68 @@ def test_classify_species_sharded_equals_single_process(tmp_path, world, n_reads
         assert sum(per_shard) == n_reads
         if n_reads >= 600:
             assert min(per_shard) > n_reads / world / 2  # byte ranges balance the reads
+
+
+def _dup_worker(rank: int, world: int, port: int, tmp: str, n_reads: int, id_mod: int, short_at: int):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model, fq = _setup(Path(tmp), n_reads, True, write=False, id_mod=id_mod, short_at=short_at)
+        try:
+            distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / "dup.json")
+            (Path(tmp) / f"rank{rank}.txt").write_text("ok")
+        except Exception as e:  # noqa: BLE001
+            (Path(tmp) / f"rank{rank}.txt").write_text(f"{type(e).__name__}: {e}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,id_mod", [(3, 350), (2, 7), (3, 1)])
+def test_repeated_ids_across_shards_follow_the_reference_dict(tmp_path, world, id_mod):
+    """Read ids that repeat in different shards (ids read_{i % id_mod}: 600
+    reads, so each id occurs in 2 to 600 records spread over the ranks): the
+    merged shards equal the single-process JSON, whose dictionaries keep one
+    entry per id at its first record with its last record's values
+    (probabilistic_filter_model.py:310) and sum the totals over them
+    (result.py:76-90); the SVM label follows those totals."""
+    import torch.multiprocessing as mp
+    from xspect2_amd import distributed
+
+    n_reads = 600
+    model, fq = _setup(tmp_path, n_reads, True, id_mod=id_mod)
+    mp.spawn(_dup_worker, args=(world, _free_port(), str(tmp_path), n_reads, id_mod, -1), nprocs=world, join=True)
+    assert all((tmp_path / f"rank{r}.txt").read_text() == "ok" for r in range(world))
+    res = model.predict_columnar(fq)
+    res.input_source = fq.name
+    res.save(tmp_path / "single.json")
+    want = json.loads((tmp_path / "single.json").read_text())
+    shards = [distributed.shard_path(tmp_path / "out" / "dup.json", r, world) for r in range(world)]
+    got = distributed.merge_result_shards(shards)
+    assert len(want["hits"]) == min(id_mod, n_reads)
+    assert got == want
+    assert list(got["hits"]) == list(want["hits"])
+    assert got["prediction"] == want["prediction"]
+    assert sum(len(json.loads(p.read_text())["hits"]) for p in shards) == len(want["hits"])
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world", [2, 3])
+def test_an_error_on_one_rank_raises_on_every_rank(tmp_path, world):
+    """Only the last shard holds a read no longer than k: every rank raises the
+    reference's ValueError instead of the others waiting in the totals'
+    all-reduce."""
+    import torch.multiprocessing as mp
+
+    n_reads = 300
+    _setup(tmp_path, n_reads, True, short_at=n_reads - 2)
+    mp.spawn(_dup_worker, args=(world, _free_port(), str(tmp_path), n_reads, 0, n_reads - 2), nprocs=world,
+             join=True)
+    for r in range(world):
+        assert (tmp_path / f"rank{r}.txt").read_text() == "ValueError: Invalid sequence, must be longer than k"
 
 
 def _gather_worker(rank: int, world: int, port: int, tmp: str):
@@ -200,7 +262,7 @@ def test_multigenus_docs_sharded_over_100_docs(tmp_path, world):
         assert np.array_equal(o["step2"], want2)
 
 
-def _docs_worker(rank: int, world: int, port: int, tmp: str):
+def _docs_worker(rank: int, world: int, port: int, tmp: str, dup: bool = False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -215,34 +277,53 @@ def _docs_worker(rank: int, world: int, port: int, tmp: str):
         m = ProbabilisticFilterModel(K, f"Genus{rank}", None, None, "Species", Path(tmp) / "m")
         names = [f"g{rank}_sp{d}" for d in range(banks[rank].D)]
         m.index = OracleIndex(banks[rank], names)
-        res = distributed.predict_docs_sharded(m, Path(tmp) / "reads.fasta")
-        if rank == 0:
-            res.save(Path(tmp) / "docs_sharded.json")
+        distributed.classify_docs_sharded(m, Path(tmp) / "reads.fasta", Path(tmp) / "out" / "docs.json")
     finally:
         dist.destroy_process_group()
 
 
-def test_predict_docs_sharded_multigenus(tmp_path):
-    """Config 5 as a library call: three genus models of 40-50 species (> 100
-    docs) on three ranks, one FASTA of reads from all of them; the gathered
-    result (labels in rank order) equals one process probing the three banks
-    and concatenating the columns."""
+def _write_reads(path: Path, reads, dup: bool):
+    """FASTA of the reads; with dup, ids repeat far apart (reads i and
+    i + n/2 share an id, so the repeats fall into different shards)."""
+    half = (len(reads) + 1) // 2
+    with open(path, "wb") as fh:
+        for i, r in enumerate(reads):
+            fh.write(b">r%d\n%s\n" % (i % half if dup else i, r))
+
+
+@pytest.mark.parametrize("world,dup", [(2, False), (3, False), (3, True), (8, False)])
+def test_predict_docs_sharded_multigenus(tmp_path, world, dup):
+    """Config 5 as a library call: `world` genus models of 40-75 species
+    (> 100 docs) on `world` ranks, one FASTA of reads from all of them.  Each
+    rank parses its byte range, the reads are all-gathered, every rank probes
+    them against its bank and the hit columns go back by all-to-all to the
+    rank that owns the reads; every rank writes its own shard.  The merged
+    shards equal the JSON of one process probing every bank and concatenating
+    the columns, repeated ids (dup) included."""
     import torch.multiprocessing as mp
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle
+    from xspect2_amd import distributed
     from xspect2_amd.result import MatrixResult
 
-    world = 3
     banks, reads = _genera(oracle, world)
-    with open(tmp_path / "reads.fasta", "wb") as fh:
-        for i, r in enumerate(reads):
-            fh.write(b">r%d\n%s\n" % (i, r))
-    mp.spawn(_docs_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    _write_reads(tmp_path / "reads.fasta", reads, dup)
+    mp.spawn(_docs_worker, args=(world, _free_port(), str(tmp_path), dup), nprocs=world, join=True)
     hits = np.concatenate([b.query(reads)[0] for b in banks], axis=1)
     nk = banks[0].query(reads)[1]
     labels = [f"g{g}_sp{d}" for g in range(world) for d in range(banks[g].D)]
-    want = MatrixResult("multi-genus-docs-sharded", [f"r{i}" for i in range(len(reads))], labels, hits, nk)
+    half = (len(reads) + 1) // 2
+    ids = [f"r{i % half if dup else i}" for i in range(len(reads))]
+    want = MatrixResult("multi-genus-docs-sharded", ids, labels, hits, nk)
     want.input_source = "reads.fasta"
     want.save(tmp_path / "want.json")
-    assert len(labels) > 100
-    assert (tmp_path / "docs_sharded.json").read_bytes() == (tmp_path / "want.json").read_bytes()
+    assert len(labels) > 100 or world < 3
+    shards = [distributed.shard_path(tmp_path / "out" / "docs.json", r, world) for r in range(world)]
+    per_shard = [json.loads(p.read_text()) for p in shards]
+    got = distributed.merge_result_shards(shards)
+    w = json.loads((tmp_path / "want.json").read_text())
+    assert got == w
+    assert list(got["hits"]) == list(w["hits"])
+    assert sum(len(d["hits"]) for d in per_shard) == len(w["hits"])  # each read in exactly one shard
+    if not dup:
+        assert min(len(d["hits"]) for d in per_shard) > 0

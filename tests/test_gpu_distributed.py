@@ -6,7 +6,10 @@ by tools/gpu/gpu_r03_sharded.sh.)
 
 * config 5: ``docs_sharded_hits_device`` — probe on the device, narrow, RCCL
   all-gather, widen — equals the bank's hit matrix, for 1-byte and 2-byte
-  transport;
+  transport; ``exchange_doc_columns`` (the all-to-all that sends every
+  rank's hit columns to the reads' rank) keeps values in 1, 2 and 4 bytes;
+  ``predict_docs_sharded`` (reads all-gathered from the device reader,
+  probed, exchanged) equals the model's own prediction;
 * config 3: ``classify_species_sharded`` — the byte-range reader, the RCCL
   all-reduce of D+1 totals on a device tensor, the SVM label — writes the
   JSON the single-process ``classify_species`` writes.
@@ -122,3 +125,19 @@ def test_predict_docs_sharded_world1_on_device(pg, tmp_path, oracle_mod):
     assert np.array_equal(res.hits.astype(np.uint32), want.hits.astype(np.uint32))
     assert np.array_equal(res.num_kmers, want.num_kmers)
     gb.close()
+
+
+@pytest.mark.parametrize("wire", ["uint8", "int16", "int32"])
+def test_exchange_doc_columns_on_device(pg, wire):
+    """Config 5's output exchange (RCCL all-to-all, world 1): the rank's hit
+    columns come back narrowed to the wire type, values intact (int16 rides
+    as float16 bit patterns)."""
+    import torch
+    from xspect2_amd import distributed
+    dt = getattr(torch, wire)
+    top = {"uint8": 255, "int16": 32767, "int32": 1 << 30}[wire]
+    g = torch.Generator(device="cuda").manual_seed(5)
+    hits = torch.randint(0, top + 1, (3001, 37), generator=g, device="cuda", dtype=torch.int64).to(torch.int32)
+    out = distributed.exchange_doc_columns(hits, [3001], [37], dt)
+    assert out.dtype == dt and out.device == hits.device and tuple(out.shape) == (3001, 37)
+    assert torch.equal(out.to(torch.int64), hits.to(torch.int64))

@@ -166,3 +166,18 @@ def test_sharded_results_stitch_to_the_whole(tmp_path, cut):
         json.loads((tmp_path / f"s{p}.json").read_text())  # every shard is valid JSON
         paths.append(tmp_path / f"s{p}.json")
     assert merge_result_shards(paths) == json.loads((tmp_path / "whole.json").read_text())
+
+
+def test_empty_shard_on_the_dict_path_saves_the_job_total(tmp_path):
+    """A shard that takes the dictionary path (equal labels) and holds no
+    reads writes empty per-read sections and the job's "total" (ADVICE r3:
+    it used to raise IndexError from the local get_total_hits)."""
+    import json
+    labels = ["a", "a", "b"]
+    sh = MatrixResult("m", [], labels, np.zeros((0, 3), np.uint8), np.zeros(0, np.uint64), 1, "470", "in.fq")
+    sh.set_job_totals(np.array([10, 20, 30], np.uint64), 100, np.array([1, 2, 3], np.uint32))
+    sh.save(tmp_path / "s.json")
+    d = json.loads((tmp_path / "s.json").read_text())
+    assert d["hits"] == {} and d["num_kmers"] == {}
+    assert d["scores"] == {"total": sh.get_total_scores()}
+    assert d["prediction"] == "470" and d["input_source"] == "in.fq"

@@ -78,3 +78,27 @@ def test_matrix_result_with_packed_ids_writes_the_same_json(tmp_path, dup):
     assert b.get_filter_mask("L3", 0.5) == a.get_filter_mask("L3", 0.5)
     with pytest.raises(ValueError, match="reserved"):
         MatrixResult("slug", PackedIds.of(["a", "total"]), ["x"], np.zeros((2, 1), np.uint8), np.ones(2))
+
+
+def test_hash128_is_xxh64_with_two_seeds():
+    """xs_ids_hash128 = python-xxhash's XXH64 of each id's bytes, seeds 0 and
+    0x27D4EB2F165667C5 (lengths 0..80 cover every tail path, non-ASCII too)."""
+    import xxhash
+    from xspect2_amd.packing import PackedIds
+    rng = np.random.default_rng(3)
+    ids = [bytes(rng.integers(0, 256, n, dtype=np.uint8)).decode("latin-1") for n in range(81)] + ["read_1", "é"]
+    p = PackedIds.of(ids)
+    h = p.hash128()
+    for i, s in enumerate(ids):
+        b = s.encode("utf-8")
+        assert int(h[i, 0]) == xxhash.xxh64_intdigest(b, 0)
+        assert int(h[i, 1]) == xxhash.xxh64_intdigest(b, 0x27D4EB2F165667C5)
+
+
+def test_take_keeps_the_selected_ids_packed():
+    from xspect2_amd.packing import PackedIds
+    ids = ["a", "", "read_22", "x" * 40, "é", "b"]
+    p = PackedIds.of(ids)
+    for idx in ([], [0], [5, 0, 2], [1, 1, 3], list(range(6))):
+        t = p.take(np.array(idx, dtype=np.int64))
+        assert isinstance(t, PackedIds) and t.tolist() == [ids[i] for i in idx]

@@ -5,16 +5,18 @@
     torchrun --nproc-per-node N tools/sharded_classify.py shard --root DIR
     python tools/sharded_classify.py check  --root DIR --world N     # merged shards == single.json
 
-Config 5 (docs sharded; one genus model per rank, every read on every rank):
+Config 5 (docs sharded; one genus model per rank; rank r parses its byte
+range, the reads are all-gathered, the hit columns go back to their reads'
+rank by all-to-all, every rank writes its shard):
     python tools/sharded_classify.py docs-setup  --root DIR --world N [--reads R]  # N genus models of 60 species
     python tools/sharded_classify.py docs-single --root DIR --world N              # all models in one process
     torchrun --nproc-per-node N tools/sharded_classify.py docs-shard --root DIR
-    python tools/sharded_classify.py docs-check  --root DIR
+    python tools/sharded_classify.py docs-check  --root DIR --world N
 
 Config 5 with ONE bank column-split over the ranks (the `setup` model):
     python tools/sharded_classify.py bank-single --root DIR        # predict_columnar -> bank_single.json
     torchrun --nproc-per-node N tools/sharded_classify.py bank-shard --root DIR
-    python tools/sharded_classify.py bank-check  --root DIR
+    python tools/sharded_classify.py bank-check  --root DIR --world N
 
 `shard` runs xspect2_amd.classify.classify_species_sharded: each rank parses
 its byte range of reads.fq, the D+1 totals are all-reduced (RCCL, or gloo
@@ -146,9 +148,8 @@ def main() -> int:
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         model = ProbabilisticFilterModel.load(classify.species_model_path(GENERA[dist.get_rank()]))
-        res = distributed.predict_docs_sharded(model, root / "docs_reads.fasta", step=a.step)
-        if dist.get_rank() == 0:
-            res.save(root / "docs_sharded.json")
+        # each rank writes the shard of its own reads (byte range of the file)
+        distributed.classify_docs_sharded(model, root / "docs_reads.fasta", root / "docs_sharded.json", step=a.step)
         dist.barrier()
         dist.destroy_process_group()
     elif a.cmd == "bank-single":
@@ -174,23 +175,21 @@ def main() -> int:
         model = distributed.load_docs_slice(ProbabilisticFilterSVMModel, classify.species_model_path(GENUS))
         print(f"rank {dist.get_rank()}: docs {model.index.num_docs}", file=sys.stderr)
         res = distributed.predict_bank_sharded(model, root / "reads.fq", step=a.step)
-        if dist.get_rank() == 0:
-            res.save(root / "bank_sharded.json")
+        res.save(distributed.shard_path(root / "bank_sharded.json", dist.get_rank(), dist.get_world_size()))
         dist.barrier()
         dist.destroy_process_group()
-    elif a.cmd == "bank-check":
-        a_ = (root / "bank_single.json").read_bytes()
-        b_ = (root / "bank_sharded.json").read_bytes()
+    elif a.cmd in ("bank-check", "docs-check"):
+        # merged shards, serialised as ModelResult.save does, against one process's file
+        from xspect2_amd.distributed import merge_result_shards, shard_path
+        stem = "bank" if a.cmd == "bank-check" else "docs"
+        a_ = (root / f"{stem}_single.json").read_bytes()
+        shards = [shard_path(root / f"{stem}_sharded.json", r, a.world) for r in range(a.world)]
+        got = merge_result_shards(shards)
+        b_ = json.dumps(got, indent=4).encode("utf-8")
         d = json.loads(a_)
-        print(json.dumps({"docs": len(d["scores"]["total"]), "reads": len(d["hits"]), "equal_bytes": a_ == b_,
-                          "prediction": d.get("prediction"), "json_bytes": len(a_)}))
-        return 0 if a_ == b_ else 1
-    elif a.cmd == "docs-check":
-        a_ = (root / "docs_single.json").read_bytes()
-        b_ = (root / "docs_sharded.json").read_bytes()
-        d = json.loads(a_)
-        print(json.dumps({"docs": len(d["scores"]["total"]), "reads": len(d["hits"]), "equal_bytes": a_ == b_,
-                          "json_bytes": len(a_)}))
+        print(json.dumps({"world": a.world, "docs": len(d["scores"]["total"]), "reads": len(d["hits"]),
+                          "equal_bytes": a_ == b_, "prediction": d.get("prediction"), "json_bytes": len(a_),
+                          "reads_per_shard": [len(json.loads(p.read_text())["hits"]) for p in shards]}))
         return 0 if a_ == b_ else 1
     else:
         from xspect2_amd.distributed import merge_result_shards, shard_path

@@ -120,6 +120,7 @@ SIGNATURES = {
     "xs_query_hits": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _int, _vp]),
     "xs_query_hits_device": (_int, [_vp, _vp, _u64, _vp, _u64, _u64, _u32, _vp, _int, _vp, _vp]),
     "xs_memcpy_to_host": (_int, [_vp, _vp, _u64]),
+    "xs_memcpy_device": (_int, [_vp, _vp, _u64, _vp]),
     "xs_host_alloc": (_int, [_u64, _pp]),
     "xs_host_free": (None, [_vp]),
     "xs_query_totals": (_int, [_vp, _vp, _vp, _u64, _u32, _vp, _vp]),
@@ -141,6 +142,7 @@ SIGNATURES = {
                                         ctypes.c_char_p, _vp, _vp, _vp, _u64, _vp, _int]),
     "xs_ids_json_quote": (_int, [ctypes.c_char_p, _vp, _u64, _vp, _u64, _vp]),
     "xs_ids_has_duplicates": (_int, [ctypes.c_char_p, _vp, _u64, ctypes.POINTER(_int)]),
+    "xs_ids_hash128": (_int, [ctypes.c_char_p, _vp, _u64, _vp]),
     "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
     "xs_fastx_open_range": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),

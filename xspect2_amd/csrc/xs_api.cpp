@@ -1343,6 +1343,12 @@ int xs_memcpy_to_host(void* host, const void* dev, uint64_t bytes) {
     return XS_OK;
 }
 
+int xs_memcpy_device(void* dst, const void* src, uint64_t bytes, void* stream) {
+    if (bytes && (!dst || !src)) return fail(XS_ERR_ARG, "null argument");
+    if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+    return XS_OK;
+}
+
 int xs_host_alloc(uint64_t bytes, void** out) {
     if (!out) return fail(XS_ERR_ARG, "null argument");
     *out = nullptr;

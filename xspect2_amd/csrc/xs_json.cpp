@@ -365,6 +365,62 @@ int xs_ids_json_quote(const char* buf, const uint64_t* offs, uint64_t n, char* o
     return XS_OK;
 }
 
+// XXH64 (the published xxHash 64-bit algorithm), host side, for id keys.
+namespace {
+constexpr uint64_t kP1 = 0x9E3779B185EBCA87ull, kP2 = 0xC2B2AE3D27D4EB4Full, kP3 = 0x165667B19E3779F9ull,
+                   kP4 = 0x85EBCA77C2B2AE63ull, kP5 = 0x27D4EB2F165667C5ull;
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+inline uint64_t rd64(const unsigned char* p) { uint64_t v; memcpy(&v, p, 8); return v; }
+inline uint32_t rd32(const unsigned char* p) { uint32_t v; memcpy(&v, p, 4); return v; }
+inline uint64_t xround(uint64_t acc, uint64_t in) { return rotl64(acc + in * kP2, 31) * kP1; }
+inline uint64_t xmerge(uint64_t acc, uint64_t v) { return (acc ^ xround(0, v)) * kP1 + kP4; }
+
+uint64_t xxh64(const unsigned char* p, uint64_t len, uint64_t seed) {
+    const unsigned char* const end = p + len;
+    uint64_t h;
+    if (len >= 32) {
+        uint64_t v1 = seed + kP1 + kP2, v2 = seed + kP2, v3 = seed, v4 = seed - kP1;
+        for (; p + 32 <= end; p += 32) {
+            v1 = xround(v1, rd64(p));
+            v2 = xround(v2, rd64(p + 8));
+            v3 = xround(v3, rd64(p + 16));
+            v4 = xround(v4, rd64(p + 24));
+        }
+        h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+        h = xmerge(xmerge(xmerge(xmerge(h, v1), v2), v3), v4);
+    } else {
+        h = seed + kP5;
+    }
+    h += len;
+    for (; p + 8 <= end; p += 8) h = rotl64(h ^ xround(0, rd64(p)), 27) * kP1 + kP4;
+    if (p + 4 <= end) {
+        h = rotl64(h ^ (uint64_t)rd32(p) * kP1, 23) * kP2 + kP3;
+        p += 4;
+    }
+    for (; p < end; ++p) h = rotl64(h ^ (uint64_t)(*p) * kP5, 11) * kP1;
+    h ^= h >> 33;
+    h *= kP2;
+    h ^= h >> 29;
+    h *= kP3;
+    return h ^ (h >> 32);
+}
+}  // namespace
+
+// out[2i], out[2i+1] = XXH64(id i, seed 0), XXH64(id i, seed kP5): a 128-bit
+// key per id, for finding ids repeated across the shards of a read-sharded
+// job without moving the ids themselves.
+int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* out) {
+    if ((!buf && n && offs[n]) || !offs || (!out && n)) return xs::set_error(XS_ERR_ARG, "null argument");
+    for (uint64_t i = 0; i < n; ++i) {
+        if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
+        const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+        const uint64_t len = offs[i + 1] - offs[i];
+        out[2 * i] = xxh64(s, len, 0);
+        out[2 * i + 1] = xxh64(s, len, kP5);
+    }
+    return XS_OK;
+}
+
 // *has_dup = 1 when two of the n ids are equal (byte for byte).  Open addressing
 // over a 64-bit FNV-1a of each id; equal hashes are compared in full.
 int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int* has_dup) {

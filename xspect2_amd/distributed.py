@@ -79,6 +79,153 @@ def allreduce_(t, op=None):
     return t
 
 
+_EXC_TYPES = {"ValueError": ValueError, "IndexError": IndexError, "KeyError": KeyError,
+              "FileNotFoundError": FileNotFoundError, "NotImplementedError": NotImplementedError}
+
+
+def agree_or_raise(exc: BaseException | None) -> None:
+    """Every rank calls this with the exception its local step raised (or
+    None) before the job's next collective.  If any rank failed, every rank
+    raises: the failing rank its own exception, the others the same type and
+    message as the lowest failing rank's (a rank that raised alone would
+    leave its peers blocked in the next collective)."""
+    dist = _dist()
+    msgs: list = [None] * dist.get_world_size()
+    dist.all_gather_object(msgs, None if exc is None else (type(exc).__name__, str(exc)))
+    bad = [(r, m) for r, m in enumerate(msgs) if m is not None]
+    if not bad:
+        return
+    if exc is not None:
+        raise exc
+    _, (tname, msg) = bad[0]
+    raise _EXC_TYPES.get(tname, RuntimeError)(msg)
+
+
+def alltoallv(chunks: list):
+    """chunks[q] (tensors of equal trailing shape and dtype, any row count) to
+    rank q; returns the list of what every rank sent this one, in rank order,
+    on the collective device.  Two all_to_all_single calls: the row counts,
+    then the rows."""
+    import torch
+    dist = _dist()
+    dev = collective_device()
+    sizes = [int(c.shape[0]) for c in chunks]
+    cnt = torch.tensor(sizes, dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt)
+    rs = [int(x) for x in rcnt.tolist()]
+    send = torch.cat([c.to(dev) for c in chunks]).contiguous()
+    recv = torch.empty((sum(rs), *send.shape[1:]), dtype=send.dtype, device=dev)
+    dist.all_to_all_single(recv, send, output_split_sizes=rs, input_split_sizes=sizes)
+    return list(torch.split(recv, rs))
+
+
+def resolve_cross_shard_duplicates(res) -> int:
+    """Apply the reference's rule for repeated read ids to one shard of a
+    read-sharded job (``res``: this rank's MatrixResult, its own repeats
+    already collapsed): the reference keeps one dict entry per id, at the
+    position of its FIRST record with the values of its LAST record
+    (``hits[record.id] = ...``, probabilistic_filter_model.py:310), and sums
+    the job totals over that dict (result.py:76-90).
+
+    Ids are keyed by 128 bits (XXH64 of the id bytes with two seeds,
+    xs_ids_hash128) and sent to the rank that owns their hash range
+    (all-to-all); the owner finds keys present on several ranks.  For each,
+    the rank holding the first record keeps the id at its position and takes
+    the hit row and k-mer count of the last record (fetched from its rank);
+    every other rank drops the id.  Merging the shards in part order then
+    gives the single-process dictionaries, and each id enters the job
+    totals once.  Returns the number of rows this rank dropped.  Two
+    different ids share a key with probability ~n^2 / 2^129."""
+    import torch
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    if world == 1:
+        return 0
+    ids = res.ids if isinstance(res.ids, PackedIds) else PackedIds.of(res.ids)
+    n = len(ids)
+    key = ids.hash128().view(np.int64)                             # [n, 2]
+    owner = (key[:, 0].view(np.uint64) % np.uint64(world)).astype(np.int64)
+    rec = np.concatenate([key, np.arange(n, dtype=np.int64)[:, None]], axis=1)
+    got = alltoallv([torch.from_numpy(np.ascontiguousarray(rec[owner == q])) for q in range(world)])
+    # the owner: records from every source rank, sorted by key, then file order (rank, index)
+    allr = np.concatenate([np.concatenate([g.cpu().numpy().reshape(-1, 3),
+                                           np.full((g.shape[0], 1), s, dtype=np.int64)], axis=1)
+                           for s, g in enumerate(got)]) if got else np.zeros((0, 4), np.int64)
+    msgs = [[] for _ in range(world)]  # per destination: (kind, index, src rank, src index)
+    if allr.shape[0] > 1:
+        o = np.lexsort((allr[:, 2], allr[:, 3], allr[:, 1], allr[:, 0]))
+        a = allr[o]
+        same = (a[1:, 0] == a[:-1, 0]) & (a[1:, 1] == a[:-1, 1])
+        start = np.flatnonzero(np.concatenate([[True], ~same]))
+        size = np.diff(np.concatenate([start, [a.shape[0]]]))
+        for g in np.flatnonzero(size > 1).tolist():
+            s0, m = int(start[g]), int(size[g])
+            first, last = a[s0], a[s0 + m - 1]
+            msgs[int(first[3])].append((0, int(first[2]), int(last[3]), int(last[2])))   # keep, take last's values
+            for j in range(s0 + 1, s0 + m):
+                msgs[int(a[j, 3])].append((1, int(a[j, 2]), 0, 0))                       # drop
+    inst = alltoallv([torch.tensor(m, dtype=torch.int64).reshape(-1, 4) for m in msgs])
+    inst = np.concatenate([x.cpu().numpy().reshape(-1, 4) for x in inst]) if inst else np.zeros((0, 4), np.int64)
+    keep_take = inst[inst[:, 0] == 0]
+    drop = inst[inst[:, 0] == 1, 1]
+    # fetch the last records' rows: request (their index, my index) from their rank, answer with the rows
+    req = alltoallv([torch.from_numpy(np.ascontiguousarray(keep_take[keep_take[:, 2] == q][:, [3, 1]]))
+                     for q in range(world)])
+    D = res.hits.shape[1]
+    answers = []
+    for q, r in enumerate(req):
+        r = r.cpu().numpy().reshape(-1, 2)
+        row = np.zeros((r.shape[0], D + 2), dtype=np.int64)
+        row[:, 0] = r[:, 1]
+        if r.shape[0]:
+            row[:, 1] = res.num_kmers[r[:, 0]].astype(np.int64)
+            row[:, 2:] = res.hits[r[:, 0]].astype(np.int64)
+        answers.append(torch.from_numpy(row))
+    back = alltoallv(answers)
+    back = np.concatenate([b.cpu().numpy().reshape(-1, D + 2) for b in back]) if back else np.zeros((0, D + 2))
+    if back.shape[0]:
+        need = int(back[:, 2:].max()) if D else 0
+        hits = res.hits
+        if need > np.iinfo(hits.dtype).max:
+            hits = hits.astype(np.uint16 if need <= 0xFFFF else np.uint32)
+        else:
+            hits = hits.copy()
+        nk = res.num_kmers.copy()
+        idx = back[:, 0]
+        hits[idx] = back[:, 2:].astype(hits.dtype)
+        nk[idx] = back[:, 1].astype(np.uint64)
+        res.hits, res.num_kmers = hits, nk
+    if drop.size:
+        keep = np.ones(n, dtype=bool)
+        keep[drop] = False
+        rows = np.flatnonzero(keep)
+        res.ids = ids.take(rows) if isinstance(res.ids, PackedIds) else [res.ids[i] for i in rows.tolist()]
+        res.hits = np.ascontiguousarray(res.hits[rows])
+        res.num_kmers = np.ascontiguousarray(res.num_kmers[rows])
+    return int(drop.size)
+
+
+def set_job_totals(res, device=None) -> None:
+    """Make ``res`` (this rank's shard) carry the whole job's "total": one
+    all-reduce of the D+1 counters (per-doc sums, k-mer total) on `device`
+    (RCCL) or the host (gloo), and the job's first hit row, which orders the
+    "total" labels as the reference's get_total_hits does (result.py:84-90)."""
+    import torch
+    D = len(res.labels)
+    local = np.zeros(D + 1, dtype=np.int64)
+    if len(res.ids):
+        local[:D] = res.hits.sum(axis=0, dtype=np.uint64).astype(np.int64)
+        local[D] = int(res.num_kmers.sum())
+    t = torch.from_numpy(local)
+    if device is not None:
+        t = t.to(device)
+    allreduce_(t)  # RCCL over xGMI: per-doc totals + k-mer total, one collective
+    tot = t.cpu().numpy()
+    first = _job_first_row(res, D)
+    res.set_job_totals(tot[:D].astype(np.uint64), int(tot[D]), first)
+
+
 def allreduce_totals(totals: np.ndarray, total_kmers: int, device=None) -> tuple[np.ndarray, int]:
     """Sum of (per-doc totals, k-mer total) over all ranks (one collective)."""
     import torch
@@ -282,10 +429,11 @@ def classify_species_sharded(model, input_file: Path, output_path: Path, step: i
        scores and k-mer counts, the job's "total" and prediction.
 
     ``merge_result_shards`` of the shards equals the single-process JSON.
-    One deviation: a read id repeated in two different shards is kept once
-    per shard in the job's totals, where the single-process dictionaries keep
-    only its last record (repeats inside one shard collapse as there).
-    Returns this rank's MatrixResult (a shard)."""
+    A read id repeated in different shards follows the reference's dict
+    (``resolve_cross_shard_duplicates``): one entry, at the first record's
+    position with the last record's values, counted once in the totals.
+    An error on any rank (a read no longer than k, a malformed record)
+    raises on every rank.  Returns this rank's MatrixResult (a shard)."""
     import torch
     from .file_io import FileShard
     from .probabilistic_filter_model import ProbabilisticFilterModel
@@ -293,31 +441,34 @@ def classify_species_sharded(model, input_file: Path, output_path: Path, step: i
     dist = _dist()
     rank, world = dist.get_rank(), dist.get_world_size()
     input_file = Path(input_file)
-    res = ProbabilisticFilterModel.predict_columnar(model, FileShard(input_file, rank, world), exclude_ids, step,
-                                                    display_name)
-    D = len(res.labels)
-    local = np.zeros(D + 1, dtype=np.int64)
-    if res.ids:
-        local[:D] = res.hits.sum(axis=0, dtype=np.uint64).astype(np.int64)
-        local[D] = int(res.num_kmers.sum())
+    res, err = None, None
+    try:
+        res = ProbabilisticFilterModel.predict_columnar(model, FileShard(input_file, rank, world), exclude_ids,
+                                                        step, display_name)
+    except Exception as e:  # noqa: BLE001 - re-raised on every rank by agree_or_raise
+        err = e
+    agree_or_raise(err)
+    resolve_cross_shard_duplicates(res)
     dev = torch.device("cuda", model.index.info.device) if collective_device().type == "cuda" else None
-    t = torch.from_numpy(local)
-    if dev is not None:
-        t = t.to(dev)
-    allreduce_(t)  # RCCL over xGMI: per-doc totals + k-mer total, one collective
-    tot = t.cpu().numpy()
-    first = _job_first_row(res, D)
-    res.set_job_totals(tot[:D].astype(np.uint64), int(tot[D]), first)
-    if hasattr(model, "_get_svm"):  # ProbabilisticFilterSVMModel: label from the job's totals
-        out = [None]
-        if rank == 0:
-            features = [[v for _, v in sorted(res.get_total_scores().items())]]
-            out[0] = str(model._get_svm(exclude_ids).predict(features)[0])
-        dist.broadcast_object_list(out, src=0)
-        res.prediction = out[0]
+    set_job_totals(res, dev)
+    _svm_label(model, res, exclude_ids)
     res.input_source = input_file.name
     res.save(shard_path(output_path, rank, world))
     return res
+
+
+def _svm_label(model, res, exclude_ids=None) -> None:
+    """SVM models (ProbabilisticFilterSVMModel, probabilistic_filter_svm_model.py:
+    175-223): rank 0 classifies the job's total scores, every rank gets the label."""
+    if not hasattr(model, "_get_svm"):
+        return
+    dist = _dist()
+    out = [None]
+    if dist.get_rank() == 0:
+        features = [[v for _, v in sorted(res.get_total_scores().items())]]
+        out[0] = str(model._get_svm(exclude_ids).predict(features)[0])
+    dist.broadcast_object_list(out, src=0)
+    res.prediction = out[0]
 
 
 def merge_result_shards(paths) -> dict:
@@ -346,17 +497,30 @@ def merge_result_shards(paths) -> dict:
 # ---------------------------------------------------------------- config 5: docs-sharded classify
 def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: bool = False):
     """Config 5 (docs sharded): every rank holds a different species model (one
-    genus of a multi-genus collection, its bank on this rank's GPU) and probes
-    every read of the file; the per-read hit columns of all ranks are
-    all-gathered into one MatrixResult over every rank's docs (labels in rank
-    order), the same on every rank.
-
-    Under RCCL each batch goes to the device once, is probed there
-    (``docs_sharded_hits_device``: probe, narrow, all-gather over xGMI, widen)
-    and only the gathered matrix, narrowed to the reads' count width, comes
-    back.  Under gloo (CPU tests, shared-GPU rehearsal) the rows are probed
-    from host buffers and gathered through the host."""
+    genus of a multi-genus collection, its bank on this rank's GPU).  Rank r
+    parses only part r of the file (record-aligned byte ranges, as config 3);
+    each batch's reads are all-gathered, every rank probes every rank's reads
+    against its bank, and the hit columns go back to the rank that owns the
+    reads (``exchange_doc_columns``: one all-to-all in the narrowest exact
+    integer type).  Returns this rank's shard: its own reads with the hit
+    columns of every rank's docs (labels in rank order), and the job's
+    "total" over all reads (``set_job_totals``).  ``merge_result_shards`` of
+    the saved shards (``classify_docs_sharded``) is the JSON one process
+    probing every bank writes.  Under RCCL reads and hits stay on the device
+    from the reader to the exchanged columns; under gloo (CPU tests, the
+    shared-GPU rehearsal) they go through host tensors."""
     return _predict_doc_columns(model, input_file, step, display_name, "multi-genus-docs-sharded")
+
+
+def classify_docs_sharded(model, input_file: Path, output_path: Path, step: int = 1, display_name: bool = False):
+    """Config 5 for one input file: ``predict_docs_sharded`` and every rank
+    writes its JSON shard (``shard_path``), as ``classify_species_sharded``
+    does for config 3 (the reference writes one result per input,
+    src/xspect/classify.py:43-92, src/xspect/models/result.py:178-189)."""
+    dist = _dist()
+    res = predict_docs_sharded(model, input_file, step, display_name)
+    res.save(shard_path(output_path, dist.get_rank(), dist.get_world_size()))
+    return res
 
 
 def cobs_classic_docs(index_path: Path) -> int:
@@ -396,59 +560,159 @@ def load_docs_slice(cls, json_path: Path, rank: int | None = None, world: int | 
 def predict_bank_sharded(model, input_file: Path, step: int = 1, display_name: bool = False):
     """Config 5 with ONE bank column-split over the ranks (each rank's model
     from load_docs_slice): every rank hashes every k-mer and reads its slice of
-    each row; the gathered MatrixResult is the whole model's prediction (labels
-    in doc order, the model's slug; an SVM model's label formed from the
-    gathered totals, probabilistic_filter_svm_model.py:175-223)."""
+    each row; the result is this rank's shard of the whole model's prediction
+    (its own reads, labels in doc order, the model's slug, the job's totals);
+    an SVM model's label is formed on rank 0 from the job's total scores
+    (probabilistic_filter_svm_model.py:175-223) and broadcast."""
     res = _predict_doc_columns(model, input_file, step, display_name, model.slug())
-    if hasattr(model, "_get_svm") and len(res.ids):
-        res.prediction = str(model._get_svm(None).predict([[v for _, v in sorted(res.get_total_scores().items())]])[0])
+    _svm_label(model, res)
     return res
+
+
+def exchange_doc_columns(hits, counts: list[int], dims: list[int], wire):
+    """Hit columns [sum(counts), D_r] of this rank (rows: rank 0's reads, then
+    rank 1's, ...) -> this rank's reads with every rank's columns
+    [counts[rank], sum(dims)] in the wire dtype (uint8 / int16 / int32, from
+    ``transport_dtype``), on the tensor's device.  Rows are narrowed where
+    they are, padded to the widest D_r and sent by one all-to-all (RCCL over
+    xGMI on the device); the narrow result is what the shard keeps."""
+    import torch
+    dist = _dist()
+    rank, world = dist.get_rank(), dist.get_world_size()
+    d_local, d_max = int(hits.shape[1]), max(dims)
+    if dims[rank] != d_local or int(hits.shape[0]) != sum(counts):
+        raise ValueError("hit columns do not match the agreed layout")
+    n_me = counts[rank]
+    if d_local == d_max:
+        send = hits.to(wire)  # lossless: counts <= k-mers per read <= the wire type's maximum
+    else:
+        send = torch.zeros((hits.shape[0], d_max), dtype=wire, device=hits.device)
+        send[:, :d_local] = hits.to(wire)
+    # gloo and RCCL move no int16: 2-byte rows travel as float16 bit patterns
+    wire_view = send.view(torch.float16) if wire == torch.int16 else send
+    w = _on_wire(wire_view.contiguous())
+    recv = torch.empty((world * n_me, d_max), dtype=w.dtype, device=w.device)
+    dist.all_to_all_single(recv, w, output_split_sizes=[n_me] * world, input_split_sizes=list(counts))
+    if wire == torch.int16:
+        recv = recv.view(torch.int16)
+    recv = recv.to(hits.device) if recv.device != hits.device else recv
+    blocks = recv.view(world, n_me, d_max)
+    return torch.cat([blocks[r, :, :dims[r]] for r in range(world)], dim=1).contiguous()
+
+
+def _read_device_batch(batch, dev, pad_to: int):
+    """A device reader batch's sequences and offsets as torch tensors on `dev`
+    (sequences padded to `pad_to` bytes for the all-gather)."""
+    import torch
+    from ._lib import check, load
+    seq = torch.zeros(max(pad_to, 1), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    if batch.seq_bytes:
+        check(load().xs_memcpy_device(seq.data_ptr(), batch.seqs_ptr, batch.seq_bytes, stream))
+    off = torch.from_numpy(batch.offsets.view(np.int64)).to(dev)
+    return seq, off
 
 
 def _predict_doc_columns(model, input_file: Path, step: int, display_name: bool, slug: str):
     import torch
-    from .bank import narrowest_count_dtype
     from .file_io import check_input_path, file_reader_device, read_batches
+    from .packing import PackedReads
     from .result import MatrixResult
 
     dist = _dist()
-    world = dist.get_world_size()
+    rank, world = dist.get_rank(), dist.get_world_size()
     input_file = Path(input_file)
-    check_input_path(input_file)
-    labels_all: list = [None] * world
-    dist.all_gather_object(labels_all, model._labels(display_name))
-    labels = [lab for part in labels_all for lab in part]
+    err = None
+    try:
+        check_input_path(input_file)
+        if step < 1:
+            raise ValueError("step must be >= 1")
+    except Exception as e:  # noqa: BLE001 - raised on every rank below
+        err = e
+    agree_or_raise(err)
+    # the layout, once per file: every rank's labels (doc columns) and k
+    meta_all: list = [None] * world
+    dist.all_gather_object(meta_all, (model._labels(display_name), int(model.k)))
+    labels = [lab for part, _ in meta_all for lab in part]
+    dims = [len(part) for part, _ in meta_all]
+    ks = {k for _, k in meta_all}
+    if len(ks) != 1:
+        raise ValueError(f"docs-sharded models must share k (one k-mer count per read), got {sorted(ks)}")
+    k = ks.pop()
     on_device = collective_device().type == "cuda"
+    dev = torch.device("cuda", model.index.info.device) if on_device else torch.device("cpu")
+    rdev = file_reader_device(model.index) if on_device else None
     ids, hits, nks = [], [], []
-    rdev = file_reader_device(model.index) if on_device else None  # text straight to HBM
-    for batch in read_batches(input_file, device=rdev):
-        L = batch.lengths()
-        if (L <= model.k).any():
-            raise ValueError("Invalid sequence, must be longer than k")
-        mx = int(((L - model.k) // step + 1).max()) if batch.n else 0
-        if on_device:
-            if rdev is not None:
-                batch.check_valid()
-                d_seq, nbytes, d_off = batch.seqs_ptr, batch.seq_bytes, batch.offsets_ptr
+    batches = read_batches(input_file, part=rank, parts=world, device=rdev)
+    try:
+        while True:
+            b, err = None, None
+            try:
+                b = next(batches, None)
+                if b is not None and rdev is not None:
+                    b.check_valid()
+                L = b.lengths() if b is not None and b.n else np.zeros(0, dtype=np.uint64)
+                if (L <= k).any():
+                    raise ValueError("Invalid sequence, must be longer than k")
+            except Exception as e:  # noqa: BLE001 - raised on every rank
+                err = e
+            agree_or_raise(err)
+            n = b.n if b is not None else 0
+            nbytes = (b.seq_bytes if rdev is not None else b.packed.nbytes) if n else 0
+            m = torch.tensor([n, nbytes, int(L.max()) if n else 0], dtype=torch.int64, device=dev)
+            allm = [torch.empty_like(m) for _ in range(world)]
+            dist.all_gather(allm, m)
+            meta = torch.stack(allm).cpu().numpy()
+            counts, sizes = meta[:, 0].tolist(), meta[:, 1].tolist()
+            if sum(counts) == 0:
+                break
+            wire = transport_dtype((int(meta[:, 2].max()) - k) // step + 1)
+            b_max, n_max = max(max(sizes), 1), max(counts)
+            # every rank's reads of this batch, on every rank
+            if rdev is not None and n:
+                seq, off = _read_device_batch(b, dev, b_max)
             else:
-                pr = batch.packed
-                dev = torch.device("cuda", model.index.info.device)
-                d_seq = torch.from_numpy(pr.buf[:max(pr.nbytes, 1)]).to(dev)
-                d_off = torch.from_numpy(pr.offsets.view(np.int64)).to(dev)
-                nbytes = pr.nbytes
-            g, d_nk = docs_sharded_hits_device(model.index, d_seq, nbytes, d_off, batch.n, step)
-            dt = narrowest_count_dtype(mx)
-            h = g.to({np.uint8: torch.uint8, np.uint16: torch.int16}.get(dt, torch.int32)).cpu().numpy()
-            h = h.view(np.uint16) if dt == np.uint16 else h.view(np.uint8) if dt == np.uint8 else h.view(np.uint32)
-            nk = d_nk.cpu().numpy().view(np.uint64)
-        else:
-            hl, nk = model._query(batch.packed, step)
-            t = torch.from_numpy(np.ascontiguousarray(hl).astype(np.int32))
-            h = gather_doc_shards(t, mx).numpy().view(np.uint32)  # every rank reads the same batches
-        ids.append(batch.ids_packed())
-        hits.append(h)
-        nks.append(nk)
-    ids = PackedIds.concat(ids) if ids else []
+                seq = torch.zeros(b_max, dtype=torch.uint8)
+                off = torch.zeros(n + 1, dtype=torch.int64)
+                if n:
+                    seq[:nbytes] = torch.from_numpy(b.packed.buf[:nbytes])
+                    off = torch.from_numpy(b.packed.offsets.astype(np.int64))
+                seq, off = seq.to(dev), off.to(dev)
+            offp = torch.zeros(n_max + 1, dtype=torch.int64, device=dev)
+            offp[:n + 1] = off[:n + 1]
+            seqs = [torch.empty_like(seq) for _ in range(world)]
+            offs = [torch.empty_like(offp) for _ in range(world)]
+            dist.all_gather(seqs, seq)
+            dist.all_gather(offs, offp)
+            cat_seq = torch.cat([seqs[q][:sizes[q]] for q in range(world)] or [seq[:0]])
+            base = np.concatenate([[0], np.cumsum(sizes)]).tolist()
+            cat_off = torch.cat([offs[q][:counts[q]] + base[q] for q in range(world)] +
+                                [torch.tensor([base[-1]], dtype=torch.int64, device=dev)])
+            N = sum(counts)
+            if on_device:
+                d_hits = torch.empty((N, model.index.num_docs), dtype=torch.int32, device=dev)
+                d_nk = torch.empty(N, dtype=torch.int64, device=dev)
+                stream = torch.cuda.current_stream(dev)
+                model.index.query_device(cat_seq, base[-1], cat_off, N, step, d_hits, d_nk, None,
+                                         stream=stream.cuda_stream)
+                cols = exchange_doc_columns(d_hits, counts, dims, wire)
+                lo = int(np.sum(counts[:rank]))
+                nk = d_nk[lo:lo + n].cpu().numpy().view(np.uint64)
+            else:
+                buf = np.concatenate([cat_seq.numpy(), np.zeros(1, dtype=np.uint8)])
+                h, nk_all = model._query(PackedReads(buf, cat_off.numpy().astype(np.uint64)), step)
+                cols = exchange_doc_columns(torch.from_numpy(np.ascontiguousarray(h).astype(np.int32)),
+                                            counts, dims, wire)
+                lo = int(np.sum(counts[:rank]))
+                nk = np.asarray(nk_all, dtype=np.uint64)[lo:lo + n]
+            hc = cols.cpu().numpy()
+            hc = hc.view(np.uint16) if wire == torch.int16 else hc.view(np.uint32) if wire == torch.int32 else hc
+            if n:
+                ids.append(b.ids_packed())
+                hits.append(hc)
+                nks.append(nk)
+    finally:
+        batches.close()
     D = len(labels)
     if hits:
         dt = max((h.dtype for h in hits), key=lambda t: t.itemsize)
@@ -456,6 +720,8 @@ def _predict_doc_columns(model, input_file: Path, step: int, display_name: bool,
         nk = np.concatenate(nks)
     else:
         hm, nk = np.zeros((0, D), np.uint8), np.zeros(0, np.uint64)
-    res = MatrixResult(slug, ids, labels, hm, nk, sparse_sampling_step=step)
+    res = MatrixResult(slug, PackedIds.concat(ids) if ids else [], labels, hm, nk, sparse_sampling_step=step)
+    resolve_cross_shard_duplicates(res)
+    set_job_totals(res, dev if on_device else None)
     res.input_source = input_file.name
     return res

@@ -173,6 +173,27 @@ class PackedIds(Sequence):
                                            ctypes.byref(flag)))
         return bool(flag.value)
 
+    def take(self, index) -> "PackedIds":
+        """The ids at `index` (int array), in that order, still packed."""
+        idx = np.asarray(index, dtype=np.int64)
+        starts = self.offs[:-1][idx].astype(np.int64)
+        lens = self.offs[1:][idx].astype(np.int64) - starts
+        offs = np.zeros(idx.size + 1, dtype=np.uint64)
+        np.cumsum(lens, out=offs[1:])
+        pos = np.repeat(starts - offs[:-1].astype(np.int64), lens) + np.arange(int(offs[-1]), dtype=np.int64)
+        return PackedIds(np.frombuffer(self.buf, dtype=np.uint8)[pos].tobytes(), offs)
+
+    def hash128(self) -> np.ndarray:
+        """[n, 2] uint64: XXH64 of every id's bytes with two seeds (xs_ids_hash128)."""
+        import ctypes
+
+        from ._lib import check, load
+        out = np.zeros((len(self), 2), dtype=np.uint64)
+        if len(self):
+            check(load().xs_ids_hash128(self.buf, ctypes.c_void_p(self.offs.ctypes.data), len(self),
+                                        ctypes.c_void_p(out.ctypes.data)))
+        return out
+
     def json_packed(self) -> tuple[bytes, np.ndarray]:
         """json.dumps(id) of every id, packed, and n+1 offsets."""
         n = len(self)

@@ -260,8 +260,16 @@ class MatrixResult:
             mr = self.to_model_result()
             if not shard:
                 return mr.save(path)
-            d = mr.to_dict()
-            d["scores"]["total"] = self.get_total_scores()
+            # the shard's own reads, the job's "total" (no local get_total_hits:
+            # a shard may hold no reads)
+            scores = {sub: {lab: round(v / mr.num_kmers[sub], 2) for lab, v in per.items()}
+                      for sub, per in mr.hits.items()}
+            scores["total"] = self.get_total_scores()
+            d = {"model_slug": mr.model_slug, "sparse_sampling_step": mr.sparse_sampling_step, "hits": mr.hits,
+                 "scores": scores, "num_kmers": mr.num_kmers, "misclassified": mr.misclassified,
+                 "input_source": mr.input_source}
+            if mr.prediction is not None:
+                d["prediction"] = mr.prediction
             path.parent.mkdir(exist_ok=True, parents=True)
             path.write_text(dumps(d, indent=4), encoding="utf-8")
             return None
