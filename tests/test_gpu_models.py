@@ -186,6 +186,79 @@ def test_svm_model_vector_and_prediction(tmp_path, species_dir, genomes):
     assert (tmp_path / "col.json").read_bytes() == (tmp_path / "ref.json").read_bytes()
 
 
+def _mutate(seq: bytes, rate: float, rng) -> bytes:
+    a = np.frombuffer(seq, dtype=np.uint8).copy()
+    pos = np.flatnonzero(rng.random(a.size) < rate)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    a[pos] = acgt[(np.searchsorted(acgt, a[pos]) + rng.integers(1, 4, pos.size)) % 4]
+    return a.tobytes()
+
+
+@pytest.mark.parametrize("svm_step", [1, 3])
+def test_svm_scores_csv_and_label_against_the_oracle(tmp_path, species_dir, genomes, oracle_mod, svm_step):
+    """ProbabilisticFilterSVMModel.fit on the GPU writes scores.csv; every row
+    equals the row computed on the CPU from the same genomes: the oracle's
+    hits of each file's records, the reference's per-record dict (a repeated
+    record id keeps its last record, probabilistic_filter_model.py:310),
+    totals round(T_d / N, 2) (result.py:57-90) sorted by label and written
+    with str() (probabilistic_filter_svm_model.py:144-173), files in the
+    reference's iterdir walk order.  The label of a query is then the one an
+    SVC fitted on the CPU rows predicts for the oracle's feature vector
+    (:208-274)."""
+    import fastx  # oracle/fastx.py: the Biopython restatement (test infrastructure)
+    from sklearn.svm import SVC
+    from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
+
+    rng = np.random.default_rng(17 + svm_step)
+    svm_dir = tmp_path / "svm"
+    for i in range(4):
+        for j in range(3):
+            # mutated windows of genome i (and a slice of its neighbour): partial scores
+            g = genomes[i].tobytes()
+            body = _mutate(g[j * 6000:j * 6000 + 12_000], 0.01 * (j + 1), rng)
+            other = genomes[(i + 1) % 4].tobytes()[:2000]
+            recs = [Record(f"c{j}", body.decode()), Record("tail", other.decode())]
+            if j == 2:  # a repeated record id: the dict keeps the last record
+                recs.append(Record("tail", _mutate(other, 0.05, rng).decode()))
+            write_fasta(recs, svm_dir / f"label{i}" / f"acc{i}{j}.fasta", width=70)
+    base = tmp_path / "xspect_data"
+    model = ProbabilisticFilterSVMModel(K, "Acinetobacter", None, None, "Species", base, "rbf", 1.0)
+    model.fit(species_dir, svm_dir, svm_step=svm_step)
+    got = (base / "acinetobacter-species" / "scores.csv").read_text().split("\n")
+
+    ob, names = _oracle_species(oracle_mod, species_dir)
+    want = ["file," + ",".join(sorted(names)) + ",label_id"]
+    for folder in svm_dir.iterdir():            # the reference's walk: iterdir, unsorted
+        if not folder.is_dir():
+            continue
+        for f in folder.iterdir():
+            if f.suffix[1:] not in ("fasta", "fna", "fa", "ffn", "frn", "fastq", "fq"):
+                continue
+            recs = fastx.parse_file(f)
+            h, nk = ob.query([seq for _, seq in recs], step=svm_step)
+            last = {rid: i for i, (rid, _) in enumerate(recs)}          # dict semantics: last record wins
+            rows = list(last.values())
+            tot = h[rows].sum(axis=0, dtype=np.uint64)
+            n_all = int(nk[rows].sum())
+            scores = {names[d]: round(int(tot[d]) / n_all, 2) for d in range(len(names))}
+            want.append(f"{f.stem}," + ",".join(str(scores[k]) for k in sorted(scores)) + f",{folder.name}")
+    assert got == want
+    vals = [r.split(",")[1:-1] for r in want[1:]]
+    assert any(0 < float(v) < 1 for r in vals for v in r)  # partial scores, not only 0 / 1
+
+    # the label: SVC fitted on the CPU rows, fed the oracle's feature vector of the query
+    x = [[float(v) for v in r.split(",")[1:-1]] for r in want[1:]]
+    y = [r.split(",")[-1] for r in want[1:]]
+    svc = SVC(kernel="rbf", C=1.0).fit(x, y)
+    for gi in range(4):
+        q = _mutate(genomes[gi].tobytes()[3000:15_000], 0.02, rng)
+        h, nk = ob.query([q], step=5)
+        feat = [round(int(h[0, d]) / int(nk[0]), 2) for d in np.argsort(names, kind="stable")]
+        res = model.predict([Record("q", q.decode())], step=5)
+        assert ProbabilisticFilterSVMModel.svm_vector(res) == feat
+        assert res.prediction == str(svc.predict([feat])[0])
+
+
 def test_genus_bloom_model(tmp_path, genomes, oracle_mod):
     from xspect2_amd.probabilistic_single_filter_model import ProbabilisticSingleFilterModel
 

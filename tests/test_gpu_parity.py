@@ -921,6 +921,50 @@ def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, monkeypatch, mode):
     gb.close()
 
 
+@pytest.mark.parametrize("mode", ["0", "3"])
+def test_device_reads_narrowing_checks_real_counts(xs, oracle_mod, monkeypatch, mode):
+    """xs_query_hits_device on device-resident reads (a device reader batch's
+    form): several chunks, each planned from its own bytes, equal the oracle
+    in u8 / u16, totals-only included; a caller's max_len below the longest
+    read no longer truncates counts silently: the narrowing kernel flags any
+    count wider than hit_bytes and the call fails."""
+    import ctypes
+    import torch
+    from xspect2_amd import _lib
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=6)
+    rng = np.random.default_rng(6)
+    genome = b"".join(seqs)
+    reads = [genome[o:o + 150] for o in rng.integers(0, len(genome) - 400, 300_000)] + [genome[:400]]
+    want, want_n = ob.query(reads)
+    buf = b"".join(reads)
+    offs = np.zeros(len(reads) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([len(r) for r in reads])
+    d_seq = torch.from_numpy(np.frombuffer(buf, dtype=np.uint8).copy()).cuda()
+    d_off = torch.from_numpy(offs.view(np.int64)).cuda()
+    n = len(reads)
+    lib = _lib.load()
+    for hb, dt, max_len in ((2, np.uint16, 400), (4, np.uint32, 400)):
+        hits = np.zeros((n, 100), dtype=dt)
+        nk = np.zeros(n, dtype=np.uint64)
+        tot = np.zeros(101, dtype=np.uint64)
+        rc = lib.xs_query_hits_device(gb.handle, d_seq.data_ptr(), len(buf), d_off.data_ptr(), n, max_len, 1,
+                                      hits.ctypes.data, hb, nk.ctypes.data, tot.ctypes.data)
+        assert rc == 0, lib.xs_last_error()
+        assert np.array_equal(hits.astype(np.uint32), want) and np.array_equal(nk, want_n)
+        assert np.array_equal(tot[:100], want.sum(axis=0, dtype=np.uint64)) and int(tot[100]) == int(want_n.sum())
+    tot = np.zeros(101, dtype=np.uint64)  # totals only: one chunk
+    assert lib.xs_query_hits_device(gb.handle, d_seq.data_ptr(), len(buf), d_off.data_ptr(), n, 400, 1, None, 4,
+                                    None, tot.ctypes.data) == 0
+    assert np.array_equal(tot[:100], want.sum(axis=0, dtype=np.uint64))
+    # the 400-bp read has 380 k-mers: a max_len of 150 claims u8 suffices
+    hits = np.zeros((n, 100), dtype=np.uint8)
+    rc = lib.xs_query_hits_device(gb.handle, d_seq.data_ptr(), len(buf), d_off.data_ptr(), n, 150, 1,
+                                  hits.ctypes.data, 1, None, None)
+    assert rc == _lib.XS_ERR_ARG and b"does not fit" in lib.xs_last_error()
+    gb.close()
+
+
 def test_pass_stats_of_the_partitioned_probe(xs, oracle_mod, monkeypatch):
     """xs_bank_pass_stats: with profiling on, the partitioned probe's passes
     are timed on the launch stream; their sum is within the probe's own time."""

@@ -155,7 +155,7 @@ struct xs_bank {
     std::mutex mu;
     // workspace
     DevBuf seqs, offs, nseg, unit_ofs, unit_read, n_units, scan_tmp, nk, hits, partials, totals, tmp,
-        best, narrow;
+        best, narrow, ovf;
     DevBuf rows_read;               // profiling: filter words the rbloom probe loaded
     DevBuf pk_nkc, pk_kofs, pk_scan, pk_entries, pk_tbl, pk_miss, pk_aux;  // partitioned probes (rbloom, COBS)
     // rbloom path choice: member fraction of the last query whose totals have
@@ -170,6 +170,7 @@ struct xs_bank {
     hipEvent_t stage_ev[2] = {nullptr, nullptr};
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
     PinnedBuf small_h;              // small host calls: the whole request and its results (query_small)
+    PinnedBuf cut_ofs;              // device-read batches: read offsets at the chunk cuts
     DevBuf small_d;
     hipEvent_t hstage_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr, d2h_stream = nullptr;
@@ -189,7 +190,7 @@ struct xs_bank {
 
     xs_bank() {
         for (DevBuf* d : {&seqs, &offs, &nseg, &unit_ofs, &unit_read, &n_units, &scan_tmp, &nk, &hits, &partials,
-                          &totals, &tmp, &best, &narrow, &rows_read, &pk_nkc, &pk_kofs, &pk_scan, &pk_entries, &pk_tbl,
+                          &totals, &tmp, &best, &narrow, &ovf, &rows_read, &pk_nkc, &pk_kofs, &pk_scan, &pk_entries, &pk_tbl,
                           &pk_miss, &pk_aux, &bloom_tot}) {
             d->guard_ev = &ws_ev;
             d->guard_used = &ws_used;
@@ -475,9 +476,11 @@ int write_bloom_file(xs_bank* b, const char* path) {
 // ---- query / build pipeline --------------------------------------------------
 struct Inputs {
     const uint8_t* seqs;
-    uint64_t seq_bytes;
+    uint64_t seq_bytes;      // readable bytes from seqs (window loads stop there)
     const uint64_t* offs;
     uint64_t n;
+    uint64_t read_bytes = 0;  // bytes of these n reads (plans and bounds); 0: seq_bytes
+    uint64_t plan_bytes() const { return read_bytes ? read_bytes : seq_bytes; }
 };
 
 // Unit decomposition (k-mer counts, units, unit -> read map) for n device-resident reads.
@@ -488,7 +491,7 @@ int prepare_units(xs_bank* b, const Inputs& in, uint32_t step, uint64_t* d_nk, u
     if (int rc = b->nseg.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->unit_ofs.ensure((in.n + 1) * 8)) return rc;
     if (int rc = b->n_units.ensure(2 * sizeof(uint64_t))) return rc;
-    const uint64_t unit_bound = in.n + in.seq_bytes / kSegKmers + 1;
+    const uint64_t unit_bound = in.n + in.plan_bytes() / kSegKmers + 1;
     if (int rc = b->unit_read.ensure(unit_bound * 4)) return rc;
     const size_t tb = scan_temp_bytes(in.n ? in.n : 1);
     if (int rc = b->scan_tmp.ensure(tb)) return rc;
@@ -530,7 +533,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     CobsPartPlan cplan;
     bool cobs_part = false;
     if (!bloom) {
-        cobs_part = cobs_part_plan(b->cobs_view(), b->k, in.n, in.seq_bytes, step, &cplan) &&
+        cobs_part = cobs_part_plan(b->cobs_view(), b->k, in.n, in.plan_bytes(), step, &cplan) &&
                     !(b->pk_nkc.ensure(cplan.nkc_bytes) || b->pk_kofs.ensure(cplan.nkc_bytes) ||
                       b->pk_scan.ensure(cplan.scan_bytes) || b->pk_entries.ensure(cplan.entry_bytes) ||
                       b->pk_tbl.ensure(cplan.tbl_bytes) || b->pk_aux.ensure(cplan.aux_bytes));
@@ -576,7 +579,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         }
         return true;
     };
-    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.seq_bytes, step, b->member_frac, &plan) && part_ws()) {
+    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.plan_bytes(), step, b->member_frac, &plan) && part_ws()) {
         path = XS_PATH_PARTITIONED;
         const BloomPartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                              b->pk_entries.as<uint64_t>(), b->pk_tbl.as<uint16_t>(), b->pk_miss.as<uint32_t>(),
@@ -724,9 +727,20 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     const uint64_t pcols = cols + 1;
     std::vector<uint64_t> cut{0};
+    std::vector<uint64_t> cut_ofs;  // device reads: offsets at the cuts (the chunks' byte counts)
     if (dev) {
-        const uint64_t per = std::max<uint64_t>(kDevChunkReads, (n + 3) / 4);
+        // chunks overlap the hit rows' D2H with the next chunk's probe; without
+        // rows to bring back, one chunk (a partitioned probe reloads the bank's
+        // partitions into L2 per chunk)
+        const uint64_t per = hits_host ? std::max<uint64_t>(kDevChunkReads, (n + 3) / 4) : n;
         while (cut.back() < n) cut.push_back(std::min(n, cut.back() + per));
+        if (int rc = b->cut_ofs.ensure(cut.size() * 8)) return rc;
+        cut_ofs.resize(cut.size());
+        for (size_t j = 0; j < cut.size(); ++j)
+            HIPCHK(hipMemcpyAsync(static_cast<uint64_t*>(b->cut_ofs.p) + j, dev->offs + cut[j], 8, hipMemcpyDeviceToHost,
+                                  b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        memcpy(cut_ofs.data(), b->cut_ofs.p, cut.size() * 8);
     } else {
         for (size_t limit = kHostFirst; cut.back() < n; limit = kHostChunk) {
             const uint64_t r0 = cut.back();
@@ -754,8 +768,12 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     }
     if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
     if (hits_host && !b->d2h_stream) HIPCHK(hipStreamCreateWithFlags(&b->d2h_stream, hipStreamNonBlocking));
-    if (hits_host && hit_bytes != 4)
+    const bool narrowing = hits_host && hit_bytes != 4;
+    if (narrowing) {
         if (int rc = b->narrow.ensure(n * cols * (uint64_t)hit_bytes + 16)) return rc;
+        if (int rc = b->ovf.ensure(sizeof(uint32_t))) return rc;
+        HIPCHK(hipMemsetAsync(b->ovf.p, 0, sizeof(uint32_t), b->stream));
+    }
     while (hits_host && b->chunk_ev.size() < nc) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -795,14 +813,15 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
             used[slot] = true;
             HIPCHK(hipStreamWaitEvent(b->stream, b->hstage_ev[slot], 0));
         }
-        const Inputs in{d_seqs, dev ? bytes : offsets[r1] - base, d_offs + r0, r1 - r0};
+        const Inputs in{d_seqs, dev ? bytes : offsets[r1] - base, d_offs + r0, r1 - r0,
+                        dev ? cut_ofs[i + 1] - cut_ofs[i] : offsets[r1] - offsets[r0]};
         if (int rc = run_query(b, in, step, d_hits ? d_hits + r0 * cols : nullptr, d_nk ? d_nk + r0 : nullptr,
                                tot_host ? b->totals.as<uint64_t>() + i * pcols : nullptr, b->stream))
             return rc;
         if (hits_host) {
             if (hit_bytes != 4)
                 HIPCHK(launch_narrow_hits(d_hits + r0 * cols, b->narrow.as<uint8_t>() + r0 * cols * hit_bytes,
-                                          (r1 - r0) * cols, hit_bytes, b->stream));
+                                          (r1 - r0) * cols, hit_bytes, b->stream, b->ovf.as<uint32_t>()));
             HIPCHK(hipEventRecord(b->chunk_ev[i], b->stream));
             if (i > 0)
                 if (int rc = drain(i - 1)) return rc;
@@ -822,6 +841,13 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     }
     HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
     if (hits_host) HIPCHK(hipStreamSynchronize(b->d2h_stream));
+    if (narrowing) {  // a count wider than hit_bytes (device reads: the caller's max_len understated)
+        uint32_t over = 0;
+        HIPCHK(hipMemcpyAsync(&over, b->ovf.p, sizeof(over), hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        if (over) return fail(XS_ERR_ARG, "a hit count does not fit %d byte(s): max_len is below the longest read",
+                              hit_bytes);
+    }
     return XS_OK;
 }
 

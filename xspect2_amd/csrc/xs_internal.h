@@ -201,7 +201,8 @@ hipError_t launch_best_doc(const uint32_t* hits, uint64_t n, uint64_t D, uint32_
                            uint32_t* best_hits, hipStream_t s);
 
 // dst[i] = src[i] as uint8 (hit_bytes 1) or uint16 (2); the caller guarantees the values fit.
-hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s);
+hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s,
+                              uint32_t* overflow = nullptr);
 
 hipError_t launch_gather_reads(const uint8_t* seqs, const uint64_t* offs, const uint32_t* index, uint64_t m,
                                uint8_t* out, const uint64_t* out_offs, hipStream_t s);

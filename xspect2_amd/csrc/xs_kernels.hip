@@ -304,24 +304,35 @@ __global__ void mlst_first_score_kernel(const uint32_t* __restrict__ hits,
 // bytes and of the host memory the caller has to touch.  Four counts per
 // thread: one 16-B load, one 4- or 8-B store.
 template <class T>
-__global__ void narrow_hits_kernel(const uint32_t* __restrict__ src, T* __restrict__ dst, uint64_t n) {
+__global__ void narrow_hits_kernel(const uint32_t* __restrict__ src, T* __restrict__ dst, uint64_t n,
+                                   uint32_t* __restrict__ overflow) {
+    constexpr int kBits = 8 * sizeof(T);
     const uint64_t n4 = n / 4;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t t0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
     const bool vec = reinterpret_cast<uintptr_t>(src) % 16 == 0 && reinterpret_cast<uintptr_t>(dst) % (4 * sizeof(T)) == 0;
+    uint32_t over = 0;  // any count that does not fit T (the caller's max_len was too small)
     if (vec) {
         for (uint64_t i = t0; i < n4; i += stride) {
             const uint4 v = reinterpret_cast<const uint4*>(src)[i];
+            over |= (v.x | v.y | v.z | v.w) >> kBits;
             if constexpr (sizeof(T) == 1) {
                 reinterpret_cast<uint32_t*>(dst)[i] = v.x | (v.y << 8) | (v.z << 16) | (v.w << 24);
             } else {
                 reinterpret_cast<uint2*>(dst)[i] = make_uint2(v.x | (v.y << 16), v.z | (v.w << 16));
             }
         }
-        for (uint64_t i = n4 * 4 + t0; i < n; i += stride) dst[i] = (T)src[i];
+        for (uint64_t i = n4 * 4 + t0; i < n; i += stride) {
+            over |= src[i] >> kBits;
+            dst[i] = (T)src[i];
+        }
     } else {
-        for (uint64_t i = t0; i < n; i += stride) dst[i] = (T)src[i];
+        for (uint64_t i = t0; i < n; i += stride) {
+            over |= src[i] >> kBits;
+            dst[i] = (T)src[i];
+        }
     }
+    if (over && overflow) overflow[0] = 1u;  // divergent: a vector store
 }
 
 // ------------------------------------------------------------------ per-read best doc
@@ -527,11 +538,12 @@ hipError_t launch_mlst_sum(const uint32_t* hits, const uint32_t* seq_of_chunk, u
     return hipGetLastError();
 }
 
-hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s) {
+hipError_t launch_narrow_hits(const uint32_t* src, void* dst, uint64_t n, int hit_bytes, hipStream_t s,
+                              uint32_t* overflow) {
     if (n == 0) return hipSuccess;
     const unsigned g = grid_for((n + 3) / 4, 256, 8192);
-    if (hit_bytes == 1) narrow_hits_kernel<uint8_t><<<g, 256, 0, s>>>(src, static_cast<uint8_t*>(dst), n);
-    else narrow_hits_kernel<uint16_t><<<g, 256, 0, s>>>(src, static_cast<uint16_t*>(dst), n);
+    if (hit_bytes == 1) narrow_hits_kernel<uint8_t><<<g, 256, 0, s>>>(src, static_cast<uint8_t*>(dst), n, overflow);
+    else narrow_hits_kernel<uint16_t><<<g, 256, 0, s>>>(src, static_cast<uint16_t*>(dst), n, overflow);
     return hipGetLastError();
 }
 
