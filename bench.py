@@ -126,8 +126,8 @@ def launch_ranks(n: int, cmd: list[str], timeout: float, env: dict | None = None
     Each child gets RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE,
     MASTER_ADDR=127.0.0.1 and a free MASTER_PORT, as torchrun would set them.
     The parent touches no GPU and never execs: it starts the children, copies
-    rank 0's stdout to its own (the one JSON line), lets every rank's stderr
-    through, and waits.  If a child fails, or the whole run outlives
+    rank 0's JSON line to its stdout (rank 0's other stdout lines go to
+    stderr), lets every rank's stderr through, and waits.  If a child fails, or the whole run outlives
     `timeout`, the remaining children are killed and the parent returns
     non-zero (the first failing child's code, 124 on timeout)."""
     import subprocess
@@ -147,9 +147,12 @@ def launch_ranks(n: int, cmd: list[str], timeout: float, env: dict | None = None
         raise
 
     def forward(stream):
+        # the JSON line to stdout; anything else rank 0 prints there (gloo's
+        # connection notes, for one) to stderr, so stdout stays one line
         for line in iter(stream.readline, b""):
-            sys.stdout.buffer.write(line)
-            sys.stdout.flush()
+            out = sys.stdout if line.lstrip().startswith(b"{") else sys.stderr
+            out.buffer.write(line)
+            out.flush()
 
     fwd = threading.Thread(target=forward, args=(procs[0].stdout,), daemon=True)
     fwd.start()

@@ -30,6 +30,7 @@ RANK_SCRIPT = textwrap.dedent("""
     r = int(os.environ["RANK"])
     env = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE",
                                           "MASTER_ADDR", "MASTER_PORT")}
+    print("[Gloo] Rank", r, "is connected", flush=True)  # a backend's note on stdout: not the line
     print(json.dumps(env), flush=True)          # every rank prints; only rank 0's may reach the parent
     print("rank", r, "stderr", file=sys.stderr, flush=True)
     if mode == "fail" and r == 1:
@@ -71,6 +72,7 @@ def test_every_rank_gets_its_environment_and_only_rank0_prints(tmp_path, rank_sc
     assert env["MASTER_ADDR"] == "127.0.0.1" and 0 < int(env["MASTER_PORT"]) < 65536
     for r in range(4):  # every rank ran (stderr passes through)
         assert f"rank {r} stderr" in p.stderr
+    assert "[Gloo] Rank 0 is connected" in p.stderr  # rank 0's other stdout lines go to stderr
 
 
 def test_a_failing_rank_stops_the_job_with_its_code(tmp_path, rank_script):

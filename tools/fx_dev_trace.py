@@ -72,6 +72,8 @@ def main():
                 for mode, kw in (("device", {"device": 0}), ("host", {})):
                     time.sleep(0.3)  # the box's CPU share (cgroup quota) refills between legs
                     t = time.perf_counter()
+                    if mode == "device":
+                        print(f"  leg {name} t={time.monotonic() * 1e3:.2f}", file=sys.stderr, flush=True)
                     for b in read_batches(p, mb, **kw):
                         q0 = time.monotonic() * 1e3
                         legs[name](b if mode == "device" else b.packed)

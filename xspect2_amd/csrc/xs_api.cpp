@@ -557,7 +557,9 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
             b->bloom_pending = false;
         }
     }
-    if (b->profiling) {
+    // probe events: at most kPassMarksMax queries between two xs_bank_probe_stats
+    const bool timed = b->profiling && b->events_used < kPassMarksMax;
+    if (timed) {
         if (b->events_used == b->events.size()) {
             hipEvent_t a, c;
             HIPCHK(hipEventCreate(&a));
@@ -602,7 +604,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         }
     }
     b->last_path = path;
-    if (b->profiling) {
+    if (timed) {
         HIPCHK(hipEventRecord(b->events[b->events_used].second, s));
         ++b->events_used;
     }
@@ -1587,6 +1589,10 @@ int xs_bank_set_profiling(xs_bank* b, int on) {
         if (int rc = b->rows_read.ensure(sizeof(uint64_t))) return rc;
         HIPCHK(hipMemsetAsync(b->rows_read.p, 0, sizeof(uint64_t), b->stream));
         HIPCHK(hipStreamSynchronize(b->stream));
+    }
+    if (on != 0 && !b->profiling) {  // a fresh profiling session: no marks left from an earlier one
+        b->pass_used = 0;
+        b->events_used = 0;
     }
     b->profiling = on != 0;
     return XS_OK;

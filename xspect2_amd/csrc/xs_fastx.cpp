@@ -742,8 +742,11 @@ void start_prefetch(xs_fastx* r, size_t lo, size_t hi, int ts) {
     d.next_text = ts ^ 1;
     d.worker = std::thread([r, lo, hi, ts] {
         DevSide& dd = *r->dev;
+        const double t0 = fx_ms();
         dd.pf_rc = load_text(r, lo, hi, ts);
         if (dd.pf_rc) dd.pf_err = xs_last_error();
+        if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f prefetch %zu+%zu done in %.2f ms\n", fx_ms(), lo, hi - lo,
+                                fx_ms() - t0);
     });
 }
 
@@ -1063,6 +1066,7 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
     memset(out, 0, sizeof(*out));
     DevSide& d = *r->dev;
     FXCHK(hipSetDevice(d.device));
+    if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f next_device\n", fx_ms());
     const int slot = d.flip;
     d.flip ^= 1;
     if (r->format == XS_FASTX_FASTQ && r->wrapped) {  // records cannot be cut by pattern: host parser
@@ -1125,6 +1129,7 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
             r->records += out->n;
             out->text_offset = r->cur;
             out->text_bytes = r->stop;
+            if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f return n=%llu\n", fx_ms(), (unsigned long long)out->n);
             return XS_OK;
         }
         memset(out, 0, sizeof(*out));  // no record in this window (text before the first one)

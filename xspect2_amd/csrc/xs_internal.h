@@ -88,11 +88,15 @@ hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t*
 // at each pass boundary, tagged with the pass that just ended (kPassStart opens
 // a query).  xs_bank_pass_stats sums the gaps per pass.
 enum PassTag { kPassStart = -1, kPassPrep = 0, kPassBucket = 1, kPassLookup = 2, kPassResolve = 3, kPassTags = 4 };
+// Marks past kPassMarksMax since the last xs_bank_pass_stats are dropped, so
+// a profiling run that never reads its stats does not grow the pool forever.
+constexpr size_t kPassMarksMax = 1u << 16;
 struct PassRecorder {
     std::vector<hipEvent_t>* pool;
     std::vector<int>* tags;
     size_t* used;
     hipError_t mark(int tag, hipStream_t s) {
+        if (*used >= kPassMarksMax) return hipSuccess;
         if (*used == pool->size()) {
             hipEvent_t e;
             hipError_t err = hipEventCreate(&e);
