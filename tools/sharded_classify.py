@@ -39,7 +39,7 @@ GENERA = ["Acinetobacter", "Pseudomonas", "Klebsiella", "Escherichia", "Salmonel
           "Staphylococcus", "Streptococcus"]
 
 
-def setup(root: Path, n_reads: int) -> None:
+def setup(root: Path, n_reads: int, dup: bool = False) -> None:
     from xspect2_amd.probabilistic_filter_svm_model import ProbabilisticFilterSVMModel
     from xspect2_amd.synth import make_genomes, make_reads
     from xspect2_amd.file_io import Record, write_fasta
@@ -61,7 +61,8 @@ def setup(root: Path, n_reads: int) -> None:
     with open(root / "reads.fq", "w") as fh:
         for i in range(n_reads):
             s = reads[i].tobytes().decode()
-            fh.write(f"@read_{i} synthetic\n{s}\n+\n{'I' * len(s)}\n")
+            rid = i % (n_reads // 2) if dup else i  # dup: read i and i + n/2 share an id (different shards)
+            fh.write(f"@read_{rid} synthetic\n{s}\n+\n{'I' * len(s)}\n")
 
 
 def docs_setup(root: Path, n_reads: int, world: int) -> None:
@@ -95,13 +96,14 @@ def main() -> int:
     ap.add_argument("--reads", type=int, default=200_000)
     ap.add_argument("--world", type=int, default=2)
     ap.add_argument("--step", type=int, default=1)
+    ap.add_argument("--dup", action="store_true", help="setup: every read id occurs twice, n/2 records apart")
     a = ap.parse_args()
     root = Path(a.root).resolve()
     root.mkdir(parents=True, exist_ok=True)
     os.environ["XSPECT_DATA"] = str(root / "xspect-data")
     t0 = time.time()
     if a.cmd == "setup":
-        setup(root, a.reads)
+        setup(root, a.reads, a.dup)
     elif a.cmd == "single":
         from xspect2_amd import classify
         classify.classify_species(GENUS, root / "reads.fq", root / "single.json", step=a.step)
