@@ -133,6 +133,8 @@ def test_classify_species_sharded_equals_single_process(tmp_path, world, n_reads
         got = distributed.merge_result_shards(shards)
         assert got == want
         assert list(got["hits"]) == list(want["hits"])
+        distributed.merge_result_files(shards, tmp_path / f"merged{i}.json")
+        assert (tmp_path / f"merged{i}.json").read_bytes() == (tmp_path / f"single{i}.json").read_bytes()
         if svm:
             assert got["prediction"] == want["prediction"]
         per_shard = [len(json.loads(p.read_text())["hits"]) for p in shards]
@@ -185,6 +187,8 @@ def test_repeated_ids_across_shards_follow_the_reference_dict(tmp_path, world, i
     assert list(got["hits"]) == list(want["hits"])
     assert got["prediction"] == want["prediction"]
     assert sum(len(json.loads(p.read_text())["hits"]) for p in shards) == len(want["hits"])
+    distributed.merge_result_files(shards, tmp_path / "merged.json")
+    assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "single.json").read_bytes()
 
 
 @pytest.mark.timeout(180)
@@ -325,5 +329,7 @@ def test_predict_docs_sharded_multigenus(tmp_path, world, dup):
     assert got == w
     assert list(got["hits"]) == list(w["hits"])
     assert sum(len(d["hits"]) for d in per_shard) == len(w["hits"])  # each read in exactly one shard
+    distributed.merge_result_files(shards, tmp_path / "merged.json")
+    assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "want.json").read_bytes()
     if not dup:
         assert min(len(d["hits"]) for d in per_shard) > 0

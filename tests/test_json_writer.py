@@ -166,6 +166,9 @@ def test_sharded_results_stitch_to_the_whole(tmp_path, cut):
         json.loads((tmp_path / f"s{p}.json").read_text())  # every shard is valid JSON
         paths.append(tmp_path / f"s{p}.json")
     assert merge_result_shards(paths) == json.loads((tmp_path / "whole.json").read_text())
+    from xspect2_amd.distributed import merge_result_files
+    merge_result_files(paths, tmp_path / "merged.json")  # streamed, no parsing: the same bytes
+    assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "whole.json").read_bytes()
 
 
 def test_empty_shard_on_the_dict_path_saves_the_job_total(tmp_path):

@@ -494,6 +494,84 @@ def merge_result_shards(paths) -> dict:
     return out
 
 
+def _json_members(buf, key: bytes, next_key: bytes) -> tuple[int, int]:
+    """Byte range of the members inside the top-level object `key` of a
+    result file (ModelResult.save layout, indent 4), empty for ``{}``."""
+    a = buf.find(b'\n    "' + key + b'": ')
+    b = buf.find(b',\n    "' + next_key + b'": ', a)
+    if a < 0 or b < 0:
+        raise ValueError(f"not a result file: no {key.decode()!r} section")
+    a += len(key) + 9
+    if buf[a:b] == b"{}":
+        return a, a
+    return a + 2, b - 6  # inside "{\n" ... "\n    }"
+
+
+def merge_result_files(paths, out_path: Path) -> None:
+    """Stream the JSON shards of a sharded job (in part order) into the
+    single-process JSON file, byte for byte, without parsing them: each
+    read's sections are already in its shard in the reference's dict order
+    (``resolve_cross_shard_duplicates`` leaves every id in the shard of its
+    first record), so the merged file is the shards' per-read members
+    concatenated, with the job's "total", prediction and fields of the first
+    shard (all shards carry the same).  Memory stays bounded by the mapped
+    files; for the dict form use ``merge_result_shards``."""
+    import mmap
+    files, maps = [], []
+    try:
+        for p in paths:
+            fh = open(p, "rb")
+            files.append(fh)
+            maps.append(mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ) if Path(p).stat().st_size else b"")
+        parts = []
+        for m in maps:
+            h = _json_members(m, b"hits", b"scores")
+            s = _json_members(m, b"scores", b"num_kmers")
+            n = _json_members(m, b"num_kmers", b"misclassified")
+            t = m.rfind(b'\n        "total": ', s[0] - 1, s[1])
+            total = (t + 1, s[1])
+            before = (s[0], t - 1) if t > s[0] else (s[0], s[0])  # members before "total" (no trailing ",")
+            parts.append((h, before, total, n))
+        m0, (h0, _, total0, _) = maps[0], parts[0]
+
+        def members(out, which):
+            first = True
+            for m, pr in zip(maps, parts):
+                a, b = pr[which]
+                if b > a:
+                    out.write(b"" if first else b",\n")
+                    out.write(m[a:b])
+                    first = False
+            return not first
+
+        with open(out_path, "wb") as out:
+            out.write(m0[:h0[0] - (2 if h0[1] > h0[0] else 0)])  # up to `"hits": `
+            if any(pr[0][1] > pr[0][0] for pr in parts):
+                out.write(b"{\n")
+                members(out, 0)
+                out.write(b"\n    }")
+            else:
+                out.write(b"{}")
+            out.write(b',\n    "scores": {\n')
+            if members(out, 1):
+                out.write(b",\n")
+            out.write(m0[total0[0]:total0[1]])
+            out.write(b'\n    },\n    "num_kmers": ')
+            if any(pr[3][1] > pr[3][0] for pr in parts):
+                out.write(b"{\n")
+                members(out, 3)
+                out.write(b"\n    }")
+            else:
+                out.write(b"{}")
+            out.write(m0[m0.find(b',\n    "misclassified": '):])
+    finally:
+        for m in maps:
+            if isinstance(m, mmap.mmap):
+                m.close()
+        for fh in files:
+            fh.close()
+
+
 # ---------------------------------------------------------------- config 5: docs-sharded classify
 def predict_docs_sharded(model, input_file: Path, step: int = 1, display_name: bool = False):
     """Config 5 (docs sharded): every rank holds a different species model (one
