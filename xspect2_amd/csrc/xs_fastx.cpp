@@ -486,17 +486,52 @@ struct DevSide {
                         &id_ofs, &desc_ofs, &ids_d, &descs_d, &seqs[0], &seqs[1], &offs[0], &offs[1]})
             b->device = dev;
     }
-    ~DevSide() {
-        if (worker.joinable()) worker.join();
-        (void)hipSetDevice(device);
-        if (stream) (void)hipStreamSynchronize(stream);
-        if (copy) (void)hipStreamSynchronize(copy);
-        for (hipEvent_t e : text_ev)
-            if (e) (void)hipEventDestroy(e);
-        if (stream) (void)hipStreamDestroy(stream);
-        if (copy) (void)hipStreamDestroy(copy);
-    }
+    ~DevSide();
 };
+
+// The streams and events of closed device readers, kept for the next reader
+// on the same device: creating them costs about a millisecond per open,
+// as much as parsing the first window.
+struct StreamSet {
+    int device;
+    hipStream_t stream, copy;
+    hipEvent_t ev[2];
+};
+std::mutex g_ss_mu;
+std::vector<StreamSet> g_ss;
+constexpr size_t kStreamSetsKept = 16;
+
+bool take_streams(DevSide& d) {
+    std::lock_guard<std::mutex> g(g_ss_mu);
+    for (size_t i = 0; i < g_ss.size(); ++i) {
+        if (g_ss[i].device != d.device) continue;
+        d.stream = g_ss[i].stream;
+        d.copy = g_ss[i].copy;
+        d.text_ev[0] = g_ss[i].ev[0];
+        d.text_ev[1] = g_ss[i].ev[1];
+        g_ss.erase(g_ss.begin() + (long)i);
+        return true;
+    }
+    return false;
+}
+
+DevSide::~DevSide() {
+    if (worker.joinable()) worker.join();
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    if (copy) (void)hipStreamSynchronize(copy);
+    if (stream && copy && text_ev[0] && text_ev[1]) {
+        std::lock_guard<std::mutex> g(g_ss_mu);
+        if (g_ss.size() < kStreamSetsKept) {
+            g_ss.push_back(StreamSet{device, stream, copy, {text_ev[0], text_ev[1]}});
+            return;
+        }
+    }
+    for (hipEvent_t e : text_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+    if (copy) (void)hipStreamDestroy(copy);
+}
 
 }  // namespace
 
@@ -1047,6 +1082,7 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
         return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
     };
     hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess && take_streams(*r->dev)) return XS_OK;
     // The parse kernels are short and sit between the caller's probes of the
     // previous batch: a high-priority stream lets their workgroups in as soon
     // as the probe frees a slot, instead of after the whole probe.

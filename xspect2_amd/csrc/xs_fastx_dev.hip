@@ -47,6 +47,26 @@ __device__ __forceinline__ uint32_t fx_rstrip(const uint8_t* t, uint32_t b, uint
 
 __device__ __forceinline__ uint32_t line_start(const uint32_t* nl, uint64_t j) { return j ? nl[j - 1] + 1 : 0; }
 
+// Bit 7 of each byte of w set where that byte equals c (exact: no carries cross bytes).
+__device__ __forceinline__ uint32_t eq_bits(uint32_t w, uint32_t c) {
+    const uint32_t x = w ^ (c * 0x01010101u);
+    return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+}
+
+// No ' ' or '\t' in t[b, e): aligned dword loads (the text is 16-B aligned and
+// zero-padded past the window), bytes outside [b, e) masked off.
+__device__ __forceinline__ bool no_space_tab(const uint8_t* t, uint32_t b, uint32_t e) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(t);
+    for (uint32_t p = b & ~3u; p < e; p += 4) {
+        const uint32_t x = w[p >> 2];
+        uint32_t keep = 0xffffffffu;
+        if (p < b) keep <<= 8 * (b - p);
+        if (e - p < 4) keep &= (1u << (8 * (e - p))) - 1u;
+        if ((eq_bits(x, ' ') | eq_bits(x, '\t')) & keep) return false;
+    }
+    return true;
+}
+
 // First whitespace-separated token of [b, e): its start and length.
 __device__ __forceinline__ void first_token(const uint8_t* t, uint32_t b, uint32_t e, uint32_t* s, uint64_t* len) {
     while (b < e && fx_ws(t[b])) ++b;
@@ -118,7 +138,7 @@ __global__ void __launch_bounds__(256) fq_records_kernel(const uint8_t* __restri
         // one sequence line, not empty, not itself a '+' line
         const uint32_t se = fx_rstrip(t, s1, e1);
         ok = ok && se > s1 && t[s1] != '+';
-        for (uint32_t p = s1; ok && p < se; ++p) ok = t[p] != ' ' && t[p] != '\t';
+        ok = ok && no_space_tab(t, s1, se);
         ok = ok && e2 > s2 && t[s2] == '+';
         if (ok) {  // a caption, if any, repeats the title
             const uint32_t cb = s2 + 1, ce = fx_rstrip(t, cb, e2);
