@@ -266,7 +266,7 @@ def test_multigenus_docs_sharded_over_100_docs(tmp_path, world):
         assert np.array_equal(o["step2"], want2)
 
 
-def _docs_worker(rank: int, world: int, port: int, tmp: str, dup: bool = False):
+def _docs_worker(rank: int, world: int, port: int, tmp: str, dup: bool = False, catch: bool = False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -281,7 +281,13 @@ def _docs_worker(rank: int, world: int, port: int, tmp: str, dup: bool = False):
         m = ProbabilisticFilterModel(K, f"Genus{rank}", None, None, "Species", Path(tmp) / "m")
         names = [f"g{rank}_sp{d}" for d in range(banks[rank].D)]
         m.index = OracleIndex(banks[rank], names)
-        distributed.classify_docs_sharded(m, Path(tmp) / "reads.fasta", Path(tmp) / "out" / "docs.json")
+        try:
+            distributed.classify_docs_sharded(m, Path(tmp) / "reads.fasta", Path(tmp) / "out" / "docs.json")
+            (Path(tmp) / f"rank{rank}.txt").write_text("ok")
+        except Exception as e:  # noqa: BLE001
+            if not catch:
+                raise
+            (Path(tmp) / f"rank{rank}.txt").write_text(f"{type(e).__name__}: {e}")
     finally:
         dist.destroy_process_group()
 
@@ -333,3 +339,23 @@ def test_predict_docs_sharded_multigenus(tmp_path, world, dup):
     assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "want.json").read_bytes()
     if not dup:
         assert min(len(d["hits"]) for d in per_shard) > 0
+
+
+@pytest.mark.timeout(180)
+def test_docs_sharded_error_on_one_rank_raises_on_every_rank(tmp_path):
+    """Config 5: only the last rank's byte range holds a read no longer than
+    k; every rank raises the reference's ValueError (a rank that
+    raised alone left the others in the batch collectives)."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+
+    world = 3
+    banks, reads = _genera(oracle, world)
+    reads = reads + [reads[-1][:K]]  # the last record: len == k
+    with open(tmp_path / "reads.fasta", "wb") as fh:
+        for i, r in enumerate(reads):
+            fh.write(b">r%d\n%s\n" % (i, r))
+    mp.spawn(_docs_worker, args=(world, _free_port(), str(tmp_path), False, True), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"rank{r}.txt").read_text() == "ValueError: Invalid sequence, must be longer than k"
