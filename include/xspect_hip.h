@@ -362,6 +362,9 @@ typedef struct xs_fastx_dbatch {
     uint64_t text_offset;        /* file offset parsed up to */
     uint64_t text_bytes;         /* end offset of the reader's text */
     int parsed_on_device;        /* 0: this window went through the host parser */
+    void* host_ready;            /* the host arrays (host_offsets, ids, descs and their offsets) are
+                                    complete once this event has; NULL: already complete.
+                                    Wait with xs_fastx_wait_host before reading them */
 } xs_fastx_dbatch;
 
 /* As xs_fastx_open_range, for xs_fastx_next_device on `device`. */
@@ -370,6 +373,10 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
 /* Next batch, complete on the device when this returns.  Buffers stay valid
  * until the SECOND following call.  Errors as xs_fastx_next. */
 int xs_fastx_next_device(xs_fastx* reader, uint64_t max_text_bytes, xs_fastx_dbatch* out);
+/* Block until a device batch's host arrays have landed (their D2H copies run
+ * behind the caller's probe of the batch, whose device data is complete when
+ * xs_fastx_next_device returns). */
+int xs_fastx_wait_host(const xs_fastx_dbatch* batch);
 
 /* Write records as Bio.SeqIO.write(record, fh, "fasta") does (the genus
  * filter's output, src/xspect/file_io.py:166-191): ">" title, then the

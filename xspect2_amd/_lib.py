@@ -89,6 +89,7 @@ class FastxDBatch(ctypes.Structure):
         ("text_offset", ctypes.c_uint64),
         ("text_bytes", ctypes.c_uint64),
         ("parsed_on_device", ctypes.c_int),
+        ("host_ready", ctypes.c_void_p),
     ]
 
 
@@ -149,6 +150,7 @@ SIGNATURES = {
     "xs_fastx_close": (None, [_vp]),
     "xs_fastx_open_device": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
     "xs_fastx_next_device": (_int, [_vp, _u64, ctypes.POINTER(FastxDBatch)]),
+    "xs_fastx_wait_host": (_int, [ctypes.POINTER(FastxDBatch)]),
     "xs_write_fasta": (_int, [ctypes.c_char_p, _int, _vp, _vp, ctypes.c_char_p, _vp, _vp, _u64, _u32]),
 }
 

@@ -461,6 +461,8 @@ struct DevSide {
     // Window text in two slots: the next window loads into one while the
     // current one is parsed from the other.
     hipEvent_t text_ev[2] = {nullptr, nullptr};
+    hipEvent_t kern_ev = nullptr;                // a batch's device data complete
+    hipEvent_t host_ev[2] = {nullptr, nullptr};  // slot s's host arrays complete
     PinBuf pin[2];      // a window's text
     PinBuf status;      // small D2H results
     DBuf text[2];       // a window's text, zero-padded to whole tiles
@@ -495,7 +497,7 @@ struct DevSide {
 struct StreamSet {
     int device;
     hipStream_t stream, copy;
-    hipEvent_t ev[2];
+    hipEvent_t ev[5];  // text_ev[2], kern_ev, host_ev[2]
 };
 std::mutex g_ss_mu;
 std::vector<StreamSet> g_ss;
@@ -509,6 +511,9 @@ bool take_streams(DevSide& d) {
         d.copy = g_ss[i].copy;
         d.text_ev[0] = g_ss[i].ev[0];
         d.text_ev[1] = g_ss[i].ev[1];
+        d.kern_ev = g_ss[i].ev[2];
+        d.host_ev[0] = g_ss[i].ev[3];
+        d.host_ev[1] = g_ss[i].ev[4];
         g_ss.erase(g_ss.begin() + (long)i);
         return true;
     }
@@ -520,15 +525,18 @@ DevSide::~DevSide() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy) (void)hipStreamSynchronize(copy);
-    if (stream && copy && text_ev[0] && text_ev[1]) {
+    hipEvent_t* evs[5] = {&text_ev[0], &text_ev[1], &kern_ev, &host_ev[0], &host_ev[1]};
+    bool all = stream && copy;
+    for (hipEvent_t* e : evs) all = all && *e;
+    if (all) {
         std::lock_guard<std::mutex> g(g_ss_mu);
         if (g_ss.size() < kStreamSetsKept) {
-            g_ss.push_back(StreamSet{device, stream, copy, {text_ev[0], text_ev[1]}});
+            g_ss.push_back(StreamSet{device, stream, copy, {text_ev[0], text_ev[1], kern_ev, host_ev[0], host_ev[1]}});
             return;
         }
     }
-    for (hipEvent_t e : text_ev)
-        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t* e : evs)
+        if (*e) (void)hipEventDestroy(*e);
     if (stream) (void)hipStreamDestroy(stream);
     if (copy) (void)hipStreamDestroy(copy);
 }
@@ -915,13 +923,17 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     FXCHK(xs::launch_fx_copy(text, d.id_src.as<uint32_t>(), d.id_ofs.as<uint64_t>(), n, d.ids_d.as<uint8_t>(), s));
     FXCHK(xs::launch_fx_copy(text, d.desc_src.as<uint32_t>(), d.desc_ofs.as<uint64_t>(), n,
                              d.descs_d.as<uint8_t>(), s));
+    FXCHK(hipEventRecord(d.kern_ev, s));  // the batch's device data: what the caller probes
+    // the host arrays land behind the caller's probe; xs_fastx_wait_host waits for them
     if (ibytes) FXCHK(hipMemcpyAsync(d.ids[slot].p, d.ids_d.p, ibytes, hipMemcpyDeviceToHost, s));
     if (dbytes) FXCHK(hipMemcpyAsync(d.descs[slot].p, d.descs_d.p, dbytes, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(d.id_offs[slot].p, d.id_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(d.desc_offs[slot].p, d.desc_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(d.hoffs[slot].p, offs, (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    FXCHK(hipStreamSynchronize(s));
+    FXCHK(hipEventRecord(d.host_ev[slot], s));
+    FXCHK(hipEventSynchronize(d.kern_ev));
     g_fx.copy = fx_ms() - t2;
+    out->host_ready = d.host_ev[slot];
     *ok = true;
     out->n = n;
     out->seq_bytes = sbytes;
@@ -1090,9 +1102,16 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
-    for (hipEvent_t& ev : r->dev->text_ev)
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    for (hipEvent_t* ev : {&r->dev->text_ev[0], &r->dev->text_ev[1], &r->dev->kern_ev, &r->dev->host_ev[0],
+                           &r->dev->host_ev[1]})
+        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) return fail(e);
+    return XS_OK;
+}
+
+int xs_fastx_wait_host(const xs_fastx_dbatch* b) {
+    if (!b) return xs::set_error(XS_ERR_ARG, "null argument");
+    if (b->host_ready) FXCHK(hipEventSynchronize(static_cast<hipEvent_t>(b->host_ready)));
     return XS_OK;
 }
 

@@ -152,6 +152,8 @@ class DeviceSeqBatch:
         self.text_offset = int(fb.text_offset)
         self.text_bytes = int(fb.text_bytes)
         self._host = (fb.host_offsets, fb.ids, fb.id_offsets, fb.descs, fb.desc_offsets)
+        self._fb = fb  # host_ready: the host arrays land behind the caller's probe of the batch
+        self._host_waited = not fb.host_ready
         self._offsets = self._ids_raw = self._descs_raw = None
 
     def check_valid(self) -> None:
@@ -160,7 +162,14 @@ class DeviceSeqBatch:
             raise RuntimeError("device batch is no longer valid: its reader was closed or has read two batches "
                                "since (the device buffers are freed or reused)")
 
+    def _wait_host(self) -> None:
+        """Block until the batch's host arrays (offsets, ids, titles) have landed."""
+        if not self._host_waited:
+            check(load().xs_fastx_wait_host(ctypes.byref(self._fb)))
+            self._host_waited = True
+
     def _u64(self, ptr) -> np.ndarray:
+        self._wait_host()
         return np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ctypes.c_uint64)), (self.n + 1,)).copy()
 
     @property
@@ -174,6 +183,7 @@ class DeviceSeqBatch:
         self.check_valid()
         if not self.n:
             return b"", np.zeros(1, dtype=np.uint64)
+        self._wait_host()
         o = self._u64(self._host[which + 1])
         return (ctypes.string_at(self._host[which], int(o[-1])) if o[-1] else b""), o
 

@@ -230,10 +230,13 @@ class ProbabilisticFilterModel:
         lens, hits, nks = [], [], []
         dev = file_reader_device(self.index)
         for batch in read_batches(path, part=part, parts=parts, device=dev):
+            # probe first: a device batch's host arrays (offsets, ids) land
+            # behind the probe; a read no longer than k has no k-mers there, and
+            # the batch raises below exactly as it would have before the probe
+            h, n = self._query(batch if dev is not None else batch.packed, step)
             L = batch.lengths()
             if (L <= self.k).any():
                 raise ValueError("Invalid sequence, must be longer than k")
-            h, n = self._query(batch if dev is not None else batch.packed, step)
             ids.append(batch.ids_packed())  # the reader's id buffer: no string per read
             lens.append(L)
             hits.append(h)
