@@ -25,6 +25,11 @@ def ms():
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="seq,gen,gen_sw")
+    ap.add_argument("--reps", type=int, default=4)
+    args = ap.parse_args()
     import torch
     from fx_dev_trace import write_fastq
     from xspect2_amd import file_io
@@ -44,8 +49,8 @@ def main():
     torch.cuda.synchronize(dev)
     del g
     out = {}
-    for rep in range(4):
-        for mode in ("seq", "gen", "gen_sw"):
+    for rep in range(args.reps):
+        for mode in args.modes.split(","):
             sys.setswitchinterval(1e-4 if mode == "gen_sw" else 0.005)
             time.sleep(0.3)
             t0 = ms()

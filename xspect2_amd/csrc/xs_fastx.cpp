@@ -571,11 +571,20 @@ namespace {
 // bytes of text (for budgets of at least 2 * kFirstWindow), so the caller's
 // first probe starts after a small parse while the later, larger windows are
 // read behind it.
-constexpr size_t kFirstWindow = 32u << 20;
+// XSPECT2_AMD_FX_FIRST_MB sets the first window (MiB, read once; default 32).
+size_t first_window() {
+    static const size_t w = [] {
+        const char* e = getenv("XSPECT2_AMD_FX_FIRST_MB");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? (size_t)v << 20 : (size_t)32 << 20;
+    }();
+    return w;
+}
 size_t window_budget(uint64_t max_text_bytes, uint64_t k) {
     const size_t b = std::max<uint64_t>(max_text_bytes, 1);
-    if (b < 2 * kFirstWindow || k >= 16) return b;
-    return std::min(b, kFirstWindow << k);
+    const size_t w0 = first_window();
+    if (b < 2 * w0 || k >= 16) return b;
+    return std::min(b, w0 << k);
 }
 
 // End of the window that starts at lo: the first record start at or after
