@@ -17,7 +17,7 @@ t0 = int(last[0]["Start_Timestamp"])
 prev_end = t0
 for r in last:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "")[:60]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
     print(f"{(s - t0) / 1e3:9.1f} us  dur {(e - s) / 1e3:8.1f}  gap {(s - prev_end) / 1e3:8.1f}  {name}")
     prev_end = max(prev_end, e)
 PY

@@ -567,16 +567,18 @@ struct xs_fastx {
 
 namespace {
 
-// Windows ramp up: the reader's k-th window takes at most kFirstWindow << k
-// bytes of text (for budgets of at least 2 * kFirstWindow), so the caller's
+// Windows ramp up: the reader's k-th window takes at most first_window() << k
+// bytes of text (for budgets of at least twice the first), so the caller's
 // first probe starts after a small parse while the later, larger windows are
 // read behind it.
-// XSPECT2_AMD_FX_FIRST_MB sets the first window (MiB, read once; default 32).
+// XSPECT2_AMD_FX_FIRST_MB sets the first window (MiB, read once; default 16:
+// file -> totals of 1 M reads 16.8-16.9 ms against 17.0-17.5 at 32 MiB and
+// 35-48 at 8 MiB, profiles/r04_e2e_first_window.txt).
 size_t first_window() {
     static const size_t w = [] {
         const char* e = getenv("XSPECT2_AMD_FX_FIRST_MB");
         const long v = e ? atol(e) : 0;
-        return v > 0 ? (size_t)v << 20 : (size_t)32 << 20;
+        return v > 0 ? (size_t)v << 20 : (size_t)16 << 20;
     }();
     return w;
 }
