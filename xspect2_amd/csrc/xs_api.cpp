@@ -764,11 +764,13 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     if (int rc = b->partials.ensure((size_t)probe_grid(b) * pcols * 8)) return rc;
     if (tot_host)
         if (int rc = b->totals.ensure(nc * pcols * 8)) return rc;
-    for (int s = 0; s < 2; ++s) {
-        if (int rc = b->hstage[s].ensure(kHostChunk)) return rc;
-        if (!b->hstage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b->hstage_ev[s], hipEventDisableTiming));
+    if (!dev) {  // host reads: the H2D staging ring and its copy stream (device reads need neither)
+        for (int s = 0; s < 2; ++s) {
+            if (int rc = b->hstage[s].ensure(kHostChunk)) return rc;
+            if (!b->hstage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b->hstage_ev[s], hipEventDisableTiming));
+        }
+        if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
     }
-    if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
     if (hits_host && !b->d2h_stream) HIPCHK(hipStreamCreateWithFlags(&b->d2h_stream, hipStreamNonBlocking));
     const bool narrowing = hits_host && hit_bytes != 4;
     if (narrowing) {
@@ -841,7 +843,7 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
             tot_host[c] = v;
         }
     }
-    HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
+    if (!dev) HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
     if (hits_host) HIPCHK(hipStreamSynchronize(b->d2h_stream));
     if (narrowing) {  // a count wider than hit_bytes (device reads: the caller's max_len understated)
         uint32_t over = 0;
