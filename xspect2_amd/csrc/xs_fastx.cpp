@@ -538,7 +538,7 @@ DevSide::~DevSide() {
     for (hipEvent_t* e : evs)
         if (*e) (void)hipEventDestroy(*e);
     if (stream) (void)hipStreamDestroy(stream);
-    if (copy) (void)hipStreamDestroy(copy);
+    if (copy && copy != stream) (void)hipStreamDestroy(copy);
 }
 
 }  // namespace
@@ -1112,7 +1112,14 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
+    // XSPECT2_AMD_FX_ONE_STREAM=1: the text DMA on the parse stream (one
+    // stream fewer: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues)
+    static const bool one_stream = [] {
+        const char* v = getenv("XSPECT2_AMD_FX_ONE_STREAM");
+        return v && v[0] == '1';
+    }();
+    if (one_stream) r->dev->copy = r->dev->stream;
+    else if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
     for (hipEvent_t* ev : {&r->dev->text_ev[0], &r->dev->text_ev[1], &r->dev->kern_ev, &r->dev->host_ev[0],
                            &r->dev->host_ev[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
@@ -1166,14 +1173,20 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
         ++r->windows;
         // the next window's text loads into the other slot while this one is
         // parsed and the caller works on the batch
-        if (r->cur < r->stop) {
-            const char* nlo = r->base + r->cur;
-            const size_t nb = window_budget(max_text_bytes, r->windows);
-            start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, nb) - r->base), ts ^ 1);
-        }
+        auto prefetch_next = [&] {
+            if (r->cur < r->stop) {
+                const char* nlo = r->base + r->cur;
+                const size_t nb = window_budget(max_text_bytes, r->windows);
+                start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, nb) - r->base), ts ^ 1);
+            }
+        };
+        // one stream (XSPECT2_AMD_FX_ONE_STREAM): the next window's DMA queues
+        // behind this window's parse on the same stream, so it starts after it
+        if (d.copy != d.stream) prefetch_next();
         bool ok = false;
         g_fx = FxTimes{};
         if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
+        if (d.copy == d.stream) prefetch_next();
         if (fx_trace())
             fprintf(stderr,
                     "[fastx-device] t=%.2f window %zu+%zu: text %s load %.2f ms, wait %.2f ms | count %.2f records %.2f "
