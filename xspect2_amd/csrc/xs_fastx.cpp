@@ -1111,7 +1111,14 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
     // as the probe frees a slot, instead of after the whole probe.
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
+    // XSPECT2_AMD_FX_PRIORITY=low: the parse stream at the lowest priority
+    // instead (the probe keeps its slots; the parse fills the gaps)
+    static const bool low_prio = [] {
+        const char* v = getenv("XSPECT2_AMD_FX_PRIORITY");
+        return v && v[0] == 'l';
+    }();
+    if (e == hipSuccess)
+        e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, low_prio ? least : greatest);
     // XSPECT2_AMD_FX_ONE_STREAM=1: the text DMA on the parse stream (one
     // stream fewer: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues)
     static const bool one_stream = [] {
