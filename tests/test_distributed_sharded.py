@@ -359,3 +359,44 @@ def test_docs_sharded_error_on_one_rank_raises_on_every_rank(tmp_path):
     mp.spawn(_docs_worker, args=(world, _free_port(), str(tmp_path), False, True), nprocs=world, join=True)
     for r in range(world):
         assert (tmp_path / f"rank{r}.txt").read_text() == "ValueError: Invalid sequence, must be longer than k"
+
+
+def _exchange_worker(rank: int, world: int, port: int, tmp: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(11)
+        dims = [3 + 2 * r for r in range(world)]                 # D_r differ: rows padded to the widest
+        counts = [int(c) for c in rng.integers(0, 40, world)]    # reads per rank (some may be 0)
+        n = sum(counts)
+        out = {}
+        for wire, top in ((torch.uint8, 255), (torch.int16, 32767), (torch.int32, 1 << 30)):
+            # every rank's full columns, from one seed: rank r holds columns of block r
+            full = np.random.default_rng(5).integers(0, top + 1, (n, sum(dims)))
+            c0 = sum(dims[:rank])
+            mine = torch.from_numpy(full[:, c0:c0 + dims[rank]].astype(np.int32))
+            got = distributed.exchange_doc_columns(mine, counts, dims, wire)
+            lo = sum(counts[:rank])
+            out[str(wire)] = (got.to(torch.int64).numpy(), full[lo:lo + counts[rank]])
+        np.savez(Path(tmp) / f"x{rank}.npz", **{k + "_got": v[0] for k, v in out.items()},
+                 **{k + "_want": v[1] for k, v in out.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_exchange_doc_columns_all_widths(tmp_path, world):
+    """exchange_doc_columns over gloo: rank q ends with its reads' rows of
+    every rank's columns, in 1, 2 (float16 bit patterns on the wire) and 4
+    bytes, with ranks of different doc counts and of no reads."""
+    import torch.multiprocessing as mp
+    mp.spawn(_exchange_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        z = np.load(tmp_path / f"x{r}.npz")
+        for k in ("torch.uint8", "torch.int16", "torch.int32"):
+            assert np.array_equal(z[k + "_got"], z[k + "_want"]), (r, k)
