@@ -21,6 +21,7 @@ int set_error(int code, const char* msg) {  // the library's version lives in xs
     return code;
 }
 }  // namespace xs
+extern "C" const char* xs_last_error(void) { return ""; }  // likewise
 
 static std::mt19937_64 rng(12345);
 
@@ -173,7 +174,20 @@ int main() {
                                      nullptr, 1 + trial % 8))
             ++errors;
     }
-    printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices; "
-           "%d clean error returns, %d on well-formed input\n", files, errors, unexpected);
+    // 128-bit id keys (xs_ids_hash128): ids of every length 0..200 packed back
+    // to back in an exactly sized buffer, so a read past an id's end is caught
+    for (int trial = 0; trial < 20; ++trial) {
+        std::vector<uint64_t> off{0};
+        std::string buf;
+        for (int i = 0; i <= 200; ++i) {
+            buf += rand_seq((size_t)((i + trial) % 201), "ACGT_:0123456789");
+            off.push_back(buf.size());
+        }
+        std::vector<char> exact(buf.begin(), buf.end());
+        std::vector<uint64_t> key(2 * (off.size() - 1));
+        if (xs_ids_hash128(exact.data(), off.data(), off.size() - 1, key.data())) ++unexpected;
+    }
+    printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices, "
+           "20 id-key batches; %d clean error returns, %d on well-formed input\n", files, errors, unexpected);
     return unexpected ? 1 : 0;
 }
