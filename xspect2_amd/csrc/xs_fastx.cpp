@@ -470,6 +470,7 @@ struct DevSide {
     DBuf hdr, hofs, line_src, line_len, line_ofs, rec_line, lens, maxlen;
     DBuf seq_src, seq_len, id_src, id_len, desc_src, desc_len, id_ofs, desc_ofs, ids_d, descs_d;
     DBuf seqs[2], offs[2];
+    DBuf fq_blk, fq_blk_ofs, fq_status;  // FASTQ record blocks' sums and offsets, the window's status
     PinBuf ids[2], id_offs[2], descs[2], desc_offs[2], hoffs[2];
     int flip = 0;
     // text of the next window, loaded by `worker` while the caller works
@@ -485,7 +486,8 @@ struct DevSide {
         device = dev;
         for (DBuf* b : {&text[0], &text[1], &tiles, &tile_ofs, &nl, &temp, &flag, &hdr, &hofs, &line_src, &line_len, &line_ofs,
                         &rec_line, &lens, &maxlen, &seq_src, &seq_len, &id_src, &id_len, &desc_src, &desc_len,
-                        &id_ofs, &desc_ofs, &ids_d, &descs_d, &seqs[0], &seqs[1], &offs[0], &offs[1]})
+                        &id_ofs, &desc_ofs, &ids_d, &descs_d, &seqs[0], &seqs[1], &offs[0], &offs[1], &fq_blk,
+                        &fq_blk_ofs, &fq_status})
             b->device = dev;
     }
     ~DevSide();
@@ -899,21 +901,21 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
         FXCHK(hipMemcpyAsync(st + 3, d.id_ofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
         FXCHK(hipMemcpyAsync(st + 4, d.desc_ofs.as<uint64_t>() + L, 8, hipMemcpyDeviceToHost, s));
     } else {
-        const uint64_t n = nmax;
-        FXCHK(xs::launch_fq_records(text, nl, n, runs, d.flag.as<uint32_t>(), s));
-        for (DBuf* b : {&d.seq_len, &d.id_len, &d.desc_len}) FXCHK(hipMemsetAsync(b->as<uint64_t>() + n, 0, 8, s));
-        FXCHK(xs::launch_scan(d.temp.p, tb, d.seq_len.as<uint64_t>(), offs, n + 1, s));
-        FXCHK(xs::launch_scan(d.temp.p, tb, d.id_len.as<uint64_t>(), d.id_ofs.as<uint64_t>(), n + 1, s));
-        FXCHK(xs::launch_scan(d.temp.p, tb, d.desc_len.as<uint64_t>(), d.desc_ofs.as<uint64_t>(), n + 1, s));
-        FXCHK(xs::launch_max_u64(d.temp.p, tb, d.seq_len.as<uint64_t>(), n, d.maxlen.as<uint64_t>(), s));
-        st[1] = n;
-        FXCHK(hipMemcpyAsync(st + 2, offs + n, 8, hipMemcpyDeviceToHost, s));
-        FXCHK(hipMemcpyAsync(st + 3, d.id_ofs.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
-        FXCHK(hipMemcpyAsync(st + 4, d.desc_ofs.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+        // records, their offsets and the window's status in three kernels and one copy back
+        const uint64_t n = nmax, nblk = (n + 255) / 256;
+        if (int rc = d.fq_blk.ensure((nblk + 1) * sizeof(xs::FqBlockSums))) return rc;
+        if (int rc = d.fq_blk_ofs.ensure((nblk + 1) * 3 * 8)) return rc;
+        if (int rc = d.fq_status.ensure(6 * 8)) return rc;
+        FXCHK(xs::launch_fq_records(text, nl, n, runs, d.flag.as<uint32_t>(),
+                                    static_cast<xs::FqBlockSums*>(d.fq_blk.p), d.fq_blk_ofs.as<uint64_t>(), offs,
+                                    d.id_ofs.as<uint64_t>(), d.desc_ofs.as<uint64_t>(), d.fq_status.as<uint64_t>(), s));
+        FXCHK(hipMemcpyAsync(st, d.fq_status.p, 6 * 8, hipMemcpyDeviceToHost, s));
     }
-    st[0] = 0;
-    FXCHK(hipMemcpyAsync(st, d.flag.p, 4, hipMemcpyDeviceToHost, s));
-    FXCHK(hipMemcpyAsync(st + 5, d.maxlen.p, 8, hipMemcpyDeviceToHost, s));
+    if (fasta) {
+        st[0] = 0;
+        FXCHK(hipMemcpyAsync(st, d.flag.p, 4, hipMemcpyDeviceToHost, s));
+        FXCHK(hipMemcpyAsync(st + 5, d.maxlen.p, 8, hipMemcpyDeviceToHost, s));
+    }
     FXCHK(hipStreamSynchronize(s));
     const double t2 = fx_ms();
     g_fx.records = t2 - t1;

@@ -26,6 +26,7 @@ namespace xs {
 namespace {
 
 constexpr int kFxThreads = 256;
+constexpr int kFqBlock = 256;  // FASTQ records per block of the record kernels
 constexpr int kFxRow = kFxThreads * 16;  // bytes per coalesced row of a tile
 static_assert(kFxTile == 4 * kFxRow, "a tile is four rows of 16 B per thread");
 
@@ -123,11 +124,13 @@ __global__ void __launch_bounds__(kFxThreads) fx_positions_kernel(const uint8_t*
 // FASTQ: record r = lines 4r .. 4r+3.  The checks are the host reader's
 // (parse_fastq, xs_fastx.cpp), narrowed to the layouts where four lines are
 // exactly one record; anything else sets *bad and the host parses the window.
-__global__ void __launch_bounds__(256) fq_records_kernel(const uint8_t* __restrict__ t,
-                                                         const uint32_t* __restrict__ nl, uint64_t n,
-                                                         FxRuns runs, uint32_t* __restrict__ bad) {
-    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r < n;
-         r += (uint64_t)gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(kFqBlock) fq_records_kernel(const uint8_t* __restrict__ t,
+                                                              const uint32_t* __restrict__ nl, uint64_t n,
+                                                              FxRuns runs, uint32_t* __restrict__ bad,
+                                                              FqBlockSums* __restrict__ blk) {
+    const uint64_t r = blockIdx.x * (uint64_t)kFqBlock + threadIdx.x;
+    uint64_t sl = 0, il = 0, dl = 0;
+    if (r < n) {
         const uint32_t s0 = line_start(nl, 4 * r), e0 = nl[4 * r];
         const uint32_t s1 = e0 + 1, e1 = nl[4 * r + 1];
         const uint32_t s2 = e1 + 1, e2 = nl[4 * r + 2];
@@ -150,15 +153,91 @@ __global__ void __launch_bounds__(256) fq_records_kernel(const uint8_t* __restri
         ok = ok && fx_rstrip(t, s3, e3) - s3 == se - s1;  // one quality line of the same length
         if (!ok) {
             *bad = 1;
-            runs.seq_len[r] = runs.id_len[r] = runs.desc_len[r] = 0;
             runs.seq_src[r] = runs.id_src[r] = runs.desc_src[r] = 0;
-            continue;
+        } else {
+            runs.seq_src[r] = s1;
+            sl = se - s1;
+            runs.desc_src[r] = tb;
+            dl = te - tb;
+            first_token(t, tb, te, &runs.id_src[r], &il);
         }
-        runs.seq_src[r] = s1;
-        runs.seq_len[r] = se - s1;
-        runs.desc_src[r] = tb;
-        runs.desc_len[r] = te - tb;
-        first_token(t, tb, te, &runs.id_src[r], &runs.id_len[r]);
+        runs.seq_len[r] = sl;
+        runs.id_len[r] = il;
+        runs.desc_len[r] = dl;
+    }
+    // the block's sums and longest sequence, for fq_block_scan_kernel
+    using Reduce = hipcub::BlockReduce<uint64_t, kFqBlock>;
+    __shared__ typename Reduce::TempStorage tmp;
+    const uint64_t a = Reduce(tmp).Sum(sl);
+    __syncthreads();
+    const uint64_t b = Reduce(tmp).Sum(il);
+    __syncthreads();
+    const uint64_t c = Reduce(tmp).Sum(dl);
+    __syncthreads();
+    const uint64_t m = Reduce(tmp).Reduce(sl, hipcub::Max());
+    if (threadIdx.x == 0) blk[blockIdx.x] = FqBlockSums{a, b, c, m};
+}
+
+// One block: exclusive offsets of every record block's sequence, id and
+// title bytes, and the window's totals into status ([0] bad, [1] records,
+// [2] sequence bytes, [3] id bytes, [4] title bytes, [5] longest sequence).
+__global__ void __launch_bounds__(1024) fq_block_scan_kernel(const FqBlockSums* __restrict__ blk, uint64_t nblk,
+                                                             uint64_t n, const uint32_t* __restrict__ bad,
+                                                             uint64_t* __restrict__ blk_ofs,
+                                                             uint64_t* __restrict__ status) {
+    using Scan = hipcub::BlockScan<uint64_t, 1024>;
+    using Reduce = hipcub::BlockReduce<uint64_t, 1024>;
+    __shared__ union {
+        typename Scan::TempStorage scan;
+        typename Reduce::TempStorage red;
+    } tmp;
+    const uint64_t per = (nblk + 1023) / 1024;
+    const uint64_t b0 = threadIdx.x * per, b1 = b0 + per < nblk ? b0 + per : nblk;
+    uint64_t tot[3] = {0, 0, 0}, mx = 0;
+    for (uint64_t b = b0; b < b1; ++b) {
+        tot[0] += blk[b].seq;
+        tot[1] += blk[b].id;
+        tot[2] += blk[b].desc;
+        mx = blk[b].mx > mx ? blk[b].mx : mx;
+    }
+    for (int k = 0; k < 3; ++k) {
+        uint64_t pre, all;
+        Scan(tmp.scan).ExclusiveSum(tot[k], pre, all);
+        __syncthreads();
+        for (uint64_t b = b0; b < b1; ++b) {
+            blk_ofs[3 * b + k] = pre;
+            pre += k == 0 ? blk[b].seq : k == 1 ? blk[b].id : blk[b].desc;
+        }
+        if (threadIdx.x == 0) status[2 + k] = all;
+    }
+    const uint64_t m = Reduce(tmp.red).Reduce(mx, hipcub::Max());
+    if (threadIdx.x == 0) {
+        status[0] = *bad;
+        status[1] = n;
+        status[5] = m;
+    }
+}
+
+// Record offsets of sequences, ids and titles (n+1 entries each): the block's
+// exclusive scan of its records' lengths plus the block's offset.
+__global__ void __launch_bounds__(kFqBlock) fq_offsets_kernel(FxRuns runs, uint64_t n,
+                                                              const uint64_t* __restrict__ blk_ofs,
+                                                              uint64_t* __restrict__ offs,
+                                                              uint64_t* __restrict__ id_ofs,
+                                                              uint64_t* __restrict__ desc_ofs) {
+    using Scan = hipcub::BlockScan<uint64_t, kFqBlock>;
+    __shared__ typename Scan::TempStorage tmp;
+    const uint64_t r = blockIdx.x * (uint64_t)kFqBlock + threadIdx.x;
+    const uint64_t* len[3] = {runs.seq_len, runs.id_len, runs.desc_len};
+    uint64_t* out[3] = {offs, id_ofs, desc_ofs};
+    for (int k = 0; k < 3; ++k) {
+        const uint64_t v = r < n ? len[k][r] : 0;
+        uint64_t pre;
+        Scan(tmp).ExclusiveSum(v, pre);
+        __syncthreads();
+        pre += blk_ofs[3 * blockIdx.x + k];
+        if (r < n) out[k][r] = pre;
+        if (r + 1 == n) out[k][n] = pre + v;
     }
 }
 
@@ -264,9 +343,12 @@ hipError_t launch_fx_positions(const uint8_t* text, uint64_t tiles, const uint64
 }
 
 hipError_t launch_fq_records(const uint8_t* text, const uint32_t* nl, uint64_t n, const FxRuns& runs,
-                             uint32_t* bad, hipStream_t s) {
-    if (!n) return hipSuccess;
-    fq_records_kernel<<<grid_for(n, 256, 8192), 256, 0, s>>>(text, nl, n, runs, bad);
+                             uint32_t* bad, FqBlockSums* blk, uint64_t* blk_ofs, uint64_t* offs, uint64_t* id_ofs,
+                             uint64_t* desc_ofs, uint64_t* status, hipStream_t s) {
+    const uint64_t nblk = (n + kFqBlock - 1) / kFqBlock;
+    if (nblk) fq_records_kernel<<<(unsigned)nblk, kFqBlock, 0, s>>>(text, nl, n, runs, bad, blk);
+    fq_block_scan_kernel<<<1, 1024, 0, s>>>(blk, nblk, n, bad, blk_ofs, status);
+    if (nblk) fq_offsets_kernel<<<(unsigned)nblk, kFqBlock, 0, s>>>(runs, n, blk_ofs, offs, id_ofs, desc_ofs);
     return hipGetLastError();
 }
 

@@ -226,12 +226,21 @@ struct FxRuns {
     uint32_t* desc_src;
     uint64_t* desc_len;
 };
+// FASTQ record blocks: sequence, id and title bytes, and the longest sequence
+struct FqBlockSums {
+    uint64_t seq, id, desc, mx;
+};
 size_t fx_temp_bytes(uint64_t n);
 hipError_t launch_fx_count(const uint8_t* text, uint64_t tiles, uint64_t* tile_cnt, hipStream_t s);
 hipError_t launch_fx_positions(const uint8_t* text, uint64_t tiles, const uint64_t* tile_ofs, uint32_t* nl,
                                hipStream_t s);
+// FASTQ records (4 lines each) of the window, then in three kernels the
+// offsets of their sequences, ids and titles (n+1 each) and the window's
+// status ([0] bad, [1] records, [2] sequence, [3] id, [4] title bytes, [5]
+// longest sequence): no host round trip between the passes.
 hipError_t launch_fq_records(const uint8_t* text, const uint32_t* nl, uint64_t n, const FxRuns& runs,
-                             uint32_t* bad, hipStream_t s);
+                             uint32_t* bad, FqBlockSums* blk, uint64_t* blk_ofs, uint64_t* offs, uint64_t* id_ofs,
+                             uint64_t* desc_ofs, uint64_t* status, hipStream_t s);
 hipError_t launch_fa_headers(const uint8_t* text, const uint32_t* nl, uint64_t L, uint64_t* hdr, hipStream_t s);
 hipError_t launch_fa_lines(const uint8_t* text, const uint32_t* nl, uint64_t L, const uint64_t* hofs,
                            uint32_t* line_src, uint64_t* line_len, uint32_t* rec_line, const FxRuns& runs,
