@@ -451,6 +451,7 @@ struct DBuf {
 };
 
 constexpr size_t kPieceBytes = 4u << 20;  // pread + DMA unit of a window's text
+constexpr size_t kRingPieces = 8;          // pinned pieces in flight (see DevSide::ring)
 constexpr size_t kLoadThreads = 6;         // pread threads of a window load
 constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
 
@@ -463,7 +464,13 @@ struct DevSide {
     hipEvent_t text_ev[2] = {nullptr, nullptr};
     hipEvent_t kern_ev = nullptr;                // a batch's device data complete
     hipEvent_t host_ev[2] = {nullptr, nullptr};  // slot s's host arrays complete
-    PinBuf pin[2];      // a window's text
+    // Window text goes to HBM through a ring of pinned pieces (kRingPieces x
+    // kPieceBytes): pinning costs ~0.19 ms per MiB (hipHostMalloc), so a
+    // whole-window pinned buffer (two of up to 288 MiB) cost tens of ms on
+    // a process's first file; the ring is 32 MiB whatever the window.
+    PinBuf ring;
+    hipEvent_t ring_ev[8] = {};  // the DMA out of ring piece r done (recorded on `copy`)
+    bool ring_used[8] = {};
     PinBuf status;      // small D2H results
     DBuf text[2];       // a window's text, zero-padded to whole tiles
     DBuf tiles, tile_ofs, nl, temp, flag;
@@ -527,6 +534,8 @@ DevSide::~DevSide() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy) (void)hipStreamSynchronize(copy);
+    for (hipEvent_t e : ring_ev)
+        if (e) (void)hipEventDestroy(e);
     hipEvent_t* evs[5] = {&text_ev[0], &text_ev[1], &kern_ev, &host_ev[0], &host_ev[1]};
     bool all = stream && copy;
     for (hipEvent_t* e : evs) all = all && *e;
@@ -719,9 +728,10 @@ thread_local FxTimes g_fx;
         if (_e != hipSuccess) return xs::set_error(XS_ERR_HIP, hipGetErrorString(_e));                 \
     } while (0)
 
-// The text of [lo, hi) (file offsets) into d.pin[ts] and on to d.text[ts]
-// (zero-padded to whole tiles), piece by piece: host threads pread the pieces,
-// the DMA of each piece is queued on d.copy as soon as it is in.
+// The text of [lo, hi) (file offsets) into d.text[ts] (zero-padded to whole
+// tiles), through the pinned ring: host threads pread 4 MiB pieces into ring
+// slots, the DMA of each piece is queued on d.copy as soon as it is in, and a
+// ring slot is reused once its previous DMA has completed.
 // d.text_ev[ts] marks the end.
 int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     DevSide& d = *r->dev;
@@ -730,25 +740,35 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     const size_t span = hi - lo;
     const size_t tiles = std::max<size_t>(1, (span + xs::kFxTile - 1) / xs::kFxTile);
     const size_t padded = tiles * xs::kFxTile;
-    PinBuf& pin = d.pin[ts];
     DBuf& text = d.text[ts];
-    if (int rc = pin.ensure(span + 1)) return rc;
+    if (int rc = d.ring.ensure(kRingPieces * kPieceBytes)) return rc;
+    for (hipEvent_t& e : d.ring_ev)
+        if (!e) FXCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (int rc = text.ensure(padded + 16)) return rc;
     const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
     // pread outruns the DMA (~50 GB/s) with a few threads; more only burn the
     // CPU share the caller's own threads need
     const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, kLoadThreads, pieces}));
     std::vector<uint8_t> done(pieces, 0);
+    size_t queued = 0;  // pieces whose DMA is queued (in order)
     std::mutex mu;
     std::condition_variable cv;
     bool failed = false;
     auto work = [&](int t) {
         for (size_t p = (size_t)t; p < pieces; p += (size_t)T) {
-            size_t o = p * kPieceBytes;
-            const size_t e = std::min(span, o + kPieceBytes);
+            const size_t slot = p % kRingPieces;
+            {   // the ring slot's previous piece must be on its way before it is overwritten
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return failed || p < kRingPieces || queued > p - kRingPieces; });
+                if (failed) return;
+            }
             bool bad = false;
-            while (o < e) {
-                const ssize_t got = pread(r->fd, pin.p + o, e - o, (off_t)(lo + o));
+            if (d.ring_used[slot] && hipEventSynchronize(d.ring_ev[slot]) != hipSuccess) bad = true;
+            char* dst = d.ring.p + slot * kPieceBytes;
+            const size_t n = std::min(span, (p + 1) * kPieceBytes) - p * kPieceBytes;
+            size_t o = 0;
+            while (!bad && o < n) {
+                const ssize_t got = pread(r->fd, dst + o, n - o, (off_t)(lo + p * kPieceBytes + o));
                 if (got <= 0) {
                     bad = true;
                     break;
@@ -760,7 +780,7 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
                 done[p] = 1;
                 failed |= bad;
             }
-            cv.notify_one();
+            cv.notify_all();
         }
     };
     std::vector<std::thread> th;
@@ -769,15 +789,25 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     for (size_t p = 0; p < pieces; ++p) {  // queue each piece's DMA as soon as it is in
         {
             std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return done[p] != 0; });
+            cv.wait(g, [&] { return done[p] != 0 || failed; });
             if (failed) break;
         }
+        const size_t slot = p % kRingPieces;
         const size_t o = p * kPieceBytes, n = std::min(span, o + kPieceBytes) - o;
-        hipError_t e = hipMemcpyAsync(text.as<char>() + o, pin.p + o, n, hipMemcpyHostToDevice, d.copy);
+        hipError_t e = hipMemcpyAsync(text.as<char>() + o, d.ring.p + slot * kPieceBytes, n, hipMemcpyHostToDevice,
+                                      d.copy);
+        if (e == hipSuccess) e = hipEventRecord(d.ring_ev[slot], d.copy);
         if (e != hipSuccess) {
             rc = xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
-            break;
+            std::lock_guard<std::mutex> g(mu);
+            failed = true;
+        } else {
+            std::lock_guard<std::mutex> g(mu);
+            d.ring_used[slot] = true;
+            queued = p + 1;
         }
+        cv.notify_all();
+        if (rc) break;
     }
     for (auto& x : th) x.join();
     if (rc) return rc;
