@@ -451,7 +451,17 @@ struct DBuf {
 };
 
 constexpr size_t kPieceBytes = 4u << 20;  // pread + DMA unit of a window's text
-constexpr size_t kRingPieces = 8;          // pinned pieces in flight (see DevSide::ring)
+constexpr size_t kRingMax = 64;            // most pinned pieces in flight (see DevSide::ring)
+// XSPECT2_AMD_FX_RING: pinned ring pieces (read once; default 16 = 64 MiB;
+// 0 = a pinned buffer the size of each window, per text slot)
+size_t ring_pieces() {
+    static const size_t r = [] {
+        const char* e = getenv("XSPECT2_AMD_FX_RING");
+        const long v = e ? atol(e) : 16;
+        return (size_t)std::max<long>(0, std::min<long>(v, (long)kRingMax));
+    }();
+    return r;
+}
 constexpr size_t kLoadThreads = 6;         // pread threads of a window load
 constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
 
@@ -464,13 +474,14 @@ struct DevSide {
     hipEvent_t text_ev[2] = {nullptr, nullptr};
     hipEvent_t kern_ev = nullptr;                // a batch's device data complete
     hipEvent_t host_ev[2] = {nullptr, nullptr};  // slot s's host arrays complete
-    // Window text goes to HBM through a ring of pinned pieces (kRingPieces x
-    // kPieceBytes): pinning costs ~0.19 ms per MiB (hipHostMalloc), so a
-    // whole-window pinned buffer (two of up to 288 MiB) cost tens of ms on
-    // a process's first file; the ring is 32 MiB whatever the window.
+    // Window text goes to HBM through a ring of pinned pieces (ring_pieces()
+    // x kPieceBytes): pinning costs ~0.19 ms per MiB (hipHostMalloc), so
+    // whole-window pinned buffers (two of up to 288 MiB) cost tens of ms on a
+    // process's first file; the ring is 64 MiB whatever the window.
     PinBuf ring;
-    hipEvent_t ring_ev[8] = {};  // the DMA out of ring piece r done (recorded on `copy`)
-    bool ring_used[8] = {};
+    PinBuf pin[2];                     // XSPECT2_AMD_FX_RING=0: a window's whole text per slot
+    hipEvent_t ring_ev[kRingMax] = {};  // the DMA out of ring piece r done (recorded on `copy`)
+    bool ring_used[kRingMax] = {};
     PinBuf status;      // small D2H results
     DBuf text[2];       // a window's text, zero-padded to whole tiles
     DBuf tiles, tile_ofs, nl, temp, flag;
@@ -741,9 +752,17 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     const size_t tiles = std::max<size_t>(1, (span + xs::kFxTile - 1) / xs::kFxTile);
     const size_t padded = tiles * xs::kFxTile;
     DBuf& text = d.text[ts];
-    if (int rc = d.ring.ensure(kRingPieces * kPieceBytes)) return rc;
-    for (hipEvent_t& e : d.ring_ev)
-        if (!e) FXCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t R = ring_pieces();
+    if (R) {
+        if (int rc = d.ring.ensure(R * kPieceBytes)) return rc;
+        for (size_t i = 0; i < R; ++i)
+            if (!d.ring_ev[i]) FXCHK(hipEventCreateWithFlags(&d.ring_ev[i], hipEventDisableTiming));
+    } else if (int rc = d.pin[ts].ensure(span + 1)) {
+        return rc;
+    }
+    char* const host = R ? d.ring.p : d.pin[ts].p;
+    // host buffer of piece p: its ring slot, or its place in the window's buffer
+    auto at = [&](size_t p) { return host + (R ? p % R : p) * kPieceBytes; };
     if (int rc = text.ensure(padded + 16)) return rc;
     const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
     // pread outruns the DMA (~50 GB/s) with a few threads; more only burn the
@@ -756,15 +775,17 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     bool failed = false;
     auto work = [&](int t) {
         for (size_t p = (size_t)t; p < pieces; p += (size_t)T) {
-            const size_t slot = p % kRingPieces;
-            {   // the ring slot's previous piece must be on its way before it is overwritten
-                std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return failed || p < kRingPieces || queued > p - kRingPieces; });
-                if (failed) return;
-            }
             bool bad = false;
-            if (d.ring_used[slot] && hipEventSynchronize(d.ring_ev[slot]) != hipSuccess) bad = true;
-            char* dst = d.ring.p + slot * kPieceBytes;
+            if (R) {
+                const size_t slot = p % R;
+                {   // the ring slot's previous piece must be on its way before it is overwritten
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [&] { return failed || p < R || queued > p - R; });
+                    if (failed) return;
+                }
+                if (d.ring_used[slot] && hipEventSynchronize(d.ring_ev[slot]) != hipSuccess) bad = true;
+            }
+            char* dst = at(p);
             const size_t n = std::min(span, (p + 1) * kPieceBytes) - p * kPieceBytes;
             size_t o = 0;
             while (!bad && o < n) {
@@ -792,18 +813,16 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
             cv.wait(g, [&] { return done[p] != 0 || failed; });
             if (failed) break;
         }
-        const size_t slot = p % kRingPieces;
         const size_t o = p * kPieceBytes, n = std::min(span, o + kPieceBytes) - o;
-        hipError_t e = hipMemcpyAsync(text.as<char>() + o, d.ring.p + slot * kPieceBytes, n, hipMemcpyHostToDevice,
-                                      d.copy);
-        if (e == hipSuccess) e = hipEventRecord(d.ring_ev[slot], d.copy);
+        hipError_t e = hipMemcpyAsync(text.as<char>() + o, at(p), n, hipMemcpyHostToDevice, d.copy);
+        if (e == hipSuccess && R) e = hipEventRecord(d.ring_ev[p % R], d.copy);
         if (e != hipSuccess) {
             rc = xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
             std::lock_guard<std::mutex> g(mu);
             failed = true;
         } else {
             std::lock_guard<std::mutex> g(mu);
-            d.ring_used[slot] = true;
+            if (R) d.ring_used[p % R] = true;
             queued = p + 1;
         }
         cv.notify_all();
