@@ -462,7 +462,15 @@ size_t ring_pieces() {
     }();
     return r;
 }
-constexpr size_t kLoadThreads = 6;         // pread threads of a window load
+// pread threads of a window load (XSPECT2_AMD_FX_LOAD_THREADS, read once; default 6)
+size_t load_threads() {
+    static const size_t t = [] {
+        const char* e = getenv("XSPECT2_AMD_FX_LOAD_THREADS");
+        const long v = e ? atol(e) : 6;
+        return (size_t)std::max<long>(1, std::min<long>(v, 32));
+    }();
+    return t;
+}
 constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
 
 struct DevSide {
@@ -767,7 +775,7 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
     // pread outruns the DMA (~50 GB/s) with a few threads; more only burn the
     // CPU share the caller's own threads need
-    const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, kLoadThreads, pieces}));
+    const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, load_threads(), pieces}));
     std::vector<uint8_t> done(pieces, 0);
     size_t queued = 0;  // pieces whose DMA is queued (in order)
     std::mutex mu;
