@@ -357,6 +357,8 @@ struct Batch {
 };
 
 // ---- device mode -------------------------------------------------------------
+bool fx_trace();
+double fx_ms();
 // Pinned host and device buffers outlive their reader in a process-wide pool:
 // a hipHostMalloc of a few MiB costs milliseconds and a hipFree synchronises
 // the device, so a reader per input file would otherwise pay more for its
@@ -407,15 +409,20 @@ struct PinBuf {
         release();
         if ((p = static_cast<char*>(g_pool.take(bytes, -1, &cap)))) return XS_OK;
         const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+        const double t0 = fx_ms();
         if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
             p = nullptr;
             return xs::set_error(XS_ERR_HIP, "hipHostMalloc failed for the device reader");
         }
+        if (fx_trace()) fprintf(stderr, "[fastx-device] pinned %zu B in %.2f ms\n", want, fx_ms() - t0);
         cap = want;
         return XS_OK;
     }
     void release() {
-        if (p && !g_pool.give(p, cap, -1)) (void)hipHostFree(p);
+        if (p && !g_pool.give(p, cap, -1)) {
+            if (fx_trace()) fprintf(stderr, "[fastx-device] unpinned %zu B\n", cap);
+            (void)hipHostFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -439,7 +446,10 @@ struct DBuf {
         return XS_OK;
     }
     void release() {
-        if (p && !g_pool.give(p, cap, device)) (void)hipFree(p);
+        if (p && !g_pool.give(p, cap, device)) {
+            if (fx_trace()) fprintf(stderr, "[fastx-device] hipFree %zu B\n", cap);
+            (void)hipFree(p);
+        }
         p = nullptr;
         cap = 0;
     }
@@ -548,6 +558,53 @@ bool take_streams(DevSide& d) {
     return false;
 }
 
+// Whole device sides of closed readers, kept for the next reader on the same
+// device: their streams, events and buffers at the sizes the last file grew
+// them to, so a process reading file after file allocates and pins nothing
+// after its first (a reader's buffers otherwise went back to g_pool piece by
+// piece and the next reader's ramp took them out in a different order,
+// pinning and freeing afresh: 17 -> 26 ms per 313 MB file over six files,
+// profiles/r04_e2e_ring.txt).  A batch's arrays are the reader's and are
+// invalid after xs_fastx_close, as before.
+std::mutex g_ds_mu;
+std::vector<DevSide*> g_ds;
+constexpr size_t kDevSidesKept = 4;
+
+DevSide* take_devside(int device) {
+    std::lock_guard<std::mutex> g(g_ds_mu);
+    for (size_t i = 0; i < g_ds.size(); ++i) {
+        if (g_ds[i]->device != device) continue;
+        DevSide* d = g_ds[i];
+        g_ds.erase(g_ds.begin() + (long)i);
+        return d;
+    }
+    return nullptr;
+}
+
+// Quiesce a closed reader's device side and keep it (or destroy it when
+// kDevSidesKept are kept already or its streams were never made).
+void put_devside(DevSide* d) {
+    if (!d) return;
+    if (d->worker.joinable()) d->worker.join();
+    d->pending = false;
+    bool ok = d->stream && d->copy && hipSetDevice(d->device) == hipSuccess &&
+              hipStreamSynchronize(d->stream) == hipSuccess && hipStreamSynchronize(d->copy) == hipSuccess;
+    if (ok) {
+        d->flip = 0;
+        d->next_text = 0;
+        d->pf_rc = XS_OK;
+        d->pf_err.clear();
+        d->pf_lo = d->pf_hi = 0;
+        d->load_ms[0] = d->load_ms[1] = 0;
+        std::lock_guard<std::mutex> g(g_ds_mu);
+        if (g_ds.size() < kDevSidesKept) {
+            g_ds.push_back(d);
+            return;
+        }
+    }
+    delete d;
+}
+
 DevSide::~DevSide() {
     if (worker.joinable()) worker.join();
     (void)hipSetDevice(device);
@@ -589,7 +646,7 @@ struct xs_fastx {
     std::vector<Part> parts;
     DevSide* dev = nullptr;
     ~xs_fastx() {
-        delete dev;
+        put_devside(dev);
         if (base && size) munmap(const_cast<char*>(base), size);
         if (fd >= 0) close(fd);
     }
@@ -1156,15 +1213,17 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
                          xs_fastx** out) {
     if (int rc = xs_fastx_open_range(path, format, threads, 0, part, parts, out)) return rc;
     xs_fastx* r = *out;
-    r->dev = new DevSide();
-    r->dev->set_device(device);
     auto fail = [&](hipError_t e) {
         xs_fastx_close(r);
         *out = nullptr;
         return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
     };
     hipError_t e = hipSetDevice(device);
-    if (e == hipSuccess && take_streams(*r->dev)) return XS_OK;
+    if (e != hipSuccess) return fail(e);
+    if ((r->dev = take_devside(device))) return XS_OK;
+    r->dev = new DevSide();
+    r->dev->set_device(device);
+    if (take_streams(*r->dev)) return XS_OK;
     // The parse kernels are short and sit between the caller's probes of the
     // previous batch: a high-priority stream lets their workgroups in as soon
     // as the probe frees a slot, instead of after the whole probe.
