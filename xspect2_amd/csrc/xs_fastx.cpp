@@ -462,12 +462,12 @@ struct DBuf {
 
 constexpr size_t kPieceBytes = 4u << 20;  // pread + DMA unit of a window's text
 constexpr size_t kRingMax = 64;            // most pinned pieces in flight (see DevSide::ring)
-// XSPECT2_AMD_FX_RING: pinned ring pieces (read once; default 16 = 64 MiB;
+// XSPECT2_AMD_FX_RING: pinned ring pieces (read once; default 32 = 128 MiB;
 // 0 = a pinned buffer the size of each window, per text slot)
 size_t ring_pieces() {
     static const size_t r = [] {
         const char* e = getenv("XSPECT2_AMD_FX_RING");
-        const long v = e ? atol(e) : 16;
+        const long v = e ? atol(e) : 32;
         return (size_t)std::max<long>(0, std::min<long>(v, (long)kRingMax));
     }();
     return r;
@@ -495,7 +495,7 @@ struct DevSide {
     // Window text goes to HBM through a ring of pinned pieces (ring_pieces()
     // x kPieceBytes): pinning costs ~0.19 ms per MiB (hipHostMalloc), so
     // whole-window pinned buffers (two of up to 288 MiB) cost tens of ms on a
-    // process's first file; the ring is 64 MiB whatever the window.
+    // process's first file; the ring is 128 MiB whatever the window.
     PinBuf ring;
     PinBuf pin[2];                     // XSPECT2_AMD_FX_RING=0: a window's whole text per slot
     hipEvent_t ring_ev[kRingMax] = {};  // the DMA out of ring piece r done (recorded on `copy`)
