@@ -181,6 +181,43 @@ def test_large_windows_many_tiles(tmp_path):
         assert sum(b["n"] for b in dev) == n
 
 
+def test_kept_device_sides_across_opens(tmp_path):
+    """Closed readers hand their device side (streams, buffers at their grown
+    sizes) to the next open: a large file, then small ones, then two readers
+    open at once and read in turns, each batch equal to the host reader's."""
+    rng = np.random.default_rng(9)
+    big = tmp_path / "big.fastq"
+    n = 60_000
+    seqs = rng.integers(0, 4, (n, 150), dtype=np.uint8)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    big.write_bytes(b"".join(b"@b%d\n%s\n+\n%s\n" % (i, acgt[seqs[i]].tobytes(), b"I" * 150) for i in range(n)))
+    small_fq = tmp_path / "s.fastq"
+    small_fq.write_bytes(_plain_fastq(rng, 500))
+    small_fa = tmp_path / "s.fasta"
+    small_fa.write_bytes(b"".join(b">c%d x\n%s\n" % (i, _pick(rng, b"ACGT", 200)) for i in range(300)))
+    for path, mb in ((big, 1 << 30), (small_fq, 1 << 30), (small_fa, 3000), (big, 4 << 20), (small_fq, 700)):
+        _same(path, mb)
+    want = {p: _batches(p, 5000, None) for p in (small_fq, small_fa)}
+    ra, rb = FastxReader(small_fq, device=0), FastxReader(small_fa, device=0)
+    try:
+        got = {small_fq: [], small_fa: []}
+        live = [(ra, small_fq), (rb, small_fa)]
+        while live:
+            for rd, p in list(live):
+                b = rd.next_batch(5000)
+                if b.n == 0:
+                    live.remove((rd, p))
+                    continue
+                pr = b.to_host()
+                o = pr.offsets.astype(np.int64)
+                got[p].append((b.n, o.tolist(), pr.buf[:o[-1]].tobytes(), b.ids(), b.descriptions()))
+        for p in got:
+            assert got[p] == [(h["n"], h["offsets"], h["seqs"], h["ids"], h["descs"]) for h in want[p] if h["n"]]
+    finally:
+        ra.close()
+        rb.close()
+
+
 def test_probe_on_device_batches_equals_host(tmp_path, oracle_mod):
     from xspect2_amd.bank import Bank
     from xspect2_amd.synth import make_genomes, make_reads
