@@ -29,6 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--modes", default="seq,gen,gen_sw")
     ap.add_argument("--reps", type=int, default=4)
+    ap.add_argument("--reads", type=int, default=1_000_000)
     args = ap.parse_args()
     import torch
     from fx_dev_trace import write_fastq
@@ -37,7 +38,7 @@ def main():
     from xspect2_amd.synth import make_genomes
 
     p = Path("/tmp/xs_stall.fastq")
-    write_fastq(p, 1_000_000)
+    write_fastq(p, args.reads)
     k, D, G = 21, 100, 4_000_000
     dev = torch.device("cuda", 0)
     genomes = make_genomes(D, G, seed=42)
