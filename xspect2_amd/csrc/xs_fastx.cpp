@@ -1044,11 +1044,13 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     if (int rc = d.desc_offs[slot].ensure((n + 1) * 8)) return rc;
     if (int rc = d.hoffs[slot].ensure((n + 1) * 8)) return rc;
     uint8_t* seqs = d.seqs[slot].as<uint8_t>();
-    if (fasta) FXCHK(xs::launch_fx_copy(text, d.line_src.as<uint32_t>(), d.line_ofs.as<uint64_t>(), L, seqs, s));
-    else FXCHK(xs::launch_fx_copy(text, d.seq_src.as<uint32_t>(), offs, n, seqs, s));
+    if (fasta)
+        FXCHK(xs::launch_fx_copy(text, d.line_src.as<uint32_t>(), d.line_ofs.as<uint64_t>(), L, sbytes, seqs, s));
+    else FXCHK(xs::launch_fx_copy(text, d.seq_src.as<uint32_t>(), offs, n, sbytes, seqs, s));
     FXCHK(hipMemsetAsync(seqs + sbytes, 0, kDevPad, s));
-    FXCHK(xs::launch_fx_copy(text, d.id_src.as<uint32_t>(), d.id_ofs.as<uint64_t>(), n, d.ids_d.as<uint8_t>(), s));
-    FXCHK(xs::launch_fx_copy(text, d.desc_src.as<uint32_t>(), d.desc_ofs.as<uint64_t>(), n,
+    FXCHK(xs::launch_fx_copy(text, d.id_src.as<uint32_t>(), d.id_ofs.as<uint64_t>(), n, ibytes, d.ids_d.as<uint8_t>(),
+                             s));
+    FXCHK(xs::launch_fx_copy(text, d.desc_src.as<uint32_t>(), d.desc_ofs.as<uint64_t>(), n, dbytes,
                              d.descs_d.as<uint8_t>(), s));
     FXCHK(hipEventRecord(d.kern_ev, s));  // the batch's device data: what the caller probes
     // the host arrays land behind the caller's probe; xs_fastx_wait_host waits for them

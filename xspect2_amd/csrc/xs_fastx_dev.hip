@@ -54,20 +54,6 @@ __device__ __forceinline__ uint32_t eq_bits(uint32_t w, uint32_t c) {
     return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
 }
 
-// No ' ' or '\t' in t[b, e): aligned dword loads (the text is 16-B aligned and
-// zero-padded past the window), bytes outside [b, e) masked off.
-__device__ __forceinline__ bool no_space_tab(const uint8_t* t, uint32_t b, uint32_t e) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(t);
-    for (uint32_t p = b & ~3u; p < e; p += 4) {
-        const uint32_t x = w[p >> 2];
-        uint32_t keep = 0xffffffffu;
-        if (p < b) keep <<= 8 * (b - p);
-        if (e - p < 4) keep &= (1u << (8 * (e - p))) - 1u;
-        if ((eq_bits(x, ' ') | eq_bits(x, '\t')) & keep) return false;
-    }
-    return true;
-}
-
 // First whitespace-separated token of [b, e): its start and length.
 __device__ __forceinline__ void first_token(const uint8_t* t, uint32_t b, uint32_t e, uint32_t* s, uint64_t* len) {
     while (b < e && fx_ws(t[b])) ++b;
@@ -130,18 +116,22 @@ __global__ void __launch_bounds__(kFqBlock) fq_records_kernel(const uint8_t* __r
                                                               FqBlockSums* __restrict__ blk) {
     const uint64_t r = blockIdx.x * (uint64_t)kFqBlock + threadIdx.x;
     uint64_t sl = 0, il = 0, dl = 0;
+    // Pass 1, a record per lane: the line layout, the title, the caption and
+    // the quality length.  The sequence line's ' '/'\t' check is pass 2.
+    bool ok = false;
+    uint32_t s1 = 0, se = 0, tb = 0, te = 0;
     if (r < n) {
         const uint32_t s0 = line_start(nl, 4 * r), e0 = nl[4 * r];
-        const uint32_t s1 = e0 + 1, e1 = nl[4 * r + 1];
+        s1 = e0 + 1;
+        const uint32_t e1 = nl[4 * r + 1];
         const uint32_t s2 = e1 + 1, e2 = nl[4 * r + 2];
         const uint32_t s3 = e2 + 1, e3 = nl[4 * r + 3];
-        bool ok = e0 > s0 && t[s0] == '@';
-        const uint32_t tb = s0 + 1;
-        const uint32_t te = ok ? fx_rstrip(t, tb, e0) : tb;
+        ok = e0 > s0 && t[s0] == '@';
+        tb = s0 + 1;
+        te = ok ? fx_rstrip(t, tb, e0) : tb;
         // one sequence line, not empty, not itself a '+' line
-        const uint32_t se = fx_rstrip(t, s1, e1);
+        se = fx_rstrip(t, s1, e1);
         ok = ok && se > s1 && t[s1] != '+';
-        ok = ok && no_space_tab(t, s1, se);
         ok = ok && e2 > s2 && t[s2] == '+';
         if (ok) {  // a caption, if any, repeats the title
             const uint32_t cb = s2 + 1, ce = fx_rstrip(t, cb, e2);
@@ -151,6 +141,43 @@ __global__ void __launch_bounds__(kFqBlock) fq_records_kernel(const uint8_t* __r
             }
         }
         ok = ok && fx_rstrip(t, s3, e3) - s3 == se - s1;  // one quality line of the same length
+    }
+    // Pass 2: no ' ' or '\t' in the sequence lines, read coalesced: a group of
+    // 16 lanes scans one record's line in 16-B loads (256 B per step), four
+    // records per wave step.  A lane scanning its own line alone put 64
+    // scattered lines in flight per load (~0.8 ms per 256 MiB window, now ~4x less).
+    {
+        const int lane = threadIdx.x & 63, g = lane >> 4, gl = lane & 15;
+        const uint4* t16 = reinterpret_cast<const uint4*>(t);
+        bool clean = true;
+        for (int j = 0; j < 64; j += 4) {
+            const int owner = j + g;
+            const uint32_t b = __shfl(s1, owner), e = __shfl(se, owner);
+            const bool need = __shfl((int)ok, owner) != 0;
+            bool dirty = false;
+            if (need) {
+                for (uint32_t p = (b & ~15u) + 16u * gl; p < e; p += 256u) {
+                    const uint4 v = t16[p >> 4];
+                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t at = p + 4u * q;
+                        uint32_t keep = 0xffffffffu;
+                        if (at + 4 <= b || at >= e) keep = 0;
+                        else {
+                            if (at < b) keep <<= 8 * (b - at);
+                            if (e - at < 4) keep &= (1u << (8 * (e - at))) - 1u;
+                        }
+                        dirty |= ((eq_bits(w[q], ' ') | eq_bits(w[q], '\t')) & keep) != 0;
+                    }
+                }
+            }
+            const uint64_t m = __ballot(dirty);
+            if (lane >= j && lane < j + 4) clean = ((m >> (16 * (lane - j))) & 0xffffull) == 0;
+        }
+        ok = ok && clean;
+    }
+    if (r < n) {
         if (!ok) {
             *bad = 1;
             runs.seq_src[r] = runs.id_src[r] = runs.desc_src[r] = 0;
@@ -306,17 +333,35 @@ __global__ void __launch_bounds__(256) fa_offsets_kernel(const uint32_t* __restr
 }
 
 // Run i = src[i] .. + (dofs[i+1] - dofs[i]) bytes of t, to dst + dofs[i].
+// G lanes per run (64 for sequences, 4-16 for ids and titles: the host picks
+// G from the mean run length); each lane writes whole aligned output dwords,
+// assembled from two aligned text dwords (alignbyte), and the bytes of the
+// run's first and last dword that it shares with its neighbours one by one.
+// dst is 4-B aligned; t is dword-readable 8 B past any run.
+template <int G>
 __global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict__ t,
                                                       const uint32_t* __restrict__ src,
                                                       const uint64_t* __restrict__ dofs, uint64_t m,
                                                       uint8_t* __restrict__ dst) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
-    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t i = wave; i < m; i += waves) {
-        const uint64_t o = dofs[i], len = dofs[i + 1] - o;
-        const uint8_t* s = t + src[i];
-        for (uint64_t x = (uint64_t)lane; x < len; x += 64) dst[o + x] = s[x];
+    const int gl = threadIdx.x % G;
+    const uint64_t grp = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    const uint64_t grps = ((uint64_t)gridDim.x * blockDim.x) / G;
+    const uint32_t* t32 = reinterpret_cast<const uint32_t*>(t);
+    uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
+    for (uint64_t i = grp; i < m; i += grps) {
+        const uint64_t o = dofs[i], end = dofs[i + 1];
+        if (end == o) continue;
+        const uint64_t s = src[i];
+        for (uint64_t w = (o >> 2) + gl; w <= (end - 1) >> 2; w += G) {
+            const uint64_t q0 = w << 2;
+            if (q0 >= o && q0 + 4 <= end) {
+                const uint64_t x = s + (q0 - o);
+                const uint32_t lo = t32[x >> 2], hi = t32[(x >> 2) + 1];
+                d32[w] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(x & 3));
+            } else {
+                for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+            }
+        }
     }
 }
 
@@ -374,10 +419,13 @@ hipError_t launch_fa_offsets(const uint32_t* rec_line, const uint64_t* line_ofs,
     return hipGetLastError();
 }
 
-hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint8_t* dst,
-                          hipStream_t s) {
-    if (!m) return hipSuccess;
-    fx_copy_kernel<<<grid_for(m, 4, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
+hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint64_t bytes,
+                          uint8_t* dst, hipStream_t s) {
+    if (!m || !bytes) return hipSuccess;
+    const uint64_t mean = bytes / m;  // lanes per run: about one output dword each
+    if (mean > 64) fx_copy_kernel<64><<<grid_for(m, 4, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
+    else if (mean > 16) fx_copy_kernel<16><<<grid_for(m, 16, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
+    else fx_copy_kernel<4><<<grid_for(m, 64, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
     return hipGetLastError();
 }
 

@@ -247,8 +247,8 @@ hipError_t launch_fa_lines(const uint8_t* text, const uint32_t* nl, uint64_t L, 
                            uint32_t* bad, hipStream_t s);
 hipError_t launch_fa_offsets(const uint32_t* rec_line, const uint64_t* line_ofs, uint64_t L, const uint64_t* n_dev,
                              uint64_t* offs, uint64_t* lens, hipStream_t s);
-hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint8_t* dst,
-                          hipStream_t s);
+hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64_t* dofs, uint64_t m, uint64_t bytes,
+                          uint8_t* dst, hipStream_t s);
 hipError_t launch_max_u64(void* temp, size_t temp_bytes, const uint64_t* in, uint64_t n, uint64_t* out,
                           hipStream_t s);
 
