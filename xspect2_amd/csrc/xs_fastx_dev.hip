@@ -333,9 +333,12 @@ __global__ void __launch_bounds__(256) fa_offsets_kernel(const uint32_t* __restr
 }
 
 // Run i = src[i] .. + (dofs[i+1] - dofs[i]) bytes of t, to dst + dofs[i].
-// G lanes per run (64 for sequences, 4-16 for ids and titles: the host picks
-// G from the mean run length); each lane writes whole aligned output dwords,
-// assembled from two aligned text dwords (alignbyte), and the bytes of the
+// A wave takes 64 runs at a time and loads their bounds in one coalesced
+// load; G lanes copy one run (64 for sequences, 4-16 for ids and titles: the
+// host picks G from the mean run length), 64/G runs per step, the bounds
+// broadcast by shuffle, so consecutive runs' loads overlap instead of each
+// run waiting on its own bounds.  Each lane writes whole aligned output dwords
+// assembled from two aligned text dwords (alignbyte), and the bytes of a
 // run's first and last dword that it shares with its neighbours one by one.
 // dst is 4-B aligned; t is dword-readable 8 B past any run.
 template <int G>
@@ -343,23 +346,30 @@ __global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict_
                                                       const uint32_t* __restrict__ src,
                                                       const uint64_t* __restrict__ dofs, uint64_t m,
                                                       uint8_t* __restrict__ dst) {
-    const int gl = threadIdx.x % G;
-    const uint64_t grp = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
-    const uint64_t grps = ((uint64_t)gridDim.x * blockDim.x) / G;
+    constexpr int kPer = 64 / G;  // runs per step
+    const int lane = threadIdx.x & 63, gl = lane % G, sub = lane / G;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint32_t* t32 = reinterpret_cast<const uint32_t*>(t);
     uint32_t* d32 = reinterpret_cast<uint32_t*>(dst);
-    for (uint64_t i = grp; i < m; i += grps) {
-        const uint64_t o = dofs[i], end = dofs[i + 1];
-        if (end == o) continue;
-        const uint64_t s = src[i];
-        for (uint64_t w = (o >> 2) + gl; w <= (end - 1) >> 2; w += G) {
-            const uint64_t q0 = w << 2;
-            if (q0 >= o && q0 + 4 <= end) {
-                const uint64_t x = s + (q0 - o);
-                const uint32_t lo = t32[x >> 2], hi = t32[(x >> 2) + 1];
-                d32[w] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(x & 3));
-            } else {
-                for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+    for (uint64_t c = wave * 64; c < m; c += waves * 64) {
+        const uint64_t i = c + lane;
+        const uint64_t my_o = i < m ? dofs[i] : 0, my_e = i < m ? dofs[i + 1] : 0;
+        const uint64_t my_s = i < m ? src[i] : 0;
+#pragma unroll 2
+        for (int k = 0; k < G; ++k) {
+            const int run = k * kPer + sub;  // lane of the run's bounds
+            const uint64_t o = __shfl(my_o, run), end = __shfl(my_e, run), s = __shfl(my_s, run);
+            if (end <= o) continue;  // empty run, or past m
+            for (uint64_t w = (o >> 2) + gl; w <= (end - 1) >> 2; w += G) {
+                const uint64_t q0 = w << 2;
+                if (q0 >= o && q0 + 4 <= end) {
+                    const uint64_t x = s + (q0 - o);
+                    const uint32_t lo = t32[x >> 2], hi = t32[(x >> 2) + 1];
+                    d32[w] = __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(x & 3));
+                } else {
+                    for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+                }
             }
         }
     }
@@ -423,9 +433,10 @@ hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64
                           uint8_t* dst, hipStream_t s) {
     if (!m || !bytes) return hipSuccess;
     const uint64_t mean = bytes / m;  // lanes per run: about one output dword each
-    if (mean > 64) fx_copy_kernel<64><<<grid_for(m, 4, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
-    else if (mean > 16) fx_copy_kernel<16><<<grid_for(m, 16, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
-    else fx_copy_kernel<4><<<grid_for(m, 64, 16384), 256, 0, s>>>(text, src, dofs, m, dst);
+    const int grid = grid_for(m, 256, 8192);  // 64 runs per wave at a time
+    if (mean > 64) fx_copy_kernel<64><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    else if (mean > 16) fx_copy_kernel<16><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    else fx_copy_kernel<4><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
     return hipGetLastError();
 }
 
