@@ -181,6 +181,24 @@ def test_large_windows_many_tiles(tmp_path):
         assert sum(b["n"] for b in dev) == n
 
 
+@pytest.mark.parametrize("inject", [None, b" ", b"\r"])
+def test_fasta_unwrapped_megabase_lines(tmp_path, inject):
+    """Assemblies written one sequence line per contig: 2-3 Mbp lines are
+    checked by whole waves; a ' ' or '\\r' inside one sends the window to the
+    host parser, which removes it, as Biopython does."""
+    rng = np.random.default_rng(11)
+    contigs = [_pick(rng, b"ACGT", L) for L in (3_000_000, 17, 2_000_003, 150)]
+    if inject is not None:
+        c = bytearray(contigs[2])
+        c[1_234_567] = inject[0]
+        contigs[2] = bytes(c)
+    p = tmp_path / "asm.fasta"
+    p.write_bytes(b"".join(b">ctg%d len=%d\n%s\n" % (i, len(c), c) for i, c in enumerate(contigs)))
+    dev = _same(p, 1 << 30)
+    assert all(b["dev"] for b in dev) == (inject is None)
+    assert sum(b["n"] for b in dev) == 4
+
+
 def test_kept_device_sides_across_opens(tmp_path):
     """Closed readers hand their device side (streams, buffers at their grown
     sizes) to the next open: a large file, then small ones, then two readers

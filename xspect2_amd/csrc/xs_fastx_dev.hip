@@ -289,27 +289,55 @@ __global__ void __launch_bounds__(256) fa_lines_kernel(const uint8_t* __restrict
                                                        uint64_t* __restrict__ line_len,
                                                        uint32_t* __restrict__ rec_line, FxRuns runs,
                                                        uint32_t* __restrict__ bad) {
-    for (uint64_t j = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; j < L;
-         j += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t s = line_start(nl, j), e = nl[j];
-        line_src[j] = s;
-        if (e > s && t[s] == '>') {
-            const uint64_t r = hofs[j];
-            rec_line[r] = (uint32_t)j;
-            const uint32_t tb = s + 1, te = fx_rstrip(t, tb, e);
-            runs.desc_src[r] = tb;
-            runs.desc_len[r] = te - tb;
-            first_token(t, tb, te, &runs.id_src[r], &runs.id_len[r]);
-            line_len[j] = 0;
-        } else if (hofs[j] == 0) {
-            line_len[j] = 0;
-        } else {
-            const uint32_t se = fx_rstrip(t, s, e);
-            bool ok = true;
-            for (uint32_t p = s; ok && p < se; ++p) ok = t[p] != ' ' && t[p] != '\r';
-            if (!ok) *bad = 1;  // the host removes them inside the line
-            line_len[j] = se - s;
+    // a wave takes 64 lines at a time: a line per lane, then the whole wave
+    // checks each kept sequence line for ' ' / '\r' in 16-B loads (1 KiB per
+    // step), so an unwrapped multi-megabase line is not one lane's byte loop
+    const int lane = threadIdx.x & 63;
+    const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint4* t16 = reinterpret_cast<const uint4*>(t);
+    for (uint64_t c = wave * 64; c < L; c += waves * 64) {
+        const uint64_t j = c + lane;
+        uint32_t s = 0, se = 0;
+        if (j < L) {
+            s = line_start(nl, j);
+            const uint32_t e = nl[j];
+            line_src[j] = s;
+            if (e > s && t[s] == '>') {
+                const uint64_t r = hofs[j];
+                rec_line[r] = (uint32_t)j;
+                const uint32_t tb = s + 1, te = fx_rstrip(t, tb, e);
+                runs.desc_src[r] = tb;
+                runs.desc_len[r] = te - tb;
+                first_token(t, tb, te, &runs.id_src[r], &runs.id_len[r]);
+                line_len[j] = 0;
+            } else if (hofs[j] == 0) {
+                line_len[j] = 0;
+            } else {
+                se = fx_rstrip(t, s, e);
+                line_len[j] = se - s;
+            }
         }
+        bool dirty = false;
+        for (int k = 0; k < 64; ++k) {  // sequence lines only (se > s)
+            const uint32_t b = __shfl(s, k), e = __shfl(se, k);
+            for (uint32_t p = (b & ~15u) + 16u * lane; p < e; p += 1024u) {
+                const uint4 v = t16[p >> 4];
+                const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t at = p + 4u * q;
+                    uint32_t keep = 0xffffffffu;
+                    if (at + 4 <= b || at >= e) keep = 0;
+                    else {
+                        if (at < b) keep <<= 8 * (b - at);
+                        if (e - at < 4) keep &= (1u << (8 * (e - at))) - 1u;
+                    }
+                    dirty |= ((eq_bits(w[q], ' ') | eq_bits(w[q], '\r')) & keep) != 0;
+                }
+            }
+        }
+        if (dirty) *bad = 1;  // the host removes them inside the line
     }
 }
 
@@ -418,7 +446,7 @@ hipError_t launch_fa_lines(const uint8_t* text, const uint32_t* nl, uint64_t L, 
                            uint32_t* bad, hipStream_t s) {
     if (!L) return hipSuccess;
     fa_lines_kernel<<<grid_for(L, 256, 8192), 256, 0, s>>>(text, nl, L, hofs, line_src, line_len, rec_line, runs,
-                                                          bad);
+                                                          bad);  // 64 lines per wave at a time
     return hipGetLastError();
 }
 
