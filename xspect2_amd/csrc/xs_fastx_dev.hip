@@ -389,10 +389,21 @@ __global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict_
             const int run = k * kPer + sub;  // lane of the run's bounds
             const uint64_t o = __shfl(my_o, run), end = __shfl(my_e, run), s = __shfl(my_s, run);
             if (end <= o) continue;  // empty run, or past m
-            const uint64_t wl = (end - 1) >> 2;  // the run's last output dword
-            // four dwords per lane per pass, all loaded before any is stored, so
-            // a long run (an unwrapped contig line) keeps 8 loads in flight
-            for (uint64_t w = (o >> 2) + gl; w <= wl; w += 4 * G) {
+            const uint64_t w0 = o >> 2, wl = (end - 1) >> 2;  // the run's output dwords
+            if (wl - w0 < (uint64_t)G) {  // a dword per lane at most (reads, ids)
+                const uint64_t w = w0 + gl, q0 = w << 2;
+                if (w > wl) continue;
+                if (q0 >= o && q0 + 4 <= end) {
+                    const uint64_t x = s + (q0 - o);
+                    d32[w] = __builtin_amdgcn_alignbyte(t32[(x >> 2) + 1], t32[x >> 2], (uint32_t)(x & 3));
+                } else {
+                    for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+                }
+                continue;
+            }
+            // a long run (an unwrapped contig line): four dwords per lane per
+            // pass, all loaded before any is stored, 8 loads in flight
+            for (uint64_t w = w0 + gl; w <= wl; w += 4 * G) {
                 uint32_t v[4];
                 bool full[4];
 #pragma unroll
