@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(256) fa_offsets_kernel(const uint32_t* __restr
 // assembled from two aligned text dwords (alignbyte), and the bytes of a
 // run's first and last dword that it shares with its neighbours one by one.
 // dst is 4-B aligned; t is dword-readable 8 B past any run.
-template <int G>
+template <int G, bool kLong>
 __global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict__ t,
                                                       const uint32_t* __restrict__ src,
                                                       const uint64_t* __restrict__ dofs, uint64_t m,
@@ -390,19 +390,21 @@ __global__ void __launch_bounds__(256) fx_copy_kernel(const uint8_t* __restrict_
             const uint64_t o = __shfl(my_o, run), end = __shfl(my_e, run), s = __shfl(my_s, run);
             if (end <= o) continue;  // empty run, or past m
             const uint64_t w0 = o >> 2, wl = (end - 1) >> 2;  // the run's output dwords
-            if (wl - w0 < (uint64_t)G) {  // a dword per lane at most (reads, ids)
-                const uint64_t w = w0 + gl, q0 = w << 2;
-                if (w > wl) continue;
-                if (q0 >= o && q0 + 4 <= end) {
-                    const uint64_t x = s + (q0 - o);
-                    d32[w] = __builtin_amdgcn_alignbyte(t32[(x >> 2) + 1], t32[x >> 2], (uint32_t)(x & 3));
-                } else {
-                    for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+            if (!kLong) {
+                for (uint64_t w = w0 + gl; w <= wl; w += G) {
+                    const uint64_t q0 = w << 2;
+                    if (q0 >= o && q0 + 4 <= end) {
+                        const uint64_t x = s + (q0 - o);
+                        d32[w] = __builtin_amdgcn_alignbyte(t32[(x >> 2) + 1], t32[x >> 2], (uint32_t)(x & 3));
+                    } else {
+                        for (uint64_t q = q0 > o ? q0 : o; q < q0 + 4 && q < end; ++q) dst[q] = t[s + (q - o)];
+                    }
                 }
                 continue;
             }
-            // a long run (an unwrapped contig line): four dwords per lane per
-            // pass, all loaded before any is stored, 8 loads in flight
+            // long runs (unwrapped contig lines): four dwords per lane per pass,
+            // all loaded before any is stored, 8 loads in flight (a separate
+            // instantiation: its registers would slow the short-run copies)
             for (uint64_t w = w0 + gl; w <= wl; w += 4 * G) {
                 uint32_t v[4];
                 bool full[4];
@@ -486,9 +488,10 @@ hipError_t launch_fx_copy(const uint8_t* text, const uint32_t* src, const uint64
     if (!m || !bytes) return hipSuccess;
     const uint64_t mean = bytes / m;  // lanes per run: about one output dword each
     const int grid = grid_for(m, 256, 8192);  // 64 runs per wave at a time
-    if (mean > 64) fx_copy_kernel<64><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
-    else if (mean > 16) fx_copy_kernel<16><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
-    else fx_copy_kernel<4><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    if (mean > 4096) fx_copy_kernel<64, true><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    else if (mean > 64) fx_copy_kernel<64, false><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    else if (mean > 16) fx_copy_kernel<16, false><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
+    else fx_copy_kernel<4, false><<<grid, 256, 0, s>>>(text, src, dofs, m, dst);
     return hipGetLastError();
 }
 
