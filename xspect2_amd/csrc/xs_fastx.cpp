@@ -42,6 +42,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -509,14 +510,22 @@ struct DevSide {
     DBuf fq_blk, fq_blk_ofs, fq_status;  // FASTQ record blocks' sums and offsets, the window's status
     PinBuf ids[2], id_offs[2], descs[2], desc_offs[2], hoffs[2];
     int flip = 0;
-    // text of the next window, loaded by `worker` while the caller works
-    std::thread worker;
-    bool pending = false;
-    size_t pf_lo = 0, pf_hi = 0;
-    int pf_slot = 0;
-    int next_text = 0;  // text slot of the next inline load
-    int pf_rc = XS_OK;
-    std::string pf_err;
+    // Text of the next windows, loaded in order by `loader` while the caller
+    // works: up to two ahead, window j+2 into window j's slot as soon as j is
+    // parsed (the parse is the only reader of a slot's text).
+    struct PfJob {
+        size_t lo, hi;
+        int slot;
+        bool started, done;
+        int rc;
+        std::string err;
+    };
+    std::thread loader;
+    std::mutex pf_mu;
+    std::condition_variable pf_cv;
+    std::deque<PfJob> pf_q;  // oldest first; popped by text_for once done
+    bool pf_stop = false;
+    int next_text = 0;  // text slot of the next window queued or loaded inline
     double load_ms[2] = {0, 0};  // each slot's last load_text: pread + DMA queueing
     void set_device(int dev) {
         device = dev;
@@ -566,6 +575,19 @@ bool take_streams(DevSide& d) {
 // pinning and freeing afresh: 17 -> 26 ms per 313 MB file over six files,
 // profiles/r04_e2e_ring.txt).  A batch's arrays are the reader's and are
 // invalid after xs_fastx_close, as before.
+// End the loader thread after the loads it has started (a queued load
+// that has not started is dropped), and forget the queue.
+void stop_loader(DevSide& d) {
+    {
+        std::lock_guard<std::mutex> g(d.pf_mu);
+        d.pf_stop = true;
+    }
+    d.pf_cv.notify_all();
+    if (d.loader.joinable()) d.loader.join();
+    d.pf_stop = false;
+    d.pf_q.clear();
+}
+
 std::mutex g_ds_mu;
 std::vector<DevSide*> g_ds;
 constexpr size_t kDevSidesKept = 4;
@@ -585,16 +607,12 @@ DevSide* take_devside(int device) {
 // kDevSidesKept are kept already or its streams were never made).
 void put_devside(DevSide* d) {
     if (!d) return;
-    if (d->worker.joinable()) d->worker.join();
-    d->pending = false;
+    stop_loader(*d);
     bool ok = d->stream && d->copy && hipSetDevice(d->device) == hipSuccess &&
               hipStreamSynchronize(d->stream) == hipSuccess && hipStreamSynchronize(d->copy) == hipSuccess;
     if (ok) {
         d->flip = 0;
         d->next_text = 0;
-        d->pf_rc = XS_OK;
-        d->pf_err.clear();
-        d->pf_lo = d->pf_hi = 0;
         d->load_ms[0] = d->load_ms[1] = 0;
         std::lock_guard<std::mutex> g(g_ds_mu);
         if (g_ds.size() < kDevSidesKept) {
@@ -606,7 +624,7 @@ void put_devside(DevSide* d) {
 }
 
 DevSide::~DevSide() {
-    if (worker.joinable()) worker.join();
+    stop_loader(*this);
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy) (void)hipStreamSynchronize(copy);
@@ -902,39 +920,95 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     return XS_OK;
 }
 
-// Load [lo, hi) into text slot ts on a worker thread.
-void start_prefetch(xs_fastx* r, size_t lo, size_t hi, int ts) {
+// The loader thread: loads queued windows in order until stopped.
+void loader_main(xs_fastx* r) {
     DevSide& d = *r->dev;
-    d.pending = true;
-    d.pf_lo = lo;
-    d.pf_hi = hi;
-    d.pf_slot = ts;
-    d.next_text = ts ^ 1;
-    d.worker = std::thread([r, lo, hi, ts] {
-        DevSide& dd = *r->dev;
+    std::unique_lock<std::mutex> g(d.pf_mu);
+    for (;;) {
+        DevSide::PfJob* job = nullptr;
+        d.pf_cv.wait(g, [&] {
+            if (d.pf_stop) return true;
+            for (auto& j : d.pf_q)
+                if (!j.started) {
+                    job = &j;  // deque references survive push_back and pop_front of others
+                    return true;
+                }
+            return false;
+        });
+        if (d.pf_stop) return;
+        job->started = true;
+        const size_t lo = job->lo, hi = job->hi;
+        const int slot = job->slot;
+        g.unlock();
         const double t0 = fx_ms();
-        dd.pf_rc = load_text(r, lo, hi, ts);
-        if (dd.pf_rc) dd.pf_err = xs_last_error();
+        const int rc = load_text(r, lo, hi, slot);
+        std::string err = rc ? xs_last_error() : "";
         if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f prefetch %zu+%zu done in %.2f ms\n", fx_ms(), lo, hi - lo,
                                 fx_ms() - t0);
+        g.lock();
+        job->rc = rc;
+        job->err = std::move(err);
+        job->done = true;
+        d.pf_cv.notify_all();
+    }
+}
+
+// Queue [lo, hi) for the next text slot (in window order).
+void queue_window(xs_fastx* r, size_t lo, size_t hi) {
+    DevSide& d = *r->dev;
+    {
+        std::lock_guard<std::mutex> g(d.pf_mu);
+        d.pf_q.push_back(DevSide::PfJob{lo, hi, d.next_text, false, false, XS_OK, std::string()});
+        d.next_text ^= 1;
+    }
+    if (!d.loader.joinable()) d.loader = std::thread(loader_main, r);
+    d.pf_cv.notify_all();
+}
+
+bool is_queued(DevSide& d, size_t lo) {
+    std::lock_guard<std::mutex> g(d.pf_mu);
+    for (const auto& j : d.pf_q)
+        if (j.lo == lo) return true;
+    return false;
+}
+
+// Wait for every queued load to finish and forget them.
+void drain_loads(DevSide& d) {
+    std::unique_lock<std::mutex> g(d.pf_mu);
+    d.pf_cv.wait(g, [&] {
+        for (const auto& j : d.pf_q)
+            if (!j.done && (j.started || !d.pf_stop)) return false;
+        return true;
     });
+    d.pf_q.clear();
 }
 
 // Wait for the text of [lo, hi) to be queued for its slot (loading it now if
-// no prefetch of exactly that window is pending); *ts = the slot.
-int text_for(xs_fastx* r, size_t lo, size_t hi, int* ts) {
+// it is not the oldest queued window); *ts = the slot, *prefetched = whether
+// it came from the queue.
+int text_for(xs_fastx* r, size_t lo, size_t hi, int* ts, bool* prefetched) {
     DevSide& d = *r->dev;
-    if (d.pending) {
-        d.worker.join();
-        d.pending = false;
-        if (d.pf_lo == lo && d.pf_hi == hi) {
-            *ts = d.pf_slot;
-            if (d.pf_rc) return xs::set_error(d.pf_rc, d.pf_err.c_str());
+    *prefetched = false;
+    {
+        std::unique_lock<std::mutex> g(d.pf_mu);
+        if (!d.pf_q.empty() && d.pf_q.front().lo == lo && d.pf_q.front().hi == hi) {
+            d.pf_cv.wait(g, [&] { return d.pf_q.front().done; });
+            DevSide::PfJob j = std::move(d.pf_q.front());
+            d.pf_q.pop_front();
+            *ts = j.slot;
+            *prefetched = true;
+            if (j.rc) return xs::set_error(j.rc, j.err.c_str());
             return XS_OK;
         }
     }
-    *ts = d.next_text;
-    d.next_text ^= 1;
+    // other windows than the queued ones (the caller changed its batch size):
+    // let those loads finish, then load this one here
+    drain_loads(d);
+    {
+        std::lock_guard<std::mutex> g(d.pf_mu);
+        *ts = d.next_text;
+        d.next_text ^= 1;
+    }
     return load_text(r, lo, hi, *ts);
 }
 
@@ -1280,10 +1354,7 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
     const char* end = r->base + r->stop;
     for (;;) {
         if (r->cur >= r->stop) {
-            if (d.pending) {
-                d.worker.join();
-                d.pending = false;
-            }
+            drain_loads(d);
             out->text_offset = r->cur;
             out->text_bytes = r->stop;
             return XS_OK;
@@ -1292,28 +1363,32 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
         const char* hi = window_end(r, lo, end, window_budget(max_text_bytes, r->windows));
         const size_t flo = (size_t)(lo - r->base), fhi = (size_t)(hi - r->base);
         const double t0 = fx_ms();
-        const bool prefetched = d.pending && d.pf_lo == flo && d.pf_hi == fhi;
+        bool prefetched = false;
         int ts = 0;
-        if (int rc = text_for(r, flo, fhi, &ts)) return rc;
+        if (int rc = text_for(r, flo, fhi, &ts, &prefetched)) return rc;
         const double t1 = fx_ms();
         r->cur = fhi;
         ++r->windows;
-        // the next window's text loads into the other slot while this one is
-        // parsed and the caller works on the batch
-        auto prefetch_next = [&] {
-            if (r->cur < r->stop) {
-                const char* nlo = r->base + r->cur;
-                const size_t nb = window_budget(max_text_bytes, r->windows);
-                start_prefetch(r, r->cur, (size_t)(window_end(r, nlo, end, nb) - r->base), ts ^ 1);
-            }
+        // The next window's text loads into the other slot while this one is
+        // parsed and the caller works on the batch; the one after it goes
+        // into this window's slot once this parse is done.
+        size_t n1_hi = 0;  // end of the next window
+        if (r->cur < r->stop)
+            n1_hi = (size_t)(window_end(r, r->base + r->cur, end, window_budget(max_text_bytes, r->windows)) - r->base);
+        auto queue_next = [&] {
+            if (n1_hi && !is_queued(d, r->cur)) queue_window(r, r->cur, n1_hi);
         };
         // one stream (XSPECT2_AMD_FX_ONE_STREAM): the next window's DMA queues
         // behind this window's parse on the same stream, so it starts after it
-        if (d.copy != d.stream) prefetch_next();
+        if (d.copy != d.stream) queue_next();
         bool ok = false;
         g_fx = FxTimes{};
         if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
-        if (d.copy == d.stream) prefetch_next();
+        if (d.copy == d.stream) queue_next();
+        if (n1_hi && n1_hi < r->stop && !is_queued(d, n1_hi))  // this slot's text is free now
+            queue_window(r, n1_hi,
+                         (size_t)(window_end(r, r->base + n1_hi, end, window_budget(max_text_bytes, r->windows + 1)) -
+                                  r->base));
         if (fx_trace())
             fprintf(stderr,
                     "[fastx-device] t=%.2f window %zu+%zu: text %s load %.2f ms, wait %.2f ms | count %.2f records %.2f "
