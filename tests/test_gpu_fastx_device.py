@@ -181,6 +181,32 @@ def test_large_windows_many_tiles(tmp_path):
         assert sum(b["n"] for b in dev) == n
 
 
+def test_batch_size_changes_between_calls(tmp_path):
+    """The reader loads up to two windows ahead for the batch size of the
+    last call; a caller that changes the size gets the windows of the new
+    size (the queued loads are finished and dropped), as the host reader."""
+    rng = np.random.default_rng(21)
+    p = tmp_path / "r.fastq"
+    p.write_bytes(_plain_fastq(rng, 4000))
+    sizes = [9000, 9000, 3000, 50_000, 50_000, 700, 1 << 20]
+
+    def run(device):
+        got = []
+        with FastxReader(p, device=device) as rd:
+            for k in range(64):
+                b = rd.next_batch(sizes[k % len(sizes)])
+                if b.n == 0:
+                    break
+                pr = b.to_host() if device is not None else b.packed
+                o = pr.offsets.astype(np.int64)
+                got.append((b.n, b.text_offset, pr.buf[:o[-1]].tobytes(), b.ids()))
+        return got
+
+    host, dev = run(None), run(0)
+    assert len(dev) == len(host) > 5
+    assert dev == host
+
+
 @pytest.mark.parametrize("inject", [None, b" ", b"\r"])
 def test_fasta_unwrapped_megabase_lines(tmp_path, inject):
     """Assemblies written one sequence line per contig: 2-3 Mbp lines are
