@@ -1117,6 +1117,7 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     if (int rc = d.id_offs[slot].ensure((n + 1) * 8)) return rc;
     if (int rc = d.desc_offs[slot].ensure((n + 1) * 8)) return rc;
     if (int rc = d.hoffs[slot].ensure((n + 1) * 8)) return rc;
+    const double t2a = fx_ms();
     uint8_t* seqs = d.seqs[slot].as<uint8_t>();
     if (fasta)
         FXCHK(xs::launch_fx_copy(text, d.line_src.as<uint32_t>(), d.line_ofs.as<uint64_t>(), L, sbytes, seqs, s));
@@ -1127,6 +1128,7 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     FXCHK(xs::launch_fx_copy(text, d.desc_src.as<uint32_t>(), d.desc_ofs.as<uint64_t>(), n, dbytes,
                              d.descs_d.as<uint8_t>(), s));
     FXCHK(hipEventRecord(d.kern_ev, s));  // the batch's device data: what the caller probes
+    const double t2b = fx_ms();
     // the host arrays land behind the caller's probe; xs_fastx_wait_host waits for them
     if (ibytes) FXCHK(hipMemcpyAsync(d.ids[slot].p, d.ids_d.p, ibytes, hipMemcpyDeviceToHost, s));
     if (dbytes) FXCHK(hipMemcpyAsync(d.descs[slot].p, d.descs_d.p, dbytes, hipMemcpyDeviceToHost, s));
@@ -1134,8 +1136,12 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     FXCHK(hipMemcpyAsync(d.desc_offs[slot].p, d.desc_ofs.p, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipMemcpyAsync(d.hoffs[slot].p, offs, (n + 1) * 8, hipMemcpyDeviceToHost, s));
     FXCHK(hipEventRecord(d.host_ev[slot], s));
+    const double t2c = fx_ms();
     FXCHK(hipEventSynchronize(d.kern_ev));
     g_fx.copy = fx_ms() - t2;
+    if (fx_trace())
+        fprintf(stderr, "[fastx-device] copy phase: buffers %.2f launches %.2f D2H queue %.2f wait %.2f ms\n", t2a - t2,
+                t2b - t2a, t2c - t2b, fx_ms() - t2c);
     out->host_ready = d.host_ev[slot];
     *ok = true;
     out->n = n;
