@@ -521,7 +521,6 @@ struct DevSide {
         std::string err;
     };
     std::thread loader;
-    std::thread warm;  // the first device-to-host copy of a new parse stream (see start_warm)
     std::mutex pf_mu;
     std::condition_variable pf_cv;
     std::deque<PfJob> pf_q;  // oldest first; popped by text_for once done
@@ -579,7 +578,6 @@ bool take_streams(DevSide& d) {
 // End the loader thread after the loads it has started (a queued load
 // that has not started is dropped), and forget the queue.
 void stop_loader(DevSide& d) {
-    if (d.warm.joinable()) d.warm.join();
     {
         std::lock_guard<std::mutex> g(d.pf_mu);
         d.pf_stop = true;
@@ -588,30 +586,6 @@ void stop_loader(DevSide& d) {
     if (d.loader.joinable()) d.loader.join();
     d.pf_stop = false;
     d.pf_q.clear();
-}
-
-// The first device-to-host copy of a few hundred KiB or more on a new parse
-// stream blocks its caller for ~5 ms (the runtime sets up that copy path;
-// traced as "D2H queue" in the second window of a process's first file,
-// profiles/r04_first_call_trace.txt).  A new device side makes that copy on
-// a helper thread while the caller's first window loads and parses.
-// XSPECT2_AMD_FX_WARM_D2H=0 turns it off.
-void start_warm(DevSide& d) {
-    static const bool on = [] {
-        const char* v = getenv("XSPECT2_AMD_FX_WARM_D2H");
-        return !(v && v[0] == '0');
-    }();
-    if (!on || !d.stream) return;
-    d.warm = std::thread([&d] {
-        if (hipSetDevice(d.device) != hipSuccess) return;
-        constexpr size_t kBytes = size_t(4) << 20;
-        DBuf src;
-        src.device = d.device;
-        PinBuf dst;
-        if (src.ensure(kBytes) || dst.ensure(kBytes)) return;  // buffers go back to the pool
-        if (hipMemcpyAsync(dst.p, src.p, kBytes, hipMemcpyDeviceToHost, d.stream) == hipSuccess)
-            (void)hipStreamSynchronize(d.stream);
-    });
 }
 
 std::mutex g_ds_mu;
@@ -1357,7 +1331,6 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
                            &r->dev->host_ev[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
     if (e != hipSuccess) return fail(e);
-    start_warm(*r->dev);
     return XS_OK;
 }
 
