@@ -405,11 +405,12 @@ BufPool g_pool;
 struct PinBuf {
     char* p = nullptr;
     size_t cap = 0;
-    int ensure(size_t bytes) {  // contents are not preserved
+    // contents are not preserved; exact: no 1/8 headroom (a fixed-size buffer)
+    int ensure(size_t bytes, bool exact = false) {
         if (bytes <= cap && p) return XS_OK;
         release();
         if ((p = static_cast<char*>(g_pool.take(bytes, -1, &cap)))) return XS_OK;
-        const size_t want = std::max<size_t>(bytes + bytes / 8, 1 << 16);
+        const size_t want = std::max<size_t>(exact ? bytes : bytes + bytes / 8, 1 << 16);
         const double t0 = fx_ms();
         if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
             p = nullptr;
@@ -853,7 +854,7 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     DBuf& text = d.text[ts];
     const size_t R = ring_pieces();
     if (R) {
-        if (int rc = d.ring.ensure(R * kPieceBytes)) return rc;
+        if (int rc = d.ring.ensure(R * kPieceBytes, true)) return rc;
         for (size_t i = 0; i < R; ++i)
             if (!d.ring_ev[i]) FXCHK(hipEventCreateWithFlags(&d.ring_ev[i], hipEventDisableTiming));
     } else if (int rc = d.pin[ts].ensure(span + 1)) {
