@@ -17,7 +17,15 @@ synthetic 150 bp reads per GPU against a D=100 species COBS classic bank
 the 256 MiB Infinity Cache).  One step = one query of the whole read batch,
 resident in HBM (units -> scan -> scatter -> probe -> totals).  With N>1
 ranks the D+1 per-doc totals (the input of the SVM vector) are all-reduced
-over RCCL: reads sharded (seed 42+rank), bank replicated, weak scaling.
+over RCCL: reads sharded (seed 42+rank), bank replicated, weak scaling; at
+N > 1 each rank takes 12.5M reads by default, so N=8 is BASELINE.json
+configs[2] (config 3: 100M reads over 8 GPUs) at its stated size.
+
+Every rank checks its own values after the timed region (`checks`): its hit
+rows of 3,000 reads against the C oracle, its local totals against its hit
+matrix, and (rank 0) the all-reduced totals against the host sum of the
+all-gathered per-rank totals; multigenus checks its exchanged column blocks
+by checksums.  A failed check prints the line and exits with status 3.
 
 Other workloads (SURVEY.md §8(d) configs 4/5 and the genus path):
   genus       rbloom filter over all 100 genomes (k=21, fpr=0.01), D=1
@@ -78,6 +86,8 @@ SURVEY_ROW_BYTES = 64
 # Rehearsal of the N>1 path on a one-GPU box: every rank on cuda:0, gloo
 # collectives through host copies (RCCL does not share a device between ranks).
 SHARE_GPU = os.environ.get("XSPECT_BENCH_SHARE_GPU") == "1"
+# BASELINE.json configs[2]: 100M reads sharded over 8 GPUs = 12.5M per GPU
+CONFIG3_READS_PER_GPU = 12_500_000
 
 
 def parse():
@@ -86,7 +96,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="species", choices=["species", "genus", "mlst", "multigenus"])
-    ap.add_argument("--reads", type=int, default=1_000_000, help="reads per GPU")
+    ap.add_argument("--reads", type=int, default=None,
+                    help="reads per GPU (default: 1M at --gpus 1 = config 2; species at --gpus N > 1: 12.5M, "
+                         "so N=8 is config 3's 100M reads; other workloads 1M)")
     ap.add_argument("--read-len", type=int, default=150)
     ap.add_argument("--docs", type=int, default=100)
     ap.add_argument("--genome-len", type=int, default=4_000_000)
@@ -99,6 +111,8 @@ def parse():
                     help="mlst: fraction of reads from outside every locus (WGS-like input: ~1.0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline time")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--check-reads", type=int, default=3000,
+                    help="reads per rank whose GPU hit rows are compared with the C oracle (every N)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the PCIe-inclusive host-buffer runs (profiling: only full-size probe launches)")
     ap.add_argument("--no-e2e", action="store_true",
@@ -108,7 +122,11 @@ def parse():
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r04_traffic.json"))
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launched N>1 runs: seconds before the parent kills every rank")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.reads is None:
+        n_gpus = int(os.environ.get("WORLD_SIZE", args.gpus))
+        args.reads = CONFIG3_READS_PER_GPU if (n_gpus > 1 and args.workload == "species") else 1_000_000
+    return args
 
 
 def free_port() -> int:
@@ -245,6 +263,7 @@ class Workload:
                     self.kernel = f"probe_cobs (k={self.k}, h={h}, D={args.docs})"
             torch.cuda.synchronize(dev)
             del g_dev
+            log(rank, f"bank built ({bank.info.device_bytes / 1e9:.2f} GB); generating {args.reads} reads per rank")
             self.banks = [bank]
             rseed = 42 if w == "multigenus" else 42 + rank  # multigenus: same reads on every rank
             reads, _ = make_reads(genomes if w != "multigenus" else make_genomes(args.docs, args.genome_len, 42),
@@ -374,6 +393,12 @@ class Workload:
         return sum(per_bank) / len(per_bank)
 
 
+def build_id() -> str:
+    """The loaded library's build id (a hash of its sources, xspect2_amd/build.py)."""
+    from xspect2_amd import _lib
+    return _lib.build_id()
+
+
 def check_distinct_devices(dev) -> list[str]:
     """PCI address of every rank's GPU (all-gathered); raises if two ranks
     drive the same device, which would make an N-GPU line an N-rank-on-one-GPU
@@ -474,6 +499,8 @@ def main():
         assert int(tot[-1]) == want, f"k-mer total {int(tot[-1])} != {want}"
     if args.workload == "genus":  # member k-mers / sampled k-mers (steers the rbloom probe path)
         wl.config["member_fraction"] = round(int(tot[0]) / max(1, int(tot[-1])), 4)
+    # every rank checks its own values (oracle sample, totals, exchanged columns); outside the timed region
+    checks = self_check(wl, args, rank, world, dev)
 
     value = wl.probes_per_step() * args.steps / elapsed
     from xspect2_amd._lib import XS_PATH_PARTITIONED
@@ -546,6 +573,9 @@ def main():
                                    "scaled by k-mers); peak = pure L2 gathers, profiles/r02_l2gather.txt"}
         except Exception:
             lookup_l2 = None
+    if world > 1:
+        # the PMC files are one-GPU, 1M-read measurements: they describe no rank of this run
+        traffic, lookup_l2 = None, None
     # the PCIe-inclusive legs are a per-GPU figure: measured at N=1 only
     host = None if args.no_host_path or world > 1 else host_path(wl, args)
     e2e = None
@@ -557,11 +587,15 @@ def main():
         cpu = cpu_baseline(wl, args)
 
     nr = f"{wl.n / 1e6:g}M x {args.read_len}bp reads"
-    species_cfg = ("config3 per-GPU shard (100M reads / 8 GPUs)" if wl.n == 12_500_000 else
-                   "config2" if wl.n == 1_000_000 else "species")
-    if world > 1:
-        species_cfg += f" per GPU, reads sharded over {world} GPUs (config 3's layout)"
-    names = {"species": f"{species_cfg}: {nr}/GPU vs D={args.docs} COBS classic species bank",
+    if world > 1 and wl.n == CONFIG3_READS_PER_GPU:
+        species_cfg = (f"config3: {wl.n * world / 1e6:g}M x {args.read_len}bp reads sharded over {world} GPUs "
+                       f"({nr}/GPU; N=8 = BASELINE configs[2]'s 100M)")
+    elif world > 1:
+        species_cfg = f"species: {nr}/GPU sharded over {world} GPUs (config 3's layout, not its size)"
+    else:
+        species_cfg = ("config3 per-GPU shard (100M reads / 8 GPUs)" if wl.n == CONFIG3_READS_PER_GPU else
+                       "config2" if wl.n == 1_000_000 else "species") + f": {nr}/GPU"
+    names = {"species": f"{species_cfg} vs D={args.docs} COBS classic species bank",
              "genus": f"genus path: {nr}/GPU vs rbloom filter over {args.docs} genomes",
              "mlst": f"config4: {nr}/GPU vs 7 loci x 1430 alleles (COBS compact)",
              "multigenus": f"config5: {nr} vs one {args.docs}-species bank per GPU, hit columns exchanged to the reads' ranks"}
@@ -584,6 +618,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
+        "build_id": build_id(),
         "data": "synthetic (seeded genomes + reads, no network)",
         "config": {
             "workload": names[args.workload],
@@ -596,6 +631,8 @@ def main():
             "bound": "mall" if args.workload == "mlst" else "hbm", "achieved": achieved, "peak": peak,
             "unit": "GB/s", "frac": achieved / peak, "traffic": traffic,
             "traffic_frac": (traffic / (probe_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if traffic else None,
+            **({"traffic_note": "traffic, traffic_frac and lookup_l2 are one-GPU PMC figures (profiles/): "
+                                "not reported at N > 1"} if world > 1 else {}),
             "frac_basis": ("frac = SURVEY.md §8(d)-priced algorithmic bytes / probe time / peak; traffic_frac = "
                            "PMC-measured HBM bytes of the same probe (traffic) / probe time / 8 TB/s: the bytes "
                            "the pipeline really moves, intermediates included" if traffic else
@@ -607,6 +644,7 @@ def main():
             **({"note": wl.roofline_note} if wl.roofline_note else {}),
         },
         "cpu_baseline": cpu,
+        "checks": checks,
         "host_path": host,
         "end_to_end": e2e,
     }
@@ -616,24 +654,126 @@ def main():
         b.close()
     if world > 1:
         dist.destroy_process_group()
+    if not checks["ok"]:
+        sys.exit(3)
+
+
+def oracle_banks(wl):
+    """The C oracle over copies of this rank's banks (checker + CPU baseline only)."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle
+    if getattr(wl, "_obanks", None) is None:
+        wl._obanks = []
+        for b in wl.banks:
+            inf = b.info
+            if inf.kind == 2:
+                wl._obanks.append(oracle.BloomFilter(b.download(), int(inf.num_hashes), int(inf.term_size)))
+            else:
+                wl._obanks.append(oracle.CobsBank(b.download(), b.signature_sizes(), int(inf.page_size),
+                                                  int(inf.num_docs), int(inf.num_hashes), int(inf.term_size)))
+    return wl._obanks
+
+
+def _checksum(x, row0: int):
+    """Position-weighted int64 checksum of an integer matrix block whose first
+    row is row `row0` of its job-wide matrix (equal blocks <=> equal sums, up to
+    collisions ~2^-63): sum of value * (global row * 1000003 + col + 1)."""
+    import torch
+    n, d = x.shape
+    r = torch.arange(row0, row0 + n, dtype=torch.int64, device=x.device)[:, None]
+    c = torch.arange(d, dtype=torch.int64, device=x.device)[None, :]
+    return int((x.to(torch.int64) * (r * 1000003 + c + 1)).sum().item())
+
+
+def self_check(wl, args, rank, world, dev):
+    """Every rank checks the values of its last step (outside the timed region):
+
+    * its GPU hit rows of `--check-reads` reads spread over its shard against
+      the C oracle on a copy of its bank (mismatching (read, doc) cells);
+    * read-sharded workloads: its local D+1 totals (one more query, no
+      collective) against the column sums of its hit matrix and its k-mer
+      counts; then rank 0 compares the all-reduced totals of the timed steps
+      with the host sum of every rank's all-gathered local totals
+      (result.py:76-90: the job totals the all-reduce must reproduce);
+    * multigenus at N > 1: the exchanged columns against the rows each rank
+      sent, by position-weighted checksums of every (bank rank, read rank)
+      block, all-gathered (a checksum of checksums).
+    Returns rank 0's view: every rank's counts, and `ok`."""
+    import torch
+    import torch.distributed as dist
+    from xspect2_amd.packing import pack_fixed
+
+    m = min(wl.n, max(0, args.check_reads))
+    idx = np.unique(np.linspace(0, wl.n - 1, m).astype(np.int64)) if m else np.zeros(0, np.int64)
+
+    def oracle_sample():
+        mism, cells = 0, 0
+        if idx.size:
+            pr = pack_fixed(wl.reads[idx])
+            for ob, d_h in zip(oracle_banks(wl), wl.d_hits):
+                hits, _ = ob.query_packed(pr.buf, pr.offsets, step=args.step, threads=host_cpus()["share"])
+                gpu = d_h[torch.from_numpy(idx).to(d_h.device)].cpu().numpy().view(np.uint32)
+                mism += int(np.count_nonzero(gpu != hits.reshape(gpu.shape)))
+                cells += gpu.size
+        return {"oracle_sample_reads": int(idx.size), "oracle_sample_cells": cells, "oracle_mismatches": mism}
+
+    mine = {}
+    if args.workload != "multigenus":
+        # local totals of one more query against the local hit matrix
+        bad_local = 0
+        local = []
+        for b, h, t in zip(wl.banks, wl.d_hits, wl.d_tot):
+            lt = torch.zeros_like(t)
+            b.query_device(wl.d_seqs, wl.seq_bytes, wl.d_offs, wl.n, args.step, h, wl.d_nk, lt,
+                           stream=wl.stream)
+            torch.cuda.synchronize(dev)
+            want = torch.cat([h.view(torch.int32).to(torch.int64).sum(0), wl.d_nk.sum().reshape(1)])
+            bad_local += int((lt != want).sum().item())
+            local.append(lt)
+        mine.update(oracle_sample())  # the hit rows this query wrote (also under --totals-only)
+        mine["local_totals_mismatches"] = bad_local
+        loc = torch.cat(local).cpu()
+        if world > 1:
+            parts = [torch.zeros_like(loc) for _ in range(world)]
+            dist.all_gather(parts, loc.to(dev) if dist.get_backend() == "nccl" else loc)
+            host_sum = np.sum([p.cpu().numpy().view(np.uint64) for p in parts], axis=0, dtype=np.uint64)
+        else:
+            host_sum = loc.numpy().view(np.uint64)
+        reduced = torch.cat([t.cpu() for t in wl.d_tot]).numpy().view(np.uint64)
+        mine["allreduce_vs_host_sum_mismatches"] = int(np.count_nonzero(reduced != host_sum))
+    else:
+        mine.update(oracle_sample())
+    if args.workload == "multigenus" and world > 1:
+        from xspect2_amd.distributed import shard_range
+        sent = torch.tensor([_checksum(wl.d_hits[0][a:b], a) for a, b in
+                             (shard_range(wl.n, q, world) for q in range(world))], dtype=torch.int64)
+        got = [torch.zeros_like(sent) for _ in range(world)]
+        dist.all_gather(got, sent.to(dev) if dist.get_backend() == "nccl" else sent)
+        a, _ = shard_range(wl.n, rank, world)
+        bad, c0 = 0, 0
+        for r, d in enumerate(wl.layout[0]):
+            bad += int(_checksum(wl.exchanged[:, c0:c0 + d], a) != int(got[r][rank].item()))
+            c0 += d
+        mine["exchange_block_mismatches"] = bad
+    keys = sorted(k for k in mine if k.endswith("mismatches"))
+    if world > 1:
+        allm: list = [None] * world
+        dist.all_gather_object(allm, mine)
+    else:
+        allm = [mine]
+    out = {"per_rank": allm, "ok": all(r[k] == 0 for r in allm for k in keys)}
+    if rank == 0 and not out["ok"]:
+        print(f"bench self-check FAILED: {allm}", file=sys.stderr, flush=True)
+    return out
 
 
 def cpu_baseline(wl, args):
     """Oracle C restatement on a bounded sample of the same reads (rank 0, N=1)."""
-    sys.path.insert(0, str(ROOT / "oracle"))
-    import oracle  # checker + CPU baseline only
     from xspect2_amd.packing import pack_fixed
 
     cpus = host_cpus()
     threads = cpus["share"]
-    obanks = []
-    for b in wl.banks:
-        inf = b.info
-        if inf.kind == 2:
-            obanks.append(oracle.BloomFilter(b.download(), int(inf.num_hashes), int(inf.term_size)))
-        else:
-            obanks.append(oracle.CobsBank(b.download(), b.signature_sizes(), int(inf.page_size), int(inf.num_docs),
-                                          int(inf.num_hashes), int(inf.term_size)))
+    obanks = oracle_banks(wl)
 
     def run(m):
         pr = pack_fixed(wl.reads[:m])

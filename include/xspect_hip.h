@@ -79,6 +79,12 @@ typedef struct xs_bank_info_t {
 } xs_bank_info_t;
 
 int xs_version(void);
+/* Build id: the first 16 hex digits of a SHA-256 over the library's sources,
+ * headers, compiler flags and target, fixed when it was built
+ * (xspect2_amd/build.py: source_id).  No reference counterpart: the
+ * reference's native dependencies are unpinned (pyproject.toml:16-17), this
+ * names exactly which sources a loaded library came from. */
+const char* xs_build_id(void);
 const char* xs_last_error(void);
 int xs_device_count(int* count);
 

@@ -18,6 +18,7 @@ import textwrap
 import time
 from pathlib import Path
 
+import numpy as np
 import pytest
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -109,3 +110,40 @@ def test_bench_self_launches_and_fails_loudly_without_a_gpu():
     assert p.returncode != 0
     assert "exited with" in p.stderr
     assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.parametrize("argv,env_world,want", [
+    (["--gpus", "1"], None, 1_000_000),                          # config 2
+    (["--gpus", "8"], None, bench.CONFIG3_READS_PER_GPU),        # config 3: 100M reads over 8 GPUs
+    (["--gpus", "2"], "2", bench.CONFIG3_READS_PER_GPU),
+    (["--gpus", "1"], "4", bench.CONFIG3_READS_PER_GPU),         # torchrun's WORLD_SIZE wins
+    (["--gpus", "8", "--workload", "genus"], None, 1_000_000),
+    (["--gpus", "8", "--reads", "5000"], None, 5000),
+])
+def test_reads_default_follows_world_size(monkeypatch, argv, env_world, want):
+    """N > 1 species runs default to config 3's per-GPU share (BASELINE.json configs[2])."""
+    if env_world is None:
+        monkeypatch.delenv("WORLD_SIZE", raising=False)
+    else:
+        monkeypatch.setenv("WORLD_SIZE", env_world)
+    monkeypatch.setattr(sys, "argv", ["bench.py", *argv])
+    assert bench.parse().reads == want
+    assert bench.CONFIG3_READS_PER_GPU * 8 == 100_000_000
+
+
+def test_block_checksum_sees_moved_and_changed_cells():
+    """The multigenus exchange check: equal blocks give equal sums; a changed
+    cell, swapped cells or a shifted block origin do not."""
+    import torch
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.integers(0, 131, (300, 40)).astype(np.int32))
+    base = bench._checksum(x, 1000)
+    assert base == bench._checksum(x.to(torch.uint8), 1000)      # the narrow wire type carries the same sum
+    y = x.clone()
+    y[7, 3] += 1
+    assert bench._checksum(y, 1000) != base
+    z = x.clone()
+    z[[7, 8]] = z[[8, 7]]
+    if not torch.equal(z, x):
+        assert bench._checksum(z, 1000) != base
+    assert bench._checksum(x, 999) != base

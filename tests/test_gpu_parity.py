@@ -81,28 +81,17 @@ def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig)
 
 @pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
                                                                                   (64, 31, 8, [300_007])])
-@pytest.mark.parametrize("ck,ws_mb,lookup,pad", [("1024", None, None, None), ("2048", None, None, None),
-                                                 ("4096", None, None, None), ("2048", "1", None, None),
-                                                 ("1024", "2", None, None), ("2048", None, "1", None),
-                                                 ("2048", None, None, "1"), ("4096", "2", "1", "1"),
-                                                 ("2048", None, "5", None), ("1024", "2", "5", None),
-                                                 ("4096", None, "5", "1"), ("2048", None, "6", None)])
-def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, ws_mb, lookup,
-                                                  pad):
+@pytest.mark.parametrize("mode,ws_mb", [("3", None), ("3", "1"), ("3", "2"), ("4", None), ("4", "2")])
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, mode, ws_mb):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
     L2-resident lookup, per-block AND + count) with partitions down to 1024
-    rows, every bucket block size, and workspaces of 1-2 MiB (the bucket
-    blocks then run in ranges of a few blocks that reuse it), partition runs
-    padded to 4 entries (default) and unpadded, on the classic cases of <= 128
-    docs: same hits, counts and totals."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
-    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
+    rows (mode 3) or of exactly 1024 rows (mode 4: banks over 512 Ki rows get
+    more than 512 partitions, whose runs are not padded), and workspaces of
+    1-2 MiB (the bucket blocks then run in ranges of a few blocks that reuse
+    it), on the classic cases of <= 128 docs: same hits, counts and totals."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    if lookup:  # 1: the register-gather lookup instead of LDS-DMA; 5, 6: LDS entry -> block map
-        monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
-    if pad:  # runs not padded to 64-B row pieces
-        monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)
     _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
 
 
@@ -114,55 +103,42 @@ def _random_partitioned_configs(n=48, seed=20261017):
         k = int(rng.integers(5, 33))
         h = int(rng.integers(1, 9))
         sig = int(rng.integers(1_000, 200_001))
-        ck = str(int(rng.choice([1024, 2048, 4096])))
-        lookup = str(int(rng.choice([0, 5, 6])))
+        mode = str(int(rng.choice([3, 4])))
         ws_mb = [None, "1", "2"][int(rng.integers(0, 3))]
-        pad = [None, "1"][int(rng.integers(0, 2))]
-        out.append((D, k, h, sig, ck, lookup, ws_mb, pad))
+        out.append((D, k, h, sig, mode, ws_mb))
     return out
 
 
-@pytest.mark.parametrize("D,k,h,sig,ck,lookup,ws_mb,pad", _random_partitioned_configs())
-def test_partitioned_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, sig, ck, lookup, ws_mb, pad):
+@pytest.mark.parametrize("D,k,h,sig,mode,ws_mb", _random_partitioned_configs())
+def test_partitioned_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, sig, mode, ws_mb):
     """Seeded random configurations of the partitioned COBS probe (docs 1-128,
-    k 5-32, h 1-8, 1 k-200 k rows in partitions down to 1024 rows, every
-    bucket block size, the entry-map lookups (5, 6) and the binary-search one
-    (0), small workspaces that force block ranges, padded and unpadded runs):
+    k 5-32, h 1-8, 1 k-200 k rows in partitions down to 1024 rows or of 1024
+    rows, small workspaces that force block ranges, padded and unpadded runs):
     same hits, k-mer counts and totals as the oracle at steps 1, 2 and 7."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
-    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
-    monkeypatch.setenv("XSPECT2_AMD_CP_LOOKUP", lookup)
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
     if ws_mb:
         monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    if pad:
-        monkeypatch.setenv("XSPECT2_AMD_CP_PAD", pad)
     _classic_case(xs, oracle_mod, D, k, h, [sig], want_path=1)
 
 
-@pytest.mark.parametrize("shift,D", [("10", 100), ("11", 100), ("10", 117), ("11", 128), ("12", 64)])
-def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, shift, D):
-    """A 1 M-row bank cut into 1024-row partitions (977 of them: more than
-    kCobsPadParts = 512, so the runs are not padded) and 2048-/4096-row
-    partitions (489 / 245: padded with all-ones pad rows), with the k-mer id
-    in the row's top bits (D <= 117) and in the entries (D = 128): same hits,
+@pytest.mark.parametrize("mode,D", [("4", 100), ("4", 117), ("4", 128), ("3", 64), ("3", 128)])
+def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, mode, D):
+    """A 1 M-row bank cut into 1024-row partitions (mode 4: 977 of them, more
+    than kCobsPadParts = 512, so the runs are not padded) and into 64
+    partitions (mode 3: padded with all-ones pad rows), with the k-mer id in
+    the row's top bits (D <= 117) and in the entries (D = 128): same hits,
     counts and totals as the oracle."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
-    monkeypatch.setenv("XSPECT2_AMD_CP_SHIFT", shift)
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
     _classic_case(xs, oracle_mod, D, 21, 7, [1_000_003], want_path=1)
 
 
-@pytest.mark.parametrize("shift,ck,want_path", [("20", "2048", 1), ("21", "2048", 0), ("20", "4096", 0),
-                                                ("21", "1024", 1)])
-def test_partition_entry_width_limit(xs, oracle_mod, monkeypatch, shift, ck, want_path):
-    """Entries are (row in partition << log2(CK)) | k-mer in block: a plan whose
-    entry would fill all 32 bits (shift + log2(CK) == 32) could produce the
-    all-ones pad sentinel for a real entry, so it falls back to the direct
-    probe; one bit less takes the partitioned path.  Bank of 2^22 + 15 rows
-    (more than one 2^21-row partition); same hits as the oracle either way."""
+def test_partitioned_largest_partitions(xs, oracle_mod, monkeypatch):
+    """A bank of 2^27 + 15 rows (2 GiB on the device): 1025 partitions of 2^17
+    rows would exceed kPartMax = 1024, so the plan doubles them to 2^18 rows
+    (513 partitions: more than kCobsPadParts, unpadded runs); same hits as
+    the oracle."""
     monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
-    monkeypatch.setenv("XSPECT2_AMD_CP_SHIFT", shift)
-    monkeypatch.setenv("XSPECT2_AMD_CP_CK", ck)
-    _classic_case(xs, oracle_mod, 100, 21, 7, [(1 << 22) + 15], want_path=want_path)
+    _classic_case(xs, oracle_mod, 100, 21, 7, [(1 << 27) + 15], want_path=1)
 
 
 def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
@@ -236,7 +212,6 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     from xspect2_amd import _lib
     from xspect2_amd.packing import pack_sequences
     monkeypatch.delenv("XSPECT2_AMD_COBS_PART", raising=False)
-    monkeypatch.delenv("XSPECT2_AMD_CP_CK", raising=False)
     D, k, h, sig = 100, 21, 7, 17_000_011
     rng = np.random.default_rng(2024)
     nb = sig * 13
@@ -340,15 +315,10 @@ def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
     gb2.close()
 
 
-@pytest.mark.parametrize("mode", ["0", "3", "3s"])
+@pytest.mark.parametrize("mode", ["0", "3"])
 @pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
 def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode):
-    """mode 0: direct probe; mode 3: partitioned probe with small partitions
-    (lookup with the LDS entry -> block map); 3s: the same with the lookup's
-    shuffle binary search (XSPECT2_AMD_BL_LOOKUP=0)."""
-    if mode == "3s":
-        mode = "3"
-        monkeypatch.setenv("XSPECT2_AMD_BL_LOOKUP", "0")
+    """mode 0: direct probe; mode 3: partitioned probe with small partitions."""
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
@@ -373,17 +343,15 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
 def _random_bloom_configs(n=24, seed=1017):
     rng = np.random.default_rng(seed)
     return [(int(rng.integers(5, 33)), int(rng.integers(1_000, 2_000_001)), int(rng.integers(1, 9)),
-             str(int(rng.integers(0, 2))), int(rng.integers(0, 1_000_000))) for _ in range(n)]
+             int(rng.integers(0, 1_000_000))) for _ in range(n)]
 
 
-@pytest.mark.parametrize("k,nbytes,K,bl_lookup,seed", _random_bloom_configs())
-def test_bloom_partitioned_random_configs(xs, oracle_mod, monkeypatch, k, nbytes, K, bl_lookup, seed):
+@pytest.mark.parametrize("k,nbytes,K,seed", _random_bloom_configs())
+def test_bloom_partitioned_random_configs(xs, oracle_mod, monkeypatch, k, nbytes, K, seed):
     """Seeded random rbloom filters (k 5-32, 1 kB-2 MB, K 1-8 bit indices)
-    through the partitioned probe with small partitions, entry-map (1) and
-    binary-search (0) lookups; mixed-case / IUPAC reads: same hits, counts
-    and totals as the oracle at steps 1 and 3."""
+    through the partitioned probe with small partitions; mixed-case / IUPAC
+    reads: same hits, counts and totals as the oracle at steps 1 and 3."""
     monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
-    monkeypatch.setenv("XSPECT2_AMD_BL_LOOKUP", bl_lookup)
     rng = np.random.default_rng(seed)
     genome = _reads(rng, 8, k, alphabet="ACGTacgtN", min_len=k, max_len=5000)
     bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)

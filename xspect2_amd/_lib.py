@@ -7,7 +7,6 @@ object is missing or cannot be loaded, importing this module raises.
 from __future__ import annotations
 
 import ctypes
-import os
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -102,6 +101,7 @@ _pp = ctypes.POINTER(ctypes.c_void_p)
 # name -> (restype, argtypes); every symbol of include/xspect_hip.h
 SIGNATURES = {
     "xs_version": (_int, []),
+    "xs_build_id": (ctypes.c_char_p, []),
     "xs_last_error": (ctypes.c_char_p, []),
     "xs_device_count": (_int, [ctypes.POINTER(_int)]),
     "xs_bank_open": (_int, [ctypes.c_char_p, _int, _int, _pp]),
@@ -163,22 +163,16 @@ def load() -> ctypes.CDLL:
     if _LIB is not None:
         return _LIB
     path = SO_PATH
-    variant = os.environ.get("XSPECT2_AMD_LIB_VARIANT")  # A/B runs: libxspect_hip.<variant>.so in-tree
-    if variant:
-        path = SO_PATH.with_name(f"libxspect_hip.{variant}.so")
-        if not path.exists():
-            raise ImportError(f"{path} is missing")
     if not path.exists():
         raise ImportError(
             f"{SO_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the probe path has no CPU fallback)")
     # torch (if present) must own the HIP runtime first: libamdhip64.so.7 is
     # then shared by soname instead of loading a second copy from /opt/rocm.
-    if os.environ.get("XSPECT2_AMD_NO_TORCH_PRELOAD") is None:
-        try:
-            import torch  # noqa: F401
-        except Exception:  # pragma: no cover - torch is optional for the ABI
-            pass
+    try:
+        import torch  # noqa: F401
+    except Exception:  # pragma: no cover - torch is optional for the ABI
+        pass
     lib = ctypes.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
@@ -192,6 +186,11 @@ def check(rc: int) -> None:
     if rc != XS_OK:
         msg = load().xs_last_error()
         raise XsError(rc, msg.decode() if msg else "unknown error")
+
+
+def build_id() -> str:
+    """The loaded library's build id (xspect2_amd.build.source_id of its sources)."""
+    return load().xs_build_id().decode()
 
 
 def device_count() -> int:

@@ -23,9 +23,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <deque>
 #include <fstream>
 #include <memory>
 #include <mutex>
@@ -166,8 +168,8 @@ struct xs_bank {
     bool bloom_pending = false;
     double member_frac = 1.0;
     int last_path = XS_PATH_GATHER;
-    PinnedBuf stage[2];             // D2H staging ring for large host outputs
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};
+    PinnedBuf stage[3];             // D2H staging ring for large host outputs (d2h_pageable: 2, HitSink: 3)
+    hipEvent_t stage_ev[3] = {nullptr, nullptr, nullptr};
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
     PinnedBuf small_h;              // small host calls: the whole request and its results (query_small)
     PinnedBuf cut_ofs;              // device-read batches: read offsets at the chunk cuts
@@ -704,6 +706,172 @@ int host_threads() {
     return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
 }
 
+// ---- hit rows back to a host array, behind the probe ------------------------
+// A host call's hit rows go to the caller's array on a worker thread while the
+// bank stream probes the next chunks (the main thread only launches): each
+// chunk's rows, in the wire width (uint8 / uint16 narrowed on the device when
+// every read's sampled k-mers fit, else uint32), are cut into pieces of
+// kSinkPiece bytes, DMA'd on d2h_stream into a ring of three pinned slots (two
+// pieces in flight while a third is copied out) and copied by host threads
+// into the caller's array, widened to its element width where the wire is
+// narrower.  A pinned destination of the wire width takes the DMA directly.
+// xs_query's uint32 matrix of 1 M reads x 100 docs thus crosses PCIe as 100 MB
+// of uint8 instead of 400 MB, and its copy-out overlaps the probe.
+constexpr size_t kSinkPiece = 32u << 20;
+constexpr int kSinkSlots = 3;
+
+template <class S, class D>
+void widen_rows(D* dst, const S* src, size_t n, int threads) {
+    auto run = [=](size_t a, size_t e) {
+        for (size_t i = a; i < e; ++i) dst[i] = (D)src[i];
+    };
+    if (n < (1u << 20) || threads <= 1) {
+        run(0, n);
+        return;
+    }
+    const size_t per = (n + threads - 1) / threads;
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
+    run(0, std::min(per, n));
+    for (auto& x : th) x.join();
+}
+
+class HitSink {
+  public:
+    // rows of `cols` counts: on the device at `src` (wire bytes each), to `host` (out bytes each)
+    HitSink(xs_bank* b, void* host, const void* src, uint64_t cols, int wire, int out)
+        : b_(b), host_(static_cast<uint8_t*>(host)), src_(static_cast<const uint8_t*>(src)), cols_(cols),
+          wire_(wire), out_(out) {}
+    HitSink(const HitSink&) = delete;
+    HitSink& operator=(const HitSink&) = delete;
+    ~HitSink() { (void)finish(); }
+
+    int start(uint64_t total_bytes_out) {
+        if (wire_ == out_ && total_bytes_out >= 2 * kSinkPiece) {
+            hipPointerAttribute_t attr;
+            if (hipPointerGetAttributes(&attr, host_) == hipSuccess) direct_ = attr.type == hipMemoryTypeHost;
+            else (void)hipGetLastError();  // pageable memory is "not a HIP pointer"
+        } else if (wire_ == out_) {
+            direct_ = true;  // small: one DMA into pageable memory is as fast as staging it
+        }
+        if (!direct_)
+            for (int s = 0; s < kSinkSlots; ++s) {
+                if (int rc = b_->stage[s].ensure(kSinkPiece)) return rc;
+                if (!b_->stage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b_->stage_ev[s], hipEventDisableTiming));
+            }
+        th_ = std::thread([this] { run(); });
+        return XS_OK;
+    }
+    // rows [r0, r1) are complete on the device once `ev` has fired
+    void push(uint64_t r0, uint64_t r1, hipEvent_t ev) {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            q_.push_back(Job{r0, r1, ev});
+        }
+        cv_.notify_one();
+    }
+    // no more rows: wait for the copies; the worker's error, if any, becomes this thread's
+    int finish() {
+        if (!th_.joinable()) return XS_OK;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            closed_ = true;
+        }
+        cv_.notify_one();
+        th_.join();
+        return rc_ ? xs::set_error(rc_, err_.c_str()) : XS_OK;
+    }
+
+  private:
+    struct Job {
+        uint64_t r0, r1;
+        hipEvent_t ev;
+    };
+    struct Piece {
+        int slot;
+        uint64_t elem0, elems;  // first element and count
+    };
+    int copy_out(const Piece& p) {
+        if (hipEventSynchronize(b_->stage_ev[p.slot]) != hipSuccess) return XS_ERR_HIP;
+        const void* in = b_->stage[p.slot].p;
+        const int t = threads_;
+        if (wire_ == out_) par_memcpy(host_ + p.elem0 * out_, in, p.elems * out_, t);
+        else if (wire_ == 1 && out_ == 2) widen_rows(reinterpret_cast<uint16_t*>(host_) + p.elem0, static_cast<const uint8_t*>(in), p.elems, t);
+        else if (wire_ == 1) widen_rows(reinterpret_cast<uint32_t*>(host_) + p.elem0, static_cast<const uint8_t*>(in), p.elems, t);
+        else widen_rows(reinterpret_cast<uint32_t*>(host_) + p.elem0, static_cast<const uint16_t*>(in), p.elems, t);
+        return XS_OK;
+    }
+    void fail_with(int rc, const char* what) {
+        if (!rc_) {
+            rc_ = rc;
+            err_ = what;
+        }
+    }
+    void run() {
+        if (hipSetDevice(b_->device) != hipSuccess) return fail_with(XS_ERR_HIP, "hipSetDevice failed in the hit copier");
+        std::deque<Piece> inflight;
+        int next_slot = 0;
+        for (;;) {
+            Job j;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return closed_ || !q_.empty(); });
+                if (q_.empty()) break;
+                j = q_.front();
+                q_.pop_front();
+            }
+            if (rc_) continue;  // drain the queue after a failure
+            hipError_t e = hipStreamWaitEvent(b_->d2h_stream, j.ev, 0);
+            const uint64_t e0 = j.r0 * cols_, e1 = j.r1 * cols_;
+            const uint64_t per = kSinkPiece / (uint64_t)wire_;
+            for (uint64_t a = e0; e == hipSuccess && a < e1; a += per) {
+                const uint64_t m = std::min(per, e1 - a);
+                if (direct_) {
+                    e = hipMemcpyAsync(host_ + a * out_, src_ + a * wire_, m * wire_, hipMemcpyDeviceToHost,
+                                       b_->d2h_stream);
+                    continue;
+                }
+                if ((int)inflight.size() == kSinkSlots - 1) {  // the oldest piece out of its slot first
+                    if (int rc = copy_out(inflight.front())) return fail_with(rc, "hit copy-out failed");
+                    inflight.pop_front();
+                }
+                const int slot = next_slot;
+                next_slot = (next_slot + 1) % kSinkSlots;
+                e = hipMemcpyAsync(b_->stage[slot].p, src_ + a * wire_, m * wire_, hipMemcpyDeviceToHost, b_->d2h_stream);
+                if (e == hipSuccess) e = hipEventRecord(b_->stage_ev[slot], b_->d2h_stream);
+                inflight.push_back(Piece{slot, a, m});
+            }
+            if (e != hipSuccess) fail_with(XS_ERR_HIP, hipGetErrorString(e));
+        }
+        while (!inflight.empty() && !rc_) {
+            if (int rc = copy_out(inflight.front())) return fail_with(rc, "hit copy-out failed");
+            inflight.pop_front();
+        }
+        if (hipStreamSynchronize(b_->d2h_stream) != hipSuccess) fail_with(XS_ERR_HIP, "hit D2H failed");
+    }
+
+    xs_bank* b_;
+    uint8_t* host_;
+    const uint8_t* src_;
+    uint64_t cols_;
+    int wire_, out_;
+    bool direct_ = false;
+    int threads_ = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    std::thread th_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Job> q_;
+    bool closed_ = false;
+    int rc_ = XS_OK;
+    std::string err_;
+};
+
+// Narrowest transport width (bytes) of hit counts up to max_count, at most `out`.
+int wire_width(uint64_t max_count, int out) {
+    const int w = max_count <= 0xFFu ? 1 : max_count <= 0xFFFFu ? 2 : 4;
+    return std::min(w, out);
+}
+
 // Reads already in HBM (a device-mode reader's batch): query_host then only
 // chunks the probe and the hit-row D2H.
 struct DevReads {
@@ -714,13 +882,15 @@ struct DevReads {
 constexpr uint64_t kDevChunkReads = 1u << 18;
 
 // hits_host: n x cols rows back on the host (needs d_hits), as hit_bytes-wide
-// counts (4: uint32; 1 / 2: narrowed on the device into b->narrow first, the
-// caller having checked that they fit); tot_host: cols + 1 entries (per-doc
-// sums, then the k-mer total).  dev: the reads are on the device (seqs and
-// offsets unused); chunks are then cut by read count.
+// counts, crossing PCIe as wire_bytes-wide counts (0: hit_bytes; narrower
+// counts are narrowed on the device into b->narrow and widened on the host,
+// the caller having checked that they fit); tot_host: cols + 1 entries
+// (per-doc sums, then the k-mer total).  dev: the reads are on the device
+// (seqs and offsets unused); chunks are then cut by read count.
 int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                uint32_t* d_hits, void* hits_host, uint64_t* d_nk, uint64_t* tot_host, int hit_bytes = 4,
-               const DevReads* dev = nullptr) {
+               const DevReads* dev = nullptr, int wire_bytes = 0) {
+    const int wire = wire_bytes ? std::min(wire_bytes, hit_bytes) : hit_bytes;
     const uint64_t base = dev ? 0 : offsets[0];
     if (!dev)
         for (uint64_t r = 0; r < n; ++r)
@@ -772,9 +942,9 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         if (!b->copy_stream) HIPCHK(hipStreamCreateWithFlags(&b->copy_stream, hipStreamNonBlocking));
     }
     if (hits_host && !b->d2h_stream) HIPCHK(hipStreamCreateWithFlags(&b->d2h_stream, hipStreamNonBlocking));
-    const bool narrowing = hits_host && hit_bytes != 4;
+    const bool narrowing = hits_host && wire != 4;
     if (narrowing) {
-        if (int rc = b->narrow.ensure(n * cols * (uint64_t)hit_bytes + 16)) return rc;
+        if (int rc = b->narrow.ensure(n * cols * (uint64_t)wire + 16)) return rc;
         if (int rc = b->ovf.ensure(sizeof(uint32_t))) return rc;
         HIPCHK(hipMemsetAsync(b->ovf.p, 0, sizeof(uint32_t), b->stream));
     }
@@ -791,14 +961,13 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         HIPCHK(hipMemcpyAsync(b->offs.p, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
     }
     const int threads = host_threads();
-    auto drain = [&](size_t j) -> int {  // chunk j's hit rows to the host
-        const uint64_t r0 = cut[j], m = cut[j + 1] - cut[j];
-        HIPCHK(hipStreamWaitEvent(b->d2h_stream, b->chunk_ev[j], 0));
-        const uint64_t hb = (uint64_t)hit_bytes;
-        const void* src = hit_bytes == 4 ? static_cast<const void*>(d_hits + r0 * cols)
-                                         : static_cast<const void*>(b->narrow.as<uint8_t>() + r0 * cols * hb);
-        return d2h_pageable(b, static_cast<uint8_t*>(hits_host) + r0 * cols * hb, src, m * cols * hb, b->d2h_stream);
-    };
+    // the hit rows go back behind the probe (HitSink: its own thread, stream and pinned ring)
+    std::unique_ptr<HitSink> sink;
+    if (hits_host) {
+        sink.reset(new HitSink(b, hits_host, narrowing ? b->narrow.p : static_cast<const void*>(d_hits), cols, wire,
+                               hit_bytes));
+        if (int rc = sink->start(n * cols * (uint64_t)hit_bytes)) return rc;
+    }
     bool used[2] = {false, false};
     for (size_t i = 0; i < nc; ++i) {
         const uint64_t r0 = cut[i], r1 = cut[i + 1];
@@ -823,16 +992,15 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
                                tot_host ? b->totals.as<uint64_t>() + i * pcols : nullptr, b->stream))
             return rc;
         if (hits_host) {
-            if (hit_bytes != 4)
-                HIPCHK(launch_narrow_hits(d_hits + r0 * cols, b->narrow.as<uint8_t>() + r0 * cols * hit_bytes,
-                                          (r1 - r0) * cols, hit_bytes, b->stream, b->ovf.as<uint32_t>()));
+            if (narrowing)
+                HIPCHK(launch_narrow_hits(d_hits + r0 * cols, b->narrow.as<uint8_t>() + r0 * cols * wire,
+                                          (r1 - r0) * cols, wire, b->stream, b->ovf.as<uint32_t>()));
             HIPCHK(hipEventRecord(b->chunk_ev[i], b->stream));
-            if (i > 0)
-                if (int rc = drain(i - 1)) return rc;
+            sink->push(r0, r1, b->chunk_ev[i]);
         }
     }
-    if (hits_host)
-        if (int rc = drain(nc - 1)) return rc;
+    if (sink)
+        if (int rc = sink->finish()) return rc;
     if (tot_host) {
         std::vector<uint64_t> t(nc * pcols);
         HIPCHK(hipMemcpyAsync(t.data(), b->totals.p, t.size() * 8, hipMemcpyDeviceToHost, b->stream));
@@ -844,13 +1012,12 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         }
     }
     if (!dev) HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
-    if (hits_host) HIPCHK(hipStreamSynchronize(b->d2h_stream));
-    if (narrowing) {  // a count wider than hit_bytes (device reads: the caller's max_len understated)
+    if (narrowing) {  // a count wider than the wire (device reads: the caller's max_len understated)
         uint32_t over = 0;
         HIPCHK(hipMemcpyAsync(&over, b->ovf.p, sizeof(over), hipMemcpyDeviceToHost, b->stream));
         HIPCHK(hipStreamSynchronize(b->stream));
         if (over) return fail(XS_ERR_ARG, "a hit count does not fit %d byte(s): max_len is below the longest read",
-                              hit_bytes);
+                              wire);
     }
     return XS_OK;
 }
@@ -1285,15 +1452,18 @@ static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uin
     if (!b || !offsets || (!seqs && n)) return fail(XS_ERR_ARG, "null argument");
     if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
     if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
-    if (hits_out && hit_bytes != 4) {
-        // a count never exceeds its read's sampled k-mers: they must fit the width
-        const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
+    // a count never exceeds its read's sampled k-mers: they must fit the width, and
+    // the rows cross PCIe in the narrowest width that holds the largest (wire_width)
+    uint64_t max_nk = 0;
+    if (hits_out) {
+        const uint64_t cap = hit_bytes == 1 ? 0xFFu : hit_bytes == 2 ? 0xFFFFu : 0xFFFFFFFFu;
         for (uint64_t r = 0; r < n; ++r) {
             const uint64_t len = offsets[r + 1] >= offsets[r] ? offsets[r + 1] - offsets[r] : 0;
             const uint64_t nk = len >= b->k ? (len - b->k) / step + 1 : 0;
             if (nk > cap)
                 return fail(XS_ERR_ARG, "read %llu has %llu sampled k-mers: counts may not fit %d byte(s)",
                             (unsigned long long)r, (unsigned long long)nk, hit_bytes);
+            max_nk = std::max(max_nk, nk);
         }
     }
     std::lock_guard<std::mutex> lk(b->mu);
@@ -1313,7 +1483,9 @@ static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uin
         if (int rc = b->nk.ensure(n * 8)) return rc;
         d_nk = b->nk.as<uint64_t>();
     }
-    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, hits_out, d_nk, nullptr, hit_bytes)) return rc;
+    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, hits_out, d_nk, nullptr, hit_bytes, nullptr,
+                            wire_width(max_nk, hit_bytes)))
+        return rc;
     if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, d_nk, n * 8, hipMemcpyDeviceToHost, b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
@@ -1335,12 +1507,12 @@ int xs_query_hits_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, con
     if (!b || (n && (!d_seqs || !d_offsets))) return fail(XS_ERR_ARG, "null argument");
     if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
     if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
+    const uint64_t max_nk = max_len >= b->k ? (max_len - b->k) / step + 1 : 0;
     if (hits_out && hit_bytes != 4) {
         const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
-        const uint64_t nk = max_len >= b->k ? (max_len - b->k) / step + 1 : 0;
-        if (nk > cap)
+        if (max_nk > cap)
             return fail(XS_ERR_ARG, "a read has %llu sampled k-mers: counts may not fit %d byte(s)",
-                        (unsigned long long)nk, hit_bytes);
+                        (unsigned long long)max_nk, hit_bytes);
     }
     std::lock_guard<std::mutex> lk(b->mu);
     HIPCHK(hipSetDevice(b->device));

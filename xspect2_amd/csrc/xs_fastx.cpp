@@ -474,23 +474,15 @@ size_t ring_pieces() {
     }();
     return r;
 }
-// pread threads of a window load (XSPECT2_AMD_FX_LOAD_THREADS, read once; default 6)
-size_t load_threads() {
-    static const size_t t = [] {
-        const char* e = getenv("XSPECT2_AMD_FX_LOAD_THREADS");
-        const long v = e ? atol(e) : 6;
-        return (size_t)std::max<long>(1, std::min<long>(v, 32));
-    }();
-    return t;
-}
+// pread threads of a window load: 6 outrun the DMA (~50 GB/s) and leave the
+// caller's threads their CPU share (profiles/r04_e2e_ring.txt)
+constexpr size_t kLoadThreads = 6;
 constexpr size_t kDevPad = 64;            // defined zero bytes past a batch's sequences
 
 struct DevSide {
     int device = 0;
     hipStream_t stream = nullptr;  // parse kernels
     hipStream_t copy = nullptr;    // text DMA
-    hipStream_t copy2 = nullptr;   // odd pieces' DMA with XSPECT2_AMD_FX_TWO_COPY=1 (made on first use)
-    hipEvent_t copy2_ev = nullptr;
     // Window text in two slots: the next window loads into one while the
     // current one is parsed from the other.
     hipEvent_t text_ev[2] = {nullptr, nullptr};
@@ -612,8 +604,7 @@ void put_devside(DevSide* d) {
     if (!d) return;
     stop_loader(*d);
     bool ok = d->stream && d->copy && hipSetDevice(d->device) == hipSuccess &&
-              hipStreamSynchronize(d->stream) == hipSuccess && hipStreamSynchronize(d->copy) == hipSuccess &&
-              (!d->copy2 || hipStreamSynchronize(d->copy2) == hipSuccess);
+              hipStreamSynchronize(d->stream) == hipSuccess && hipStreamSynchronize(d->copy) == hipSuccess;
     if (ok) {
         d->flip = 0;
         d->next_text = 0;
@@ -632,11 +623,6 @@ DevSide::~DevSide() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
     if (copy) (void)hipStreamSynchronize(copy);
-    if (copy2) {
-        (void)hipStreamSynchronize(copy2);
-        (void)hipStreamDestroy(copy2);
-    }
-    if (copy2_ev) (void)hipEventDestroy(copy2_ev);
     for (hipEvent_t e : ring_ev)
         if (e) (void)hipEventDestroy(e);
     hipEvent_t* evs[5] = {&text_ev[0], &text_ev[1], &kern_ev, &host_ev[0], &host_ev[1]};
@@ -652,7 +638,7 @@ DevSide::~DevSide() {
     for (hipEvent_t* e : evs)
         if (*e) (void)hipEventDestroy(*e);
     if (stream) (void)hipStreamDestroy(stream);
-    if (copy && copy != stream) (void)hipStreamDestroy(copy);
+    if (copy) (void)hipStreamDestroy(copy);
 }
 
 }  // namespace
@@ -840,14 +826,6 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     DevSide& d = *r->dev;
     const double t0 = fx_ms();
     FXCHK(hipSetDevice(d.device));
-    static const bool two_copy = [] {
-        const char* v = getenv("XSPECT2_AMD_FX_TWO_COPY");
-        return v && v[0] == '1';
-    }();
-    if (two_copy && !d.copy2 && d.copy != d.stream) {
-        FXCHK(hipStreamCreateWithFlags(&d.copy2, hipStreamNonBlocking));
-        FXCHK(hipEventCreateWithFlags(&d.copy2_ev, hipEventDisableTiming));
-    }
     const size_t span = hi - lo;
     const size_t tiles = std::max<size_t>(1, (span + xs::kFxTile - 1) / xs::kFxTile);
     const size_t padded = tiles * xs::kFxTile;
@@ -867,7 +845,7 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     const size_t pieces = (span + kPieceBytes - 1) / kPieceBytes;
     // pread outruns the DMA (~50 GB/s) with a few threads; more only burn the
     // CPU share the caller's own threads need
-    const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, load_threads(), pieces}));
+    const int T = (int)std::max<size_t>(1, std::min<size_t>({(size_t)r->threads, kLoadThreads, pieces}));
     std::vector<uint8_t> done(pieces, 0);
     size_t queued = 0;  // pieces whose DMA is queued (in order)
     std::mutex mu;
@@ -914,9 +892,8 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
             if (failed) break;
         }
         const size_t o = p * kPieceBytes, n = std::min(span, o + kPieceBytes) - o;
-        const hipStream_t cs = d.copy2 && (p & 1) ? d.copy2 : d.copy;  // two DMA queues: ~56 vs ~50 GB/s
-        hipError_t e = hipMemcpyAsync(text.as<char>() + o, at(p), n, hipMemcpyHostToDevice, cs);
-        if (e == hipSuccess && R) e = hipEventRecord(d.ring_ev[p % R], cs);
+        hipError_t e = hipMemcpyAsync(text.as<char>() + o, at(p), n, hipMemcpyHostToDevice, d.copy);
+        if (e == hipSuccess && R) e = hipEventRecord(d.ring_ev[p % R], d.copy);
         if (e != hipSuccess) {
             rc = xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
             std::lock_guard<std::mutex> g(mu);
@@ -932,10 +909,6 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
     for (auto& x : th) x.join();
     if (rc) return rc;
     if (failed) return xs::set_error(XS_ERR_IO, "read failed while loading the window's text");
-    if (d.copy2) {  // the window is complete when both queues are
-        FXCHK(hipEventRecord(d.copy2_ev, d.copy2));
-        FXCHK(hipStreamWaitEvent(d.copy, d.copy2_ev, 0));
-    }
     FXCHK(hipMemsetAsync(text.as<char>() + span, 0, padded + 16 - span, d.copy));
     FXCHK(hipEventRecord(d.text_ev[ts], d.copy));
     d.load_ms[ts] = fx_ms() - t0;
@@ -1041,7 +1014,12 @@ int parse_on_device(xs_fastx* r, size_t lo, size_t hi, int slot, int ts, bool* o
     DevSide& d = *r->dev;
     *ok = false;
     const size_t span = hi - lo;
-    if (span == 0 || span >= (1ull << 31) - xs::kFxTile) return XS_OK;  // u32 positions, int scan sizes
+    if (span == 0 || span >= (1ull << 31) - xs::kFxTile) {  // u32 positions, int scan sizes: host parser
+        // the slot's text DMA must be done before the slot is queued for a later window
+        // (whose larger buffer could otherwise take this one's back while it is written)
+        FXCHK(hipEventSynchronize(d.text_ev[ts]));
+        return XS_OK;
+    }
     const hipStream_t s = d.stream;
     FXCHK(hipStreamWaitEvent(s, d.text_ev[ts], 0));
     const uint64_t tiles = (span + xs::kFxTile - 1) / xs::kFxTile;
@@ -1330,25 +1308,14 @@ int xs_fastx_open_device(const char* path, int format, int threads, int device, 
     if (take_streams(*r->dev)) return XS_OK;
     // The parse kernels are short and sit between the caller's probes of the
     // previous batch: a high-priority stream lets their workgroups in as soon
-    // as the probe frees a slot, instead of after the whole probe.
+    // as the probe frees a slot, instead of after the whole probe.  The text
+    // DMA has a stream of its own, so the next window's copy never queues
+    // behind this window's parse.
     int least = 0, greatest = 0;
     if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    // XSPECT2_AMD_FX_PRIORITY=low: the parse stream at the lowest priority
-    // instead (the probe keeps its slots; the parse fills the gaps)
-    static const bool low_prio = [] {
-        const char* v = getenv("XSPECT2_AMD_FX_PRIORITY");
-        return v && v[0] == 'l';
-    }();
-    if (e == hipSuccess)
-        e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, low_prio ? least : greatest);
-    // XSPECT2_AMD_FX_ONE_STREAM=1: the text DMA on the parse stream (one
-    // stream fewer: HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues)
-    static const bool one_stream = [] {
-        const char* v = getenv("XSPECT2_AMD_FX_ONE_STREAM");
-        return v && v[0] == '1';
-    }();
-    if (one_stream) r->dev->copy = r->dev->stream;
-    else if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
+    (void)least;
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
     for (hipEvent_t* ev : {&r->dev->text_ev[0], &r->dev->text_ev[1], &r->dev->kern_ev, &r->dev->host_ev[0],
                            &r->dev->host_ev[1]})
         if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
@@ -1406,13 +1373,10 @@ int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* 
         auto queue_next = [&] {
             if (n1_hi && !is_queued(d, r->cur)) queue_window(r, r->cur, n1_hi);
         };
-        // one stream (XSPECT2_AMD_FX_ONE_STREAM): the next window's DMA queues
-        // behind this window's parse on the same stream, so it starts after it
-        if (d.copy != d.stream) queue_next();
+        queue_next();
         bool ok = false;
         g_fx = FxTimes{};
         if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
-        if (d.copy == d.stream) queue_next();
         if (n1_hi && n1_hi < r->stop && !is_queued(d, n1_hi))  // this slot's text is free now
             queue_window(r, n1_hi,
                          (size_t)(window_end(r, r->base + n1_hi, end, window_budget(max_text_bytes, r->windows + 1)) -

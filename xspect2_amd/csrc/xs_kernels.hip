@@ -55,8 +55,9 @@ __global__ void scatter_units_kernel(const uint64_t* __restrict__ nseg,
 
 // ------------------------------------------------------------------ rbloom probe
 // Filter bits tested before the rest: 2 measured fastest for member-heavy
-// and foreign-heavy reads alike (tools/gpu/gpu_bloom_ab.sh).
-constexpr int kBloomSplitDefault = 2;
+// and foreign-heavy reads alike (all 7 at once: 15.69 against 13.43 ms per
+// config-2 step).
+constexpr int kBloomSplit = 2;
 // All K bit indices first, then all K dword loads in flight at once (the
 // reference stops at the first zero bit; the answer is the same).
 // Returns bit 0: member; bit 1: the second load phase ran.
@@ -453,46 +454,17 @@ hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* h
     return launch_cobs_general(rv, bv, hits, partials, blocks, s);
 }
 
-// Bits tested before the rest (XSPECT2_AMD_BLOOM_SPLIT; 0 = all at once).
-static int bloom_split() {
-    static const int v = [] {  // thread-safe one-time init
-        const char* e = getenv("XSPECT2_AMD_BLOOM_SPLIT");
-        const int s = e ? atoi(e) : kBloomSplitDefault;
-        return (s == 0 || s == 1 || s == 2 || s == 3) ? s : kBloomSplitDefault;
-    }();
-    return v;
-}
-
 int probe_grid_bloom() {
-    static std::atomic<int> cache[4];
-    const int sp = bloom_split();
-    return cached_grid(cache[sp], [sp] {
-        switch (sp) {
-            case 1: return resident_grid(probe_bloom_kernel<21, 7, 1>, kProbeThreads, 0);
-            case 2: return resident_grid(probe_bloom_kernel<21, 7, 2>, kProbeThreads, 0);
-            case 3: return resident_grid(probe_bloom_kernel<21, 7, 3>, kProbeThreads, 0);
-            default: return resident_grid(probe_bloom_kernel<21, 7, 0>, kProbeThreads, 0);
-        }
-    });
-}
-
-template <int SPLIT>
-static void launch_bloom_t(const ReadView& rv, const BloomView& bv, uint32_t* hits, uint64_t* partials,
-                           int blocks, hipStream_t s) {
-    if (rv.k == 21 && bv.K == 7)
-        probe_bloom_kernel<21, 7, SPLIT><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
-    else
-        probe_bloom_kernel<0, 0, SPLIT><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    static std::atomic<int> cache{0};
+    return cached_grid(cache, [] { return resident_grid(probe_bloom_kernel<21, 7, kBloomSplit>, kProbeThreads, 0); });
 }
 
 hipError_t launch_probe_bloom(const ReadView& rv, const BloomView& bv, uint32_t* hits,
                               uint64_t* partials, int blocks, hipStream_t s) {
-    switch (bloom_split()) {
-        case 1: launch_bloom_t<1>(rv, bv, hits, partials, blocks, s); break;
-        case 2: launch_bloom_t<2>(rv, bv, hits, partials, blocks, s); break;
-        case 3: launch_bloom_t<3>(rv, bv, hits, partials, blocks, s); break;
-        default: launch_bloom_t<0>(rv, bv, hits, partials, blocks, s); break;
-    }
+    if (rv.k == 21 && bv.K == 7)
+        probe_bloom_kernel<21, 7, kBloomSplit><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
+    else
+        probe_bloom_kernel<0, 0, kBloomSplit><<<blocks, kProbeThreads, 0, s>>>(rv, bv, hits, partials);
     return hipGetLastError();
 }
 

@@ -188,10 +188,11 @@ __global__ void __launch_bounds__(kBucketThreads) bloom_bucket_kernel(ReadView r
 // sits on its own 128-B line (a line's atomics are serialised at the memory
 // side).  Every lane keeps kLookupUnroll entries in flight.
 
-// W > 0: each group's entry -> block map is built in LDS per window of W
-// entries, as in cobs_lookup_kernel (xs_probe_cobspart.hip), instead of a
-// shuffle binary search per entry.
-template <int kLookupUnroll, int W = 0>
+// Each group's entry -> block map is built in LDS per window of W entries, as
+// in cobs_lookup_kernel (xs_probe_cobspart.hip): every lane writes its block's
+// position base over its run's slots, then each entry reads its base back
+// (positions are u32: the host keeps a call under 2^32 entries).
+template <int kLookupUnroll, int W>
 __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const uint64_t* __restrict__ kofs,
                                                            uint64_t n, uint32_t K, uint32_t shift, uint32_t P,
                                                            uint64_t tstride, const uint32_t* __restrict__ eoff,
@@ -199,9 +200,8 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
                                                            uint8_t* __restrict__ emiss, uint32_t* qctr) {
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    __shared__ uint32_t s_base[W > 0 ? 4 : 1][W > 0 ? W : 1];  // entry -> position base (host: < 2^32 entries)
-    (void)wid;
-    (void)s_base;
+    static_assert(W > 0, "window of the entry -> block map");
+    __shared__ uint32_t s_base[4][W];  // entry -> position base
     const uint64_t nblk = (kofs[n] + kTK - 1) / kTK;
     const uint64_t cap = (uint64_t)kTK * K;
     const uint32_t xcd = blockIdx.x & 7;
@@ -230,9 +230,9 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
             const uint32_t pre = inc - len;
             const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
             const uint32_t base = (uint32_t)(b * cap + s) - pre;  // entry i sits at base + i (mod 2^32)
-            for (uint32_t w0 = 0; w0 < total; w0 += (W > 0 ? W : total)) {
-            const uint32_t wend = W > 0 ? min(total, w0 + W) : total;
-            if constexpr (W > 0) {
+            for (uint32_t w0 = 0; w0 < total; w0 += W) {
+            const uint32_t wend = min(total, w0 + W);
+            {
                 const uint32_t lo = max(pre, w0), hi = min(pre + len, wend);
                 for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
                 __builtin_amdgcn_wave_barrier();
@@ -243,19 +243,7 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u) {
                     const uint32_t i = i0 + u * 64 + lane;
-                    if constexpr (W > 0) {
-                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
-                    } else {
-                        int j = 0;
-#pragma unroll
-                        for (int st = 32; st; st >>= 1) {
-                            const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
-                            if (pv <= i) j += st;
-                        }
-                        const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
-                        const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
-                        pos[u] = (b0 + j) * cap + sj + (i - pj);
-                    }
+                    pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
                 }
 #pragma unroll
                 for (int u = 0; u < kLookupUnroll; ++u)
@@ -267,7 +255,7 @@ __global__ void __launch_bounds__(256) bloom_lookup_kernel(BloomView bv, const u
                 for (int u = 0; u < kLookupUnroll; ++u)
                     if (!((w[u] >> (off[u] & 31)) & 1u)) emiss[pos[u]] = 1;
             }
-            if constexpr (W > 0) __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
+            __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
             }
         }
         }
@@ -370,11 +358,6 @@ static int part_env() {
     return e ? atoi(e) : 1;
 }
 
-static int env_int_bl(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
 // Partition shift for a filter of `mbits` bits: 2^24-bit (2 MiB) partitions
 // (2 MiB: 8.92 ms per config-2 step; 1 MiB 9.31, 512 KiB 10.86, 4 MiB 10.00),
 // halved down to 2^20 bits while that leaves fewer than 64 partitions (8 per
@@ -412,8 +395,9 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
     size_t sb = 0;
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, sb, (const uint64_t*)nullptr, (uint64_t*)nullptr, (int)(n + 1));
     plan->scan_bytes = sb;
-    // entries are transient: cap the workspace (larger batches take the direct probe)
-    return plan->entry_bytes <= (24ull << 30);
+    // entries are transient: cap the workspace (larger batches take the direct probe);
+    // the lookup's u32 entry positions need fewer than 2^32 entries (7 B each: the cap keeps them)
+    return plan->entry_bytes <= (24ull << 30) && nblk * kTK * bv.K < (1ull << 32);
 }
 
 // Entries in flight per lane: 4 / 8 / 16 measured 10.67 / 10.59 / 10.44 ms per
@@ -423,6 +407,10 @@ bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32
 // saved a further 0.1 ms only, and is not done.
 constexpr int kUnroll = 16;
 constexpr int kLookupPerCu = 3;
+// the entry -> block map's window: 1024 entries (lookup 5.27 -> 5.02-5.05 ms against
+// round 2's shuffle binary search; 2048 / 512-entry windows 5.13 / 5.51, 24 / 12 entries
+// per lane 5.09 / 5.21; profiles/r03_lookup_ownermap.txt)
+constexpr int kLookupWindow = 1024;
 
 static int lookup_grid() {
     static std::atomic<int> cache{0};
@@ -431,7 +419,7 @@ static int lookup_grid() {
         hipDeviceProp_t prop;
         int per_cu = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 768;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bloom_lookup_kernel<kUnroll>, 256, 0) !=
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bloom_lookup_kernel<kUnroll, kLookupWindow>, 256, 0) !=
                 hipSuccess || per_cu < 1)
             per_cu = 1;
         const int g = std::min(per_cu, kLookupPerCu) * prop.multiProcessorCount;
@@ -467,17 +455,8 @@ hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, cons
     uint32_t* qctr = ws.aux + (plan.tstride + 1 + kQStride - 1) / kQStride * kQStride;  // 128-B aligned
     if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
     pass_mark(rec, kPassBucket, s);
-    // XSPECT2_AMD_BL_LOOKUP: 1 (default) the LDS entry -> block map over 1024-entry windows,
-    // 0 the shuffle binary search (round 2); u32 positions need < 2^32 entries.  Lookup
-    // 5.27 -> 5.02-5.05 ms; 2048 / 512-entry windows 5.13 / 5.51, 24 / 12 entries per lane
-    // 5.09 / 5.21 (profiles/r03_lookup_ownermap.txt)
-    const int blv = ne < (1ull << 32) ? env_int_bl("XSPECT2_AMD_BL_LOOKUP", 1) : 0;
-    if (blv == 1)
-        bloom_lookup_kernel<kUnroll, 1024><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                         plan.tstride, eoff, ws.tbl, emiss, qctr);
-    else
-        bloom_lookup_kernel<kUnroll><<<lookup_grid(), 256, 0, s>>>(bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P,
-                                                                    plan.tstride, eoff, ws.tbl, emiss, qctr);
+    bloom_lookup_kernel<kUnroll, kLookupWindow><<<lookup_grid(), 256, 0, s>>>(
+        bv, ws.kofs, rv.n, bv.K, plan.shift, plan.P, plan.tstride, eoff, ws.tbl, emiss, qctr);
     pass_mark(rec, kPassLookup, s);
     bloom_resolve_kernel<<<(unsigned)plan.tstride, 256, 0, s>>>(ws.kofs, rv.n, bv.K, eid, emiss, ws.miss);
     bloom_count_kernel<<<blocks, 256, 0, s>>>(rv, ws.kofs, ws.miss, bv.K, hits, partials, bv.rows_read);

@@ -36,7 +36,7 @@ namespace xs {
 
 namespace {
 
-// CK k-mers per bucket block (1024 or 2048); an entry's low IDB bits name
+// CK k-mers per bucket block (kCobsCK = 2048); an entry's low IDB bits name
 // its k-mer within the block.
 template <int CK>
 constexpr int id_bits() { return CK == 4096 ? 12 : CK == 2048 ? 11 : 10; }
@@ -213,16 +213,26 @@ __global__ void __launch_bounds__(bucket_threads<CK>(), CK == 4096 ? 1 : 2) cobs
 // bits (docs 118..127), so the resolve pass need not read the entries again.
 template <int CK>
 constexpr uint32_t emb_max_docs() { return 128 - id_bits<CK>(); }
-// DMA: rows gathered by LDS-DMA into per-wave slots (default), else into
-// registers.  Rows go back with non-temporal dword stores (7.8 vs 10.1 ms for
-// one plain dwordx4 in tools/partgather.hip; the other store and load cache
-// policies measured no better: profiles/r02_cobspart_ab.txt item 9).
-// W > 0: the entry -> block map of a group is built in LDS per window of W
-// entries (each lane writes its block's position base over its run's slots,
-// then every entry reads its base: ~2 LDS operations per 64 entries) instead
-// of a 6-step shuffle binary search per entry (8 shuffles per 64 entries);
-// 6.37 -> 6.01 ms on tools/ldslookup.hip's config-2 entries at W = 1024.
-template <int kUnroll, bool EMB, int CK, int DMA, int W = 0>
+// Rows are gathered by LDS-DMA (global_load_lds_dwordx4) into per-wave slots,
+// one gather instruction in flight per wave: 1 in flight x 2 workgroups per CU
+// beat 2, 3 or 6 in flight and 1, 3 or 4 workgroups (more requests per CU only
+// lengthen the L2 wait; register gathers 12.64 vs 12.15 ms per step;
+// DESIGN.md §6b items 8-9).  Rows go back with non-temporal dword stores (7.8
+// vs 10.1 ms for one plain dwordx4 in tools/partgather.hip; the other store
+// and load cache policies measured no better: profiles/r02_cobspart_ab.txt
+// item 9).  The entry -> block map of a group is built in LDS per window of
+// kWin entries (each lane writes its block's position base over its run's
+// slots, then every entry reads its base: ~2 LDS operations per 64 entries)
+// instead of a 6-step shuffle binary search per entry (8 shuffles per 64
+// entries): lookup 6.33 -> 6.06 ms, and with 8 entries per lane over
+// 2048-entry windows 5.84-5.88 ms (6 / 10 / 12 / 14 per lane: 6.06 / 6.08 /
+// 6.55 / 6.78 ms; profiles/r03_lookup_ownermap.txt).  Positions are u32: the
+// host keeps a range's workspace under 2^32 entries.
+constexpr int kLookupUnroll = 8;
+constexpr int kLookupWin = 2048;
+constexpr int kLookupPerCu = 2;
+
+template <bool EMB, int CK>
 __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uint64_t* __restrict__ kofs,
                                                           uint64_t n, uint32_t H, uint32_t shift, uint32_t P,
                                                           uint64_t tstride, const uint32_t* __restrict__ ent,
@@ -231,12 +241,11 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
                                                           uint64_t b_begin, uint64_t b_end, uint32_t gb,
                                                           uint64_t stride) {
     constexpr int IDB = id_bits<CK>();
+    constexpr int U = kLookupUnroll;
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
-    __shared__ uint4 s_rows[DMA > 0 ? 4 : 1][DMA > 0 ? kUnroll : 1][64];  // LDS-DMA landing slots
-    __shared__ uint32_t s_base[W > 0 ? 4 : 1][W > 0 ? W : 1];  // entry -> position base (host: range < 2^32 entries)
-    (void)wid;
-    (void)s_base;
+    __shared__ uint4 s_rows[4][U][64];            // LDS-DMA landing slots
+    __shared__ uint32_t s_base[4][kLookupWin];    // entry -> position base
     // this call's bucket blocks: b_begin .. b_end-1 (those past the batch's last k-mer
     // excluded), rows 0 .. nblk-1 of the range's workspace and partition tables
     const uint64_t last = min(b_end, (kofs[n] + CK - 1) / CK);
@@ -265,82 +274,60 @@ __global__ void __launch_bounds__(256) cobs_lookup_kernel(PartBank pb, const uin
             }
             const uint32_t pre = inc - len;
             const uint32_t total = (uint32_t)__shfl((int)inc, 63, 64);
-            // entry i of the group sits at its block's base + i (mod 2^32: the range's
-            // workspace holds < 2^32 entries when W > 0)
+            // entry i of the group sits at its block's base + i (mod 2^32)
             const uint32_t base = (uint32_t)(b * stride + s) - pre;
-            for (uint32_t w0 = 0; w0 < total; w0 += (W > 0 ? W : total)) {
-            const uint32_t wend = W > 0 ? min(total, w0 + W) : total;
-            if constexpr (W > 0) {
-                const uint32_t lo = max(pre, w0), hi = min(pre + len, wend);
-                for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
-                __builtin_amdgcn_wave_barrier();
-            }
-            for (uint32_t i0 = w0; i0 < wend; i0 += 64 * kUnroll) {
-                uint64_t pos[kUnroll];
-                uint32_t e[kUnroll];
-                uint4 v[kUnroll];
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u) {
-                    const uint32_t i = i0 + u * 64 + lane;
-                    if constexpr (W > 0) {
-                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
-                    } else {
-                        int j = 0;
-#pragma unroll
-                        for (int st = 32; st; st >>= 1) {
-                            const uint32_t pv = (uint32_t)__shfl((int)pre, j + st, 64);
-                            if (pv <= i) j += st;
-                        }
-                        const uint32_t sj = (uint32_t)__shfl((int)s, j, 64);
-                        const uint32_t pj = (uint32_t)__shfl((int)pre, j, 64);
-                        pos[u] = (b0 + j) * stride + sj + (i - pj);
-                    }
+            for (uint32_t w0 = 0; w0 < total; w0 += kLookupWin) {
+                const uint32_t wend = min(total, w0 + kLookupWin);
+                {
+                    const uint32_t lo = max(pre, w0), hi = min(pre + len, wend);
+                    for (uint32_t x = lo; x < hi; ++x) s_base[wid][x - w0] = base;
+                    __builtin_amdgcn_wave_barrier();
                 }
+                for (uint32_t i0 = w0; i0 < wend; i0 += 64 * U) {
+                    uint64_t pos[U];
+                    uint32_t e[U];
+                    uint4 v[U];
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u)
-                    e[u] = i0 + u * 64 + lane < wend ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
+                    for (int u = 0; u < U; ++u) {
+                        const uint32_t i = i0 + u * 64 + lane;
+                        pos[u] = i < wend ? s_base[wid][i - w0] + i : 0u;
+                    }
 #pragma unroll
-                for (int u = 0; u < kUnroll; ++u)
-                    if (i0 + u * 64 + lane < wend && e[u] != kCobsPadEntry) {
-                        if constexpr (DMA > 0) {  // the row lands in this wave's slot u
+                    for (int u = 0; u < U; ++u)
+                        e[u] = i0 + u * 64 + lane < wend ? __builtin_nontemporal_load(ent + pos[u]) : 0u;
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (i0 + u * 64 + lane < wend && e[u] != kCobsPadEntry) {
 #if defined(__HIP_DEVICE_COMPILE__)  // a device-only builtin: the host pass must not see it
-                            // DMA 1: one row gather in flight per wave (each waits for the one before);
-                            // 3, 4: two, three in flight; 2: all kUnroll
-                            if constexpr (DMA == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                            if constexpr (DMA == 3) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                            if constexpr (DMA == 4) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+                            // one row gather in flight per wave: each waits for the one before
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                             __builtin_amdgcn_global_load_lds(prow + (e[u] >> IDB), &s_rows[wid][u][0], 16, 0, 0);
 #endif
-                        } else {
-                            v[u] = prow[e[u] >> IDB];
                         }
-                    }
-                if constexpr (DMA > 0) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
-                    for (int u = 0; u < kUnroll; ++u) v[u] = s_rows[wid][u][lane];
+                    for (int u = 0; u < U; ++u) v[u] = s_rows[wid][u][lane];
+                    // a pad slot's row is all ones, so ANDing it into any k-mer changes nothing; its id
+                    // bits name the k-mer of its slot's position, spreading the pad rows' LDS ANDs in
+                    // the resolve pass over the block instead of one address
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (e[u] == kCobsPadEntry) {
+                            v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
+                            e[u] = (uint32_t)pos[u] & (CK - 1);
+                        }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (i0 + u * 64 + lane < wend) {
+                            if constexpr (EMB) v[u].w = (v[u].w & (0xFFFFFFFFu >> IDB)) | (e[u] << (32 - IDB));
+                            uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
+                            __builtin_nontemporal_store(v[u].x, o);
+                            __builtin_nontemporal_store(v[u].y, o + 1);
+                            __builtin_nontemporal_store(v[u].z, o + 2);
+                            __builtin_nontemporal_store(v[u].w, o + 3);
+                        }
                 }
-                // a pad slot's row is all ones, so ANDing it into any k-mer changes nothing; its id
-                // bits name the k-mer of its slot's position, spreading the pad rows' LDS ANDs in
-                // the resolve pass over the block instead of one address
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u)
-                    if (e[u] == kCobsPadEntry) {
-                        v[u] = make_uint4(~0u, ~0u, ~0u, ~0u);
-                        e[u] = (uint32_t)pos[u] & (CK - 1);
-                    }
-#pragma unroll
-                for (int u = 0; u < kUnroll; ++u)
-                    if (i0 + u * 64 + lane < wend) {
-                        if constexpr (EMB) v[u].w = (v[u].w & (0xFFFFFFFFu >> IDB)) | (e[u] << (32 - IDB));
-                        uint32_t* o = reinterpret_cast<uint32_t*>(out + pos[u]);
-                        __builtin_nontemporal_store(v[u].x, o);
-                        __builtin_nontemporal_store(v[u].y, o + 1);
-                        __builtin_nontemporal_store(v[u].z, o + 2);
-                        __builtin_nontemporal_store(v[u].w, o + 3);
-                    }
-            }
-            if constexpr (W > 0) __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
+                __builtin_amdgcn_wave_barrier();  // bases read before the next window's writes
             }
         }
     }
@@ -531,19 +518,18 @@ __global__ void part_zero_rows_kernel(const uint64_t* __restrict__ kofs, uint64_
 
 // XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
 // probe for classic banks of <= 128 docs of at least kCobsPartMinBankMiB and
-// batches of at least kCobsPartMinKmers k-mers;
-// 2 = partitioned for such banks of any size; 3 = as 2 with partitions down
-// to 1024 rows (tests reach many partitions on small banks).  Read per call.
+// batches of at least kCobsPartMinKmers k-mers; 2 = partitioned for such banks
+// of any size; 3 = as 2 with partitions down to 1024 rows (tests reach many
+// partitions on small banks); 4 = as 2 with 1024-row partitions (tests reach
+// more than kCobsPadParts partitions: unpadded runs).  Read per call.
 static int cobs_part_env() {
     const char* e = getenv("XSPECT2_AMD_COBS_PART");
     return e ? atoi(e) : 1;
 }
 
-// Bucket block k-mers: XSPECT2_AMD_CP_CK = 1024, 2048 (default) or 4096 (read per call).
-static int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
+// Bucket blocks of 2048 k-mers: 12.71-12.85 ms per config-2 step against 13.81
+// at 1024 and 14.4 at 4096 when measured.
+constexpr uint32_t kCobsCK = 2048;
 
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
                     CobsPartPlan* plan) {
@@ -555,20 +541,17 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     // banks that (nearly) fit the XCDs' L2s: the direct probe is as fast there
     // (15 MB: 11.09 vs 11.03 ms; 61 MB: 14.40 vs 11.53; profiles/r02_cobspart_banksize.txt)
     if (mode == 1 && sig * 16 < (kCobsPartMinBankMiB << 20)) return false;
-    const int ck_env = env_int("XSPECT2_AMD_CP_CK", 2048);
-    const uint32_t ck = ck_env == 4096 ? 4096 : ck_env == 1024 ? 1024 : 2048;
-    const uint32_t idb = ck == 4096 ? 12 : ck == 2048 ? 11 : 10;
+    const uint32_t ck = kCobsCK, idb = id_bits<kCobsCK>();
     // 2^17 rows (2 MiB) per partition, fewer rows while that leaves under 64
     // partitions (8 per XCD), more while over kPartMax
-    const uint32_t floor_shift = mode >= 3 ? 10 : 13;
-    // (an explicit XSPECT2_AMD_CP_SHIFT is kept as given, up to the kPartMax bound)
-    const bool shift_set = getenv("XSPECT2_AMD_CP_SHIFT") != nullptr;
-    uint32_t shift = (uint32_t)std::min(std::max(env_int("XSPECT2_AMD_CP_SHIFT", 17), 10), 21);
     auto parts = [sig](uint32_t s) { return (sig + (1ull << s) - 1) >> s; };
-    while (!shift_set && shift > floor_shift && parts(shift) < 64) --shift;
+    uint32_t shift = mode == 4 ? 10 : 17;
+    const uint32_t floor_shift = mode >= 3 ? 10 : 13;
+    while (mode != 4 && shift > floor_shift && parts(shift) < 64) --shift;
     while (parts(shift) > kPartMax) ++shift;
     // entry = (row in partition << idb) | k-mer in block: at shift + idb == 32 the
-    // last row's last k-mer would encode to kCobsPadEntry (0xFFFFFFFF)
+    // last row's last k-mer would encode to kCobsPadEntry (0xFFFFFFFF); sig < 2^30
+    // and kPartMax partitions keep shift <= 20 (a guard, not a reachable case)
     if (shift + idb >= 32) return false;
     const uint64_t kbound = seq_bytes / step + n + 1;  // >= sum of ceil((len-k+1)/step)
     // small batches: the direct probe is faster below ~60-100 k reads of 150 bp
@@ -578,14 +561,16 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     const uint64_t P = parts(shift);
     // The bucket blocks run in ranges that reuse one workspace of at most
     // XSPECT2_AMD_CP_WS_MB MiB of entries + rows (default kCobsPartWsMiB), so
-    // any batch size fits.
-    // runs padded to 4 entries (64-B row pieces: 4.37 -> 3.51 ms for the lookup's
-    // write stream alone, tools/runwrite.hip); XSPECT2_AMD_CP_PAD=1 turns it off
-    const uint32_t pad = (P <= kCobsPadParts && env_int("XSPECT2_AMD_CP_PAD", 4) != 1) ? 4 : 1;
+    // any batch size fits.  Runs are padded to 4 entries (64-B row pieces: 4.37
+    // -> 3.51 ms for the lookup's write stream alone, tools/runwrite.hip) while
+    // the pad slots fit the bucket block's LDS (P <= kCobsPadParts).
+    const uint32_t pad = P <= kCobsPadParts ? 4 : 1;
     const uint64_t stride = ((uint64_t)ck * bv.h + (pad - 1) * P + 7) / 8 * 8;
     const uint64_t per_block = stride * (sizeof(uint32_t) + sizeof(uint4));
-    const uint64_t cap = (uint64_t)std::max(1, env_int("XSPECT2_AMD_CP_WS_MB", (int)kCobsPartWsMiB)) << 20;
-    const uint64_t rblk = std::max<uint64_t>(1, std::min<uint64_t>(nblk, cap / per_block));
+    const char* ws_env = getenv("XSPECT2_AMD_CP_WS_MB");
+    const uint64_t cap = (uint64_t)std::max(1, ws_env ? atoi(ws_env) : (int)kCobsPartWsMiB) << 20;
+    // a range holds fewer than 2^32 entries (the lookup's u32 positions)
+    const uint64_t rblk = std::max<uint64_t>(1, std::min<uint64_t>({nblk, cap / per_block, ((1ull << 32) - 1) / stride}));
     plan->ck = ck;
     plan->shift = shift;
     plan->P = (uint32_t)P;
@@ -604,35 +589,18 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     return true;
 }
 
-static int cobs_lookup_grid(int per_cu_want) {
+static int cobs_lookup_grid() {
     static std::atomic<int> cache{0};
-    const int per_cu_res = cached_grid(cache, [] {
-        int per_cu = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<8, true, 1024, 0>, 256, 0) !=
+    return cached_grid(cache, [] {
+        int dev = 0, per_cu = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 768;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, cobs_lookup_kernel<true, kCobsCK>, 256, 0) !=
                 hipSuccess || per_cu < 1)
             per_cu = 1;
-        return per_cu;
+        const int g = std::min(per_cu, kLookupPerCu) * prop.multiProcessorCount;
+        return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
     });
-    int dev = 0;
-    hipDeviceProp_t prop;
-    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 768;
-    const int g = std::min(per_cu_res, std::max(1, per_cu_want)) * prop.multiProcessorCount;
-    return g >= 8 ? g / 8 * 8 : 8;  // whole groups of 8 blocks (one per XCD)
-}
-
-template <int U, int CK, int DMA, int W = 0>
-static void lookup_launch(bool emb, int grid, const PartBank& pb, const uint64_t* kofs, uint64_t n, uint32_t H,
-                          const CobsPartPlan& plan, const uint32_t* ent, const uint16_t* tbl, uint4* rowv,
-                          uint32_t* qctr, uint64_t b0, uint64_t b1, hipStream_t s) {
-    // groups per partition >= the XCD's waves (grid / 8 workgroups x 4 waves)
-    const uint64_t waves = (uint64_t)grid / 8 * 4;
-    const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
-    if (emb)
-        cobs_lookup_kernel<U, true, CK, DMA, W><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                    ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
-    else
-        cobs_lookup_kernel<U, false, CK, DMA, W><<<grid, 256, 0, s>>>(pb, kofs, n, H, plan.shift, plan.P, plan.rblk,
-                                                                     ent, tbl, rowv, qctr, b0, b1, gb, plan.stride);
 }
 
 // Ranges of plan.rblk bucket blocks, one after the other on stream s, each
@@ -653,19 +621,9 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
         part_zero_rows_kernel<CK><<<grid_for(rv.n, 256, 4096), 256, 0, s>>>(ws.kofs, rv.n, blk_read, pb.D, hits);
     pass_mark(rec, kPassPrep, s);
     const bool emb = pb.D <= emb_max_docs<CK>();
-    // lookup: 5 (default) LDS-DMA row gathers of 8 entries per lane, one gather in
-    // flight per wave at a time, 2 workgroups per CU, entry -> block map in LDS
-    // over windows of 2048 entries; 6 the same with 6 entries per lane and
-    // 1024-entry windows (the map alone: lookup 6.33 -> 6.06-6.10 ms; 8 per lane
-    // 5.87-5.91, 10 / 12 / 14 per lane 6.08 / 6.55 / 6.78 ms, interleaved,
-    // profiles/r03_lookup_ownermap.txt); 0 6 per lane with the shuffle binary
-    // search (round 2's default); 1 register gathers, 8 in flight, 3 per CU
-    // (the first build); 2 LDS-DMA with all 6 in flight.
-    // XSPECT2_AMD_CP_PERCU overrides the workgroups per CU.
-    int var = env_int("XSPECT2_AMD_CP_LOOKUP", 5);
-    // 5, 6: the LDS entry -> block map (u32 positions: ranges of < 2^32 entries)
-    if (var >= 5 && plan.rblk * plan.stride >= (1ull << 32)) var = 0;
-    const int grid = cobs_lookup_grid(env_int("XSPECT2_AMD_CP_PERCU", var == 1 ? 3 : 2));
+    const int grid = cobs_lookup_grid();
+    // groups per partition >= the XCD's waves (grid / 8 workgroups x 4 waves)
+    const uint64_t waves = (uint64_t)grid / 8 * 4;
     for (uint64_t b0 = 0; b0 < plan.nblk; b0 += plan.rblk) {
         const uint64_t b1 = std::min(plan.nblk, b0 + plan.rblk);
         const unsigned nb = (unsigned)(b1 - b0);
@@ -681,15 +639,13 @@ static hipError_t cobs_part_pipeline(const ReadView& rv, const PartBank& pb, uin
             tbm, plan.P + 1, plan.rblk, ws.tbl, 0, nb);
         if ((e = hipMemsetAsync(qctr, 0, (size_t)plan.P * kQStride * sizeof(uint32_t), s)) != hipSuccess) return e;
         pass_mark(rec, kPassBucket, s);
-        switch (var) {
-            case 1: lookup_launch<8, CK, 0>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 2: lookup_launch<6, CK, 2>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 3: lookup_launch<6, CK, 3>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 4: lookup_launch<6, CK, 4>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 5: lookup_launch<8, CK, 1, 2048>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            case 6: lookup_launch<6, CK, 1, 1024>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-            default: lookup_launch<6, CK, 1>(emb, grid, pb, ws.kofs, rv.n, H, plan, ent, ws.tbl, rowv, qctr, b0, b1, s); break;
-        }
+        const uint32_t gb = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (b1 - b0) / std::max<uint64_t>(1, waves)));
+        if (emb)
+            cobs_lookup_kernel<true, CK><<<grid, 256, 0, s>>>(pb, ws.kofs, rv.n, H, plan.shift, plan.P, plan.rblk, ent,
+                                                              ws.tbl, rowv, qctr, b0, b1, gb, plan.stride);
+        else
+            cobs_lookup_kernel<false, CK><<<grid, 256, 0, s>>>(pb, ws.kofs, rv.n, H, plan.shift, plan.P, plan.rblk,
+                                                               ent, ws.tbl, rowv, qctr, b0, b1, gb, plan.stride);
         pass_mark(rec, kPassLookup, s);
         if (emb)
             cobs_resolve_kernel<true, CK><<<nb, resolve_threads<CK>(), 0, s>>>(
@@ -722,9 +678,7 @@ hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const 
     size_t sb = ws.scan_bytes;
     if ((e = hipcub::DeviceScan::ExclusiveSum(ws.scan_tmp, sb, ws.nkc, ws.kofs, (int)(rv.n + 1), s)) != hipSuccess)
         return e;
-    if (plan.ck == 4096) return cobs_part_pipeline<4096>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
-    if (plan.ck == 2048) return cobs_part_pipeline<2048>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
-    return cobs_part_pipeline<1024>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
+    return cobs_part_pipeline<kCobsCK>(rv, pb, bv.h, plan, ws, hits, partials, blocks, s, rec);
 }
 
 }  // namespace xs

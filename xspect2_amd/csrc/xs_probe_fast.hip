@@ -11,25 +11,9 @@ struct FastBank {
     const uint8_t* rows;
     uint64_t sig, magic;
     uint32_t D, nwords;  // nwords = ceil(D/32)
-    uint32_t image_bytes;
 };
 
-// Row gather policies (XSPECT2_AMD_LOADPOL): 0 global_load_dwordx4; buffer_load
-// with cache-policy aux 1: none, 2: nt, 3: sc1, 4: sc0 sc1 (L1 bypass forms).
-template <int POL>
-__device__ __forceinline__ uint4 load_row(const FastBank& fb, uint32_t off) {
-    if constexpr (POL == 0) {
-        return *reinterpret_cast<const uint4*>(fb.rows + off);
-    } else {
-        constexpr int aux = POL == 1 ? 0 : POL == 2 ? 2 : POL == 3 ? 16 : 17;
-        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(fb.rows), (short)0,
-                                                            (int)fb.image_bytes, 0x00020000);
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)off, 0, aux);
-        return make_uint4(v[0], v[1], v[2], v[3]);
-    }
-}
-
-template <int KT, int HT, int POL>
+template <int KT, int HT>
 __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv, FastBank fb,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials) {
@@ -75,7 +59,7 @@ __global__ void __launch_bounds__(kProbeThreads, 2) probe_cobs_fast(ReadView rv,
                     m = make_uint4(~0u, ~0u, ~0u, ~0u);
 #pragma unroll
                     for (int j = 0; j < HT; ++j)
-                        m = and4(m, load_row<POL>(fb, off[j]));
+                        m = and4(m, *reinterpret_cast<const uint4*>(fb.rows + off[j]));
                 }
                 a0 += column_popc32(m.x, X);
                 if (nwords > 1) a1 += column_popc32(m.y, X);
@@ -126,32 +110,17 @@ bool cobs_fast(const CobsView& bv, uint32_t k) {
            ((k == 21 && bv.h == 7) || (k == 31 && bv.h == 1));
 }
 
-static int load_policy() {
-    static const int pol = [] {  // thread-safe one-time init
-        const char* e = getenv("XSPECT2_AMD_LOADPOL");
-        const int v = e ? atoi(e) : 0;
-        return (v < 0 || v > 4) ? 0 : v;
-    }();
-    return pol;
-}
-
 template <int KT, int HT>
 static hipError_t launch_fast_t(const ReadView& rv, const FastBank& fb, uint32_t* hits,
                                 uint64_t* partials, int blocks, hipStream_t s) {
-    switch (load_policy()) {
-        case 1: probe_cobs_fast<KT, HT, 1><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
-        case 2: probe_cobs_fast<KT, HT, 2><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
-        case 3: probe_cobs_fast<KT, HT, 3><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
-        case 4: probe_cobs_fast<KT, HT, 4><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
-        default: probe_cobs_fast<KT, HT, 0><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials); break;
-    }
+    probe_cobs_fast<KT, HT><<<blocks, kProbeThreads, 0, s>>>(rv, fb, hits, partials);
     return hipGetLastError();
 }
 
 int grid_cobs_fast(uint32_t k) {
     static std::atomic<int> g21{0}, g31{0};
-    if (k == 21) return cached_grid(g21, [] { return resident_grid(probe_cobs_fast<21, 7, 0>, kProbeThreads, 0); });
-    return cached_grid(g31, [] { return resident_grid(probe_cobs_fast<31, 1, 0>, kProbeThreads, 0); });
+    if (k == 21) return cached_grid(g21, [] { return resident_grid(probe_cobs_fast<21, 7>, kProbeThreads, 0); });
+    return cached_grid(g31, [] { return resident_grid(probe_cobs_fast<31, 1>, kProbeThreads, 0); });
 }
 
 hipError_t launch_cobs_fast(const ReadView& rv, const CobsView& bv, uint32_t* hits, uint64_t* partials,
@@ -162,7 +131,6 @@ hipError_t launch_cobs_fast(const ReadView& rv, const CobsView& bv, uint32_t* hi
     fb.magic = barrett_magic(bv.sig0);
     fb.D = (uint32_t)bv.D;
     fb.nwords = (uint32_t)((bv.D + 31) / 32);
-    fb.image_bytes = (uint32_t)min(bv.sig0 * 16ull, 0xFFFFFFFFull);
     if (rv.k == 21) return launch_fast_t<21, 7>(rv, fb, hits, partials, blocks, s);
     return launch_fast_t<31, 1>(rv, fb, hits, partials, blocks, s);
 }

@@ -311,7 +311,7 @@ def read_batches(path: Path, max_bytes: int | None = None, threads: int = 0,
 
     max_bytes = DEFAULT_BATCH_TEXT if max_bytes is None else max_bytes
 
-    if device is not None and os.environ.get("XSPECT2_AMD_FX_PARSE_AHEAD") != "1":
+    if device is not None:
         # device mode: the next window's text already loads behind the
         # caller's work (the reader's own prefetch thread); parsing it on the
         # GPU beside the caller's probe only slows both, so the parse waits
