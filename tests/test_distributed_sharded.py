@@ -55,7 +55,8 @@ class OracleIndex:
         return h.astype(hit_dtype), nk
 
 
-def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int = 0, short_at: int = -1):
+def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int = 0, short_at: int = -1,
+           mis_at: int = -1):
     """A species model over 6 synthetic genomes (oracle bank), its reads as a
     FASTQ file (written by the parent before the ranks start: a rank must not
     rewrite a file another rank is reading)."""
@@ -91,7 +92,8 @@ def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int =
         g = genomes[i % 6] if i % 7 else acgt[rng.integers(0, 4, 3000)].tobytes()
         L = int(rng.integers(K + 1, 200)) if i != short_at else K  # len <= k: the reference raises
         s = int(rng.integers(0, len(g) - L))
-        reads.append((f"read_{i % id_mod if id_mod else i}", g[s:s + L].decode()))
+        rid = "misclassified" if i == mis_at else f"read_{i % id_mod if id_mod else i}"
+        reads.append((rid, g[s:s + L].decode()))
     fq = tmp / "reads.fq"
     if write:
         fq.write_text("".join(f"@{rid} x\n{s}\n+\n{'I' * len(s)}\n" for rid, s in reads))
@@ -187,6 +189,45 @@ def test_repeated_ids_across_shards_follow_the_reference_dict(tmp_path, world, i
     assert list(got["hits"]) == list(want["hits"])
     assert got["prediction"] == want["prediction"]
     assert sum(len(json.loads(p.read_text())["hits"]) for p in shards) == len(want["hits"])
+    distributed.merge_result_files(shards, tmp_path / "merged.json")
+    assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "single.json").read_bytes()
+
+
+def _mis_worker(rank: int, world: int, port: int, tmp: str, n_reads: int, mis_at: int):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model, fq = _setup(Path(tmp), n_reads, True, write=False, mis_at=mis_at)
+        distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / "mis.json")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mis_at", [(3, 595), (2, 0), (3, 300)])
+def test_read_named_misclassified_in_any_shard(tmp_path, world, mis_at):
+    """A read literally named "misclassified" is popped from the reference's
+    hits into the result's "misclassified" field (result.py:43): it leaves the
+    per-doc totals and the choice of the first row that orders "total", but
+    keeps its k-mers in num_kmers.  Whichever shard holds it (the last, the
+    first as its first read, a middle one), the merged shards equal the
+    single-process JSON."""
+    import torch.multiprocessing as mp
+    from xspect2_amd import distributed
+
+    n_reads = 600
+    model, fq = _setup(tmp_path, n_reads, True, mis_at=mis_at)
+    mp.spawn(_mis_worker, args=(world, _free_port(), str(tmp_path), n_reads, mis_at), nprocs=world, join=True)
+    res = model.predict_columnar(fq)
+    res.input_source = fq.name
+    res.save(tmp_path / "single.json")
+    want = json.loads((tmp_path / "single.json").read_text())
+    assert want["misclassified"] is not None and "misclassified" not in want["hits"]
+    shards = [distributed.shard_path(tmp_path / "out" / "mis.json", r, world) for r in range(world)]
+    assert distributed.merge_result_shards(shards) == want
     distributed.merge_result_files(shards, tmp_path / "merged.json")
     assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "single.json").read_bytes()
 

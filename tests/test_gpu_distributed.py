@@ -9,7 +9,10 @@ by tools/gpu/gpu_r03_sharded.sh.)
   transport; ``exchange_doc_columns`` (the all-to-all that sends every
   rank's hit columns to the reads' rank) keeps values in 1, 2 and 4 bytes;
   ``predict_docs_sharded`` (reads all-gathered from the device reader,
-  probed, exchanged) equals the model's own prediction;
+  probed, exchanged) over three banks equals the C oracle's hit columns;
+* configs 3 and 5 at world 2 over RCCL (two GPUs, skipped on a one-GPU box):
+  child ranks started by bench.launch_ranks write shards whose merge equals
+  one process's JSON byte for byte;
 * config 3: ``classify_species_sharded`` — the byte-range reader, the RCCL
   all-reduce of D+1 totals on a device tensor, the SVM label — writes the
   JSON the single-process ``classify_species`` writes.
@@ -108,23 +111,70 @@ def test_classify_species_sharded_world1_equals_classify_species(pg, tmp_path, m
     assert want["prediction"].startswith("L")
 
 
-def test_predict_docs_sharded_world1_on_device(pg, tmp_path, oracle_mod):
-    """Config 5's library call through the device path (RCCL, world 1):
-    equals the model's own columnar prediction."""
+def test_predict_docs_sharded_world1_matches_oracle(pg, tmp_path, oracle_mod):
+    """Config 5's library call through the device path (RCCL, world 1) for
+    three banks of 40, 50 and 37 docs (127 docs in all, as three ranks of a
+    multi-genus job would hold them): every bank's reads parsed on the device,
+    probed, exchanged by the all-to-all; each bank's hit columns and the k-mer
+    counts equal the C oracle's on the same reads, and so does the
+    column-concatenated matrix one process probing every bank would write."""
     import numpy as np
     from xspect2_amd import distributed
     from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
-    ob, gb, docs = _bank(oracle_mod, D=100, seed=3)
-    m = ProbabilisticFilterModel(K, "Genus", None, None, "Species", tmp_path)
-    m.index = gb
+    banks = [_bank(oracle_mod, D=d, seed=10 + d) for d in (40, 50, 37)]
+    rng = np.random.default_rng(11)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    seqs = [d[o:o + 150] for _, _, docs in banks for d in docs[::3] for o in (0, 3000)]
+    seqs += [acgt[rng.integers(0, 4, int(rng.integers(22, 400)))].tobytes() for _ in range(80)]
     fa = tmp_path / "r.fasta"
-    fa.write_text("".join(f">r{i}\n{d[o:o + 150].decode()}\n" for i, d in enumerate(docs) for o in (0, 3000)))
-    res = distributed.predict_docs_sharded(m, fa)
-    want = m.predict_columnar(fa)
-    assert res.ids == want.ids and res.labels == want.labels
-    assert np.array_equal(res.hits.astype(np.uint32), want.hits.astype(np.uint32))
-    assert np.array_equal(res.num_kmers, want.num_kmers)
-    gb.close()
+    fa.write_text("".join(f">r{i} x\n{s.decode()}\n" for i, s in enumerate(seqs)))
+    cols, want_cols = [], []
+    for j, (ob, gb, _) in enumerate(banks):
+        m = ProbabilisticFilterModel(K, f"Genus{j}", None, None, "Species", tmp_path)
+        m.index = gb
+        res = distributed.predict_docs_sharded(m, fa)
+        want_h, want_n = ob.query(seqs)
+        assert list(res.ids) == [f"r{i}" for i in range(len(seqs))]
+        assert np.array_equal(res.hits.astype(np.uint32), want_h), f"bank {j}: hit columns differ from the oracle"
+        assert np.array_equal(res.num_kmers.astype(np.uint64), want_n)
+        cols.append(res.hits.astype(np.uint32))
+        want_cols.append(want_h)
+        gb.close()
+    assert np.array_equal(np.concatenate(cols, axis=1), np.concatenate(want_cols, axis=1))
+    assert sum(c.shape[1] for c in cols) == 127
+
+
+@pytest.mark.skipif("not __import__('torch').cuda.device_count() >= 2",
+                    reason="needs 2 GPUs (RCCL refuses two ranks on one device)")
+def test_rccl_world2_sharded_equals_one_process(tmp_path):
+    """Configs 3 and 5 over a real RCCL process group of 2 ranks (cuda:0 and
+    cuda:1), each rank a fresh child process started by bench.launch_ranks
+    (no GPU work in this process): classify_species_sharded (byte ranges,
+    all-reduced totals, SVM label on rank 0) and predict_docs_sharded (one
+    genus bank per rank, reads all-gathered, columns all-to-all'd) write
+    shards whose merge is byte-equal to one process's JSON
+    (tools/sharded_classify.py; src/xspect/classify.py:43-92)."""
+    import subprocess
+    import sys
+    from pathlib import Path
+    root = Path(__file__).resolve().parents[1]
+    sys.path.insert(0, str(root))
+    import bench
+    tool = str(root / "tools" / "sharded_classify.py")
+    d = str(tmp_path)
+
+    def one(*args):
+        subprocess.run([sys.executable, tool, *args, "--root", d], check=True, timeout=600)
+
+    one("setup", "--reads", "20000")
+    one("single")
+    one("docs-setup", "--world", "2", "--reads", "20000")
+    one("docs-single", "--world", "2")
+    env = {k: v for k, v in __import__("os").environ.items() if k != "XSPECT_SHARE_GPU"}
+    for cmd in ("shard", "docs-shard"):
+        assert bench.launch_ranks(2, [sys.executable, tool, cmd, "--root", d], 600, env=env) == 0
+    one("check", "--world", "2")
+    one("docs-check", "--world", "2")
 
 
 @pytest.mark.parametrize("wire", ["uint8", "int16", "int32"])

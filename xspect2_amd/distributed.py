@@ -120,6 +120,34 @@ def alltoallv(chunks: list):
     return list(torch.split(recv, rs))
 
 
+def _dup_messages(t: np.ndarray, world: int) -> list[np.ndarray]:
+    """The owner's instructions for its candidate records ``t`` (rows of
+    (key0, key1, source rank, source index)): for every key held by more than
+    one record, the record first in file order (rank, then index) keeps the id
+    and takes the values of the last, every other record drops it.  Returns,
+    per destination rank, rows (kind, index, src rank, src index): kind 0 =
+    keep, values from (src rank, src index); kind 1 = drop.  Vectorised: one
+    lexsort over the candidates, no per-group loop."""
+    out = [np.zeros((0, 4), np.int64) for _ in range(world)]
+    if t.shape[0] < 2:
+        return out
+    a = t[np.lexsort((t[:, 3], t[:, 2], t[:, 1], t[:, 0]))]
+    start = np.concatenate([[True], (a[1:, 0] != a[:-1, 0]) | (a[1:, 1] != a[:-1, 1])])
+    gid = np.cumsum(start) - 1
+    first = np.flatnonzero(start)
+    size = np.diff(np.concatenate([first, [a.shape[0]]]))
+    dup = np.flatnonzero(size > 1)
+    if not dup.size:
+        return out
+    f, lst = a[first[dup]], a[first[dup] + size[dup] - 1]
+    keep = np.stack([f[:, 2], np.zeros(dup.size, np.int64), f[:, 3], lst[:, 2], lst[:, 3]], axis=1)
+    d = a[(size[gid] > 1) & ~start]
+    drop = np.stack([d[:, 2], np.ones(d.shape[0], np.int64), d[:, 3], np.zeros_like(d[:, 3]),
+                     np.zeros_like(d[:, 3])], axis=1)
+    msgs = np.concatenate([keep, drop])
+    return [np.ascontiguousarray(msgs[msgs[:, 0] == q, 1:]) for q in range(world)]
+
+
 def resolve_cross_shard_duplicates(res) -> int:
     """Apply the reference's rule for repeated read ids to one shard of a
     read-sharded job (``res``: this rank's MatrixResult, its own repeats
@@ -129,14 +157,17 @@ def resolve_cross_shard_duplicates(res) -> int:
     the job totals over that dict (result.py:76-90).
 
     Ids are keyed by 128 bits (XXH64 of the id bytes with two seeds,
-    xs_ids_hash128) and sent to the rank that owns their hash range
-    (all-to-all); the owner finds keys present on several ranks.  For each,
-    the rank holding the first record keeps the id at its position and takes
-    the hit row and k-mer count of the last record (fetched from its rank);
-    every other rank drops the id.  Merging the shards in part order then
-    gives the single-process dictionaries, and each id enters the job
-    totals once.  Returns the number of rows this rank dropped.  Two
-    different ids share a key with probability ~n^2 / 2^129."""
+    xs_ids_hash128); key half 0 picks the owning rank.  Round 1 sends only
+    key half 0 (8 B per read) to the owner, which finds the records whose
+    half 0 another record shares (the candidates: the repeats, plus ~n^2/2^65
+    accidental pairs); round 2 fetches half 1 and the read index of the
+    candidates only.  For each full key held by several records, the rank
+    holding the first record keeps the id at its position and takes the hit
+    row and k-mer count of the last record (fetched from its rank); every
+    other rank drops the id.  Merging the shards in part order then gives the
+    single-process dictionaries, and each id enters the job totals once.
+    Returns the number of rows this rank dropped.  Two different ids share a
+    key with probability ~n^2 / 2^129."""
     import torch
     dist = _dist()
     rank, world = dist.get_rank(), dist.get_world_size()
@@ -146,26 +177,28 @@ def resolve_cross_shard_duplicates(res) -> int:
     n = len(ids)
     key = ids.hash128().view(np.int64)                             # [n, 2]
     owner = (key[:, 0].view(np.uint64) % np.uint64(world)).astype(np.int64)
-    rec = np.concatenate([key, np.arange(n, dtype=np.int64)[:, None]], axis=1)
-    got = alltoallv([torch.from_numpy(np.ascontiguousarray(rec[owner == q])) for q in range(world)])
-    # the owner: records from every source rank, sorted by key, then file order (rank, index)
-    allr = np.concatenate([np.concatenate([g.cpu().numpy().reshape(-1, 3),
-                                           np.full((g.shape[0], 1), s, dtype=np.int64)], axis=1)
-                           for s, g in enumerate(got)]) if got else np.zeros((0, 4), np.int64)
-    msgs = [[] for _ in range(world)]  # per destination: (kind, index, src rank, src index)
-    if allr.shape[0] > 1:
-        o = np.lexsort((allr[:, 2], allr[:, 3], allr[:, 1], allr[:, 0]))
-        a = allr[o]
-        same = (a[1:, 0] == a[:-1, 0]) & (a[1:, 1] == a[:-1, 1])
-        start = np.flatnonzero(np.concatenate([[True], ~same]))
-        size = np.diff(np.concatenate([start, [a.shape[0]]]))
-        for g in np.flatnonzero(size > 1).tolist():
-            s0, m = int(start[g]), int(size[g])
-            first, last = a[s0], a[s0 + m - 1]
-            msgs[int(first[3])].append((0, int(first[2]), int(last[3]), int(last[2])))   # keep, take last's values
-            for j in range(s0 + 1, s0 + m):
-                msgs[int(a[j, 3])].append((1, int(a[j, 2]), 0, 0))                       # drop
-    inst = alltoallv([torch.tensor(m, dtype=torch.int64).reshape(-1, 4) for m in msgs])
+    sent = [np.flatnonzero(owner == q) for q in range(world)]      # my rows, in the order each owner gets them
+    # round 1: half 0 of every key to its owner
+    got = [g.cpu().numpy() for g in alltoallv([torch.from_numpy(np.ascontiguousarray(key[o, 0])) for o in sent])]
+    k0 = np.concatenate(got) if got else np.zeros(0, np.int64)
+    src = np.repeat(np.arange(world, dtype=np.int64), [g.shape[0] for g in got])
+    pos = np.concatenate([np.arange(g.shape[0], dtype=np.int64) for g in got]) if got else np.zeros(0, np.int64)
+    o = np.argsort(k0, kind="stable")
+    eq = k0[o][1:] == k0[o][:-1]
+    mark = np.zeros(k0.size, dtype=bool)
+    mark[1:] |= eq
+    mark[:-1] |= eq
+    cand = np.sort(o[mark])                                        # by source rank, then position
+    # round 2: half 1 and the read index of each candidate, from its source
+    req = alltoallv([torch.from_numpy(np.ascontiguousarray(pos[cand][src[cand] == q])) for q in range(world)])
+    answers = []
+    for r, p in enumerate(req):
+        rows = sent[r][p.cpu().numpy().astype(np.int64)]
+        answers.append(torch.from_numpy(np.ascontiguousarray(np.stack([key[rows, 1], rows], axis=1))))
+    back1 = alltoallv(answers)
+    kv = np.concatenate([b.cpu().numpy().reshape(-1, 2) for b in back1]) if back1 else np.zeros((0, 2), np.int64)
+    t = np.stack([k0[cand], kv[:, 0], src[cand], kv[:, 1]], axis=1) if cand.size else np.zeros((0, 4), np.int64)
+    inst = alltoallv([torch.from_numpy(m) for m in _dup_messages(t, world)])
     inst = np.concatenate([x.cpu().numpy().reshape(-1, 4) for x in inst]) if inst else np.zeros((0, 4), np.int64)
     keep_take = inst[inst[:, 0] == 0]
     drop = inst[inst[:, 0] == 1, 1]
@@ -215,7 +248,10 @@ def set_job_totals(res, device=None) -> None:
     D = len(res.labels)
     local = np.zeros(D + 1, dtype=np.int64)
     if len(res.ids):
-        local[:D] = res.hits.sum(axis=0, dtype=np.uint64).astype(np.int64)
+        # a read named "misclassified" leaves the hits (result.py:43) but keeps its k-mers
+        m = _misclassified_row(res)
+        hits = res.hits if m is None else np.delete(res.hits, m, axis=0)
+        local[:D] = hits.sum(axis=0, dtype=np.uint64).astype(np.int64)
         local[D] = int(res.num_kmers.sum())
     t = torch.from_numpy(local)
     if device is not None:
@@ -391,21 +427,35 @@ def shard_path(output_path: Path, rank: int, world: int) -> Path:
     return output_path.with_name(f"{output_path.stem}.part{rank + 1}-of-{world}{output_path.suffix}")
 
 
+def _misclassified_row(res):
+    """Row of this shard's read literally named "misclassified" (None if
+    none): the reference pops it from the hits into the result's
+    "misclassified" field (result.py:43)."""
+    ids = res.ids
+    if "misclassified" not in ids:
+        return None
+    return (ids.tolist() if isinstance(ids, PackedIds) else list(ids)).index("misclassified")
+
+
 def _job_first_row(res, D: int) -> np.ndarray:
     """Hit row of the job's first read (first read of the lowest rank that has
-    one), which orders the labels of the job's "total" scores as the
+    one, a read named "misclassified" excepted: it is not in the reference's
+    hits), which orders the labels of the job's "total" scores as the
     reference's get_total_hits does (result.py:84-90)."""
     import torch
     dist = _dist()
     world = dist.get_world_size()
+    m = _misclassified_row(res)
+    first = 0 if m != 0 else 1  # the first row that is in the hits
+    have = len(res.ids) - (m is not None)
     flags = [torch.zeros(1, dtype=torch.int64, device=collective_device()) for _ in range(world)]
-    dist.all_gather(flags, _on_wire(torch.tensor([len(res.ids)], dtype=torch.int64)))
+    dist.all_gather(flags, _on_wire(torch.tensor([have], dtype=torch.int64)))
     owners = [r for r, f in enumerate(flags) if int(f.item()) > 0]
     if not owners:
         raise IndexError("list index out of range")  # get_total_hits on no reads, as the reference
     row = torch.zeros(D, dtype=torch.int64)
     if dist.get_rank() == owners[0]:
-        row = torch.from_numpy(res.hits[0].astype(np.int64))
+        row = torch.from_numpy(res.hits[first].astype(np.int64))
     row = _on_wire(row)
     dist.broadcast(row, src=owners[0])
     return row.cpu().numpy().astype(np.uint32)
@@ -485,6 +535,8 @@ def merge_result_shards(paths) -> dict:
             out["hits"], out["num_kmers"] = {}, {}
             out["scores"] = {}
         total = d["scores"].pop("total")
+        if d.get("misclassified") is not None:  # the shard that held the read named so (result.py:43)
+            out["misclassified"] = d["misclassified"]
         out["hits"].update(d["hits"])
         out["scores"].update(d["scores"])
         out["num_kmers"].update(d["num_kmers"])
@@ -563,7 +615,15 @@ def merge_result_files(paths, out_path: Path) -> None:
                 out.write(b"\n    }")
             else:
                 out.write(b"{}")
-            out.write(m0[m0.find(b',\n    "misclassified": '):])
+            # the "misclassified" section of the shard that held such a read (result.py:43), else shard 0's
+            tails = [m[m.find(b',\n    "misclassified": '):] for m in maps]
+            tail = tails[0]
+            for t in tails:
+                if not t.startswith(b',\n    "misclassified": null'):
+                    mis = t[:t.find(b',\n    "input_source": ')]
+                    tail = mis + tails[0][tails[0].find(b',\n    "input_source": '):]
+                    break
+            out.write(tail)
     finally:
         for m in maps:
             if isinstance(m, mmap.mmap):
