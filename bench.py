@@ -845,8 +845,15 @@ def host_path(wl, args, reps=3):
     # pinned output reused call after call, as a serving loop holds it
     hdt = narrowest_count_dtype(max_kmers(pr, wl.k, args.step))
     outs = {id(b): pinned_empty((pr.n, b.num_docs), hdt) for b in wl.banks}
+    def fresh(b):  # a never-touched pageable array: the OS faults each page as the copy-out reaches it
+        return b.query(pr, step=args.step, out=np.empty((pr.n, b.num_docs), np.uint32))
+
+    def touch(b):  # first-touch cost alone: one write per 4 KiB page of a fresh matrix-sized array
+        np.empty((pr.n, b.num_docs), np.uint32).reshape(-1).view(np.uint8)[::4096] = 0
+
     for name, fn in (("hits", lambda b: b.query(pr, step=args.step, hit_dtype=hdt, out=outs[id(b)])),
                      ("hits_u32_pageable", lambda b: b.query(pr, step=args.step)),
+                     ("hits_u32_fresh_pageable", fresh), ("first_touch_u32_matrix", touch),
                      ("totals", lambda b: b.query_totals(pr, step=args.step))):
         for b in wl.banks:  # warm
             fn(b)
@@ -855,12 +862,18 @@ def host_path(wl, args, reps=3):
             for b in wl.banks:
                 fn(b)
         dt = (time.perf_counter() - t) / reps
-        out[name] = {"ms_per_step": dt * 1e3, "probes_per_s": wl.probes_per_step() / wl.world / dt}
+        out[name] = {"ms_per_step": dt * 1e3}
+        if not name.startswith("first_touch"):
+            out[name]["probes_per_s"] = wl.probes_per_step() / wl.world / dt
     out["hit_dtype"] = np.dtype(hdt).name
     out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H.  hits: the n x D matrix in "
                    f"{np.dtype(hdt).name} (narrowed on the device; counts <= k-mers per read) into a reused pinned "
-                   "buffer (xs_query_hits); hits_u32_pageable: xs_query's uint32 matrix into a fresh pageable "
-                   "array; totals: D+1 counters.  The headline value starts with the reads in HBM")
+                   "buffer (xs_query_hits); hits_u32_pageable: Bank.query's default, xs_query's uint32 matrix into "
+                   "a pageable array from the recycled host pool (bank._HostPool: pages faulted once), the rows "
+                   "crossing PCIe as uint8 and widened on the host behind the probe; hits_u32_fresh_pageable: the "
+                   "same into a never-touched np.empty array, which adds the OS's first-touch faults, measured "
+                   "alone as first_touch_u32_matrix (no probe); totals: D+1 counters.  The headline value starts "
+                   "with the reads in HBM")
     return out
 
 

@@ -255,3 +255,31 @@ def test_doc_slices_cover_the_bank_in_byte_columns(tmp_path):
     p = tmp_path / "index.cobs_classic"
     p.write_bytes(oracle.cobs_classic_file(names, 21, 7, 11, np.zeros((11, 2), dtype=np.uint8)))
     assert cobs_classic_docs(p) == 13
+
+
+def test_host_pool_recycles_only_dropped_blocks():
+    """Bank.query's result arrays come from recycled host blocks
+    (bank._HostPool): a block is reused only once no array or view of it is
+    alive, and never beyond the pool's byte cap."""
+    import numpy as np
+    from xspect2_amd.bank import _HostPool
+    p = _HostPool(cap=64 << 20, min_bytes=1 << 20)
+    a = p.empty((1000, 4096), np.uint32)            # 16 MB
+    view = a[10:20]
+    del a
+    b = p.empty((1000, 4096), np.uint32)
+    assert not np.shares_memory(b, view)            # a view keeps its block busy
+    del view
+    c = p.empty((1000, 4096), np.uint32)
+    assert len(p.blocks) == 2                       # the first block again
+    mv = memoryview(b)
+    del b
+    d = p.empty((1000, 4096), np.uint32)
+    assert not np.shares_memory(d, np.asarray(mv)) and not np.shares_memory(d, c)
+    e = p.empty((1000, 4096), np.uint32)            # 4 blocks = the 64 MB cap
+    f = p.empty((1000, 4096), np.uint32)            # over the cap: a fresh array, not kept
+    assert len(p.blocks) == 4 and not any(np.shares_memory(f, x) for x in p.blocks)
+    del c, d, e, f, mv
+    g = p.empty((2000, 4096), np.uint32)            # 32 MB: free blocks make room for it
+    assert g.nbytes == 2000 * 4096 * 4 and sum(x.size for x in p.blocks) <= 64 << 20
+    assert p.empty((3, 3), np.uint8).base is None   # small requests: plain arrays

@@ -88,6 +88,53 @@ def pinned_empty(shape, dtype=np.uint32) -> np.ndarray:
     return np.asarray(_PinnedAlloc(max(n, 1)))[:n].view(dtype).reshape(shape)
 
 
+class _HostPool:
+    """Recycled pageable host blocks for the arrays Bank.query returns.
+
+    The first write to fresh pageable memory faults every page, and on the
+    MI355X boxes those faults neither batch nor spread over threads: 400 MB
+    (config 2's uint32 hit matrix) costs ~28 ms of first touch, more than the
+    whole query (profiles/r05_host_out.json).  So result arrays are views of
+    blocks kept here; a block goes back into service once no array refers to
+    it any more (every numpy view of a block holds the block itself as its
+    base, so the block's reference count says whether one is alive), and a
+    repeated query of the same size writes into pages faulted once.  At most
+    ``cap`` bytes are kept; larger requests get fresh arrays."""
+
+    def __init__(self, cap: int = 4 << 30, min_bytes: int = 8 << 20):
+        import sys
+        self._refs = sys.getrefcount
+        self.blocks: list[np.ndarray] = []
+        self.cap, self.min_bytes = cap, min_bytes
+
+    def _free(self, i: int) -> bool:
+        # references to block i: the list's and getrefcount's argument, and none from an array
+        return self._refs(self.blocks[i]) <= 2
+
+    def empty(self, shape, dtype) -> np.ndarray:
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        if n < self.min_bytes:
+            return np.empty(shape, dtype)
+        for i in range(len(self.blocks)):
+            if n <= self.blocks[i].size <= 2 * n and self._free(i):
+                return self.blocks[i][:n].view(dtype).reshape(shape)
+        kept = sum(b.size for b in self.blocks)
+        i = 0
+        while kept + n > self.cap and i < len(self.blocks):  # drop free blocks, oldest first
+            if self._free(i):
+                kept -= self.blocks.pop(i).size
+            else:
+                i += 1
+        if kept + n > self.cap:
+            return np.empty(shape, dtype)
+        self.blocks.append(np.empty(n, np.uint8))
+        return self.blocks[-1][:n].view(dtype).reshape(shape)
+
+
+_HOST_POOL = _HostPool()
+
+
 class Bank:
     """One filter bank resident on one GPU."""
 
@@ -259,7 +306,7 @@ class Bank:
                     raise ValueError(f"out must be a C-contiguous {(pr.n, cols)} {hit_dtype} array")
                 hits = out
             else:
-                hits = np.empty((pr.n, cols), dtype=hit_dtype)
+                hits = _HOST_POOL.empty((pr.n, cols), hit_dtype)  # recycled pages, see _HostPool
         nk = np.empty(pr.n, dtype=np.uint64)
         if dev:
             check(load().xs_query_hits_device(self.handle, pr.seqs_ptr, pr.seq_bytes, pr.offsets_ptr, pr.n,

@@ -915,7 +915,15 @@ constexpr uint64_t kDevChunkReads = 1u << 18;
 int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                uint32_t* d_hits, void* hits_host, uint64_t* d_nk, uint64_t* tot_host, int hit_bytes = 4,
                const DevReads* dev = nullptr, int wire_bytes = 0) {
-    const int wire = wire_bytes ? std::min(wire_bytes, hit_bytes) : hit_bytes;
+    int wire = wire_bytes ? std::min(wire_bytes, hit_bytes) : hit_bytes;
+    if (hits_host && wire != hit_bytes) {  // a pinned destination takes the rows by DMA as they are
+        hipPointerAttribute_t attr;
+        if (hipPointerGetAttributes(&attr, hits_host) == hipSuccess) {
+            if (attr.type == hipMemoryTypeHost) wire = hit_bytes;
+        } else {
+            (void)hipGetLastError();  // pageable memory is "not a HIP pointer"
+        }
+    }
     const uint64_t base = dev ? 0 : offsets[0];
     if (!dev)
         for (uint64_t r = 0; r < n; ++r)
