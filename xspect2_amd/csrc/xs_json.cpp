@@ -410,7 +410,7 @@ uint64_t xxh64(const unsigned char* p, uint64_t len, uint64_t seed) {
 // key per id, for finding ids repeated across the shards of a read-sharded
 // job without moving the ids themselves.
 int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* out) {
-    if ((!buf && n && offs[n]) || !offs || (!out && n)) return xs::set_error(XS_ERR_ARG, "null argument");
+    if (!offs || (!out && n) || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
     for (uint64_t i = 0; i < n; ++i) {
         if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
         const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);

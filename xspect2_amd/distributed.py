@@ -827,22 +827,29 @@ def _predict_doc_columns(model, input_file: Path, step: int, display_name: bool,
             cat_off = torch.cat([offs[q][:counts[q]] + base[q] for q in range(world)] +
                                 [torch.tensor([base[-1]], dtype=torch.int64, device=dev)])
             N = sum(counts)
-            if on_device:
-                d_hits = torch.empty((N, model.index.num_docs), dtype=torch.int32, device=dev)
-                d_nk = torch.empty(N, dtype=torch.int64, device=dev)
-                stream = torch.cuda.current_stream(dev)
-                model.index.query_device(cat_seq, base[-1], cat_off, N, step, d_hits, d_nk, None,
-                                         stream=stream.cuda_stream)
-                cols = exchange_doc_columns(d_hits, counts, dims, wire)
-                lo = int(np.sum(counts[:rank]))
-                nk = d_nk[lo:lo + n].cpu().numpy().view(np.uint64)
-            else:
-                buf = np.concatenate([cat_seq.numpy(), np.zeros(1, dtype=np.uint8)])
-                h, nk_all = model._query(PackedReads(buf, cat_off.numpy().astype(np.uint64)), step)
-                cols = exchange_doc_columns(torch.from_numpy(np.ascontiguousarray(h).astype(np.int32)),
-                                            counts, dims, wire)
-                lo = int(np.sum(counts[:rank]))
-                nk = np.asarray(nk_all, dtype=np.uint64)[lo:lo + n]
+            lo = int(np.sum(counts[:rank]))
+            # the probe of every rank's reads (it allocates N x D_r counts): a failure on one
+            # rank raises on every rank before the exchange, instead of leaving the others in it
+            err = None
+            try:
+                if on_device:
+                    d_hits = torch.empty((N, model.index.num_docs), dtype=torch.int32, device=dev)
+                    d_nk = torch.empty(N, dtype=torch.int64, device=dev)
+                    stream = torch.cuda.current_stream(dev)
+                    model.index.query_device(cat_seq, base[-1], cat_off, N, step, d_hits, d_nk, None,
+                                             stream=stream.cuda_stream)
+                    stream.synchronize()
+                    local = d_hits
+                    nk = d_nk[lo:lo + n].cpu().numpy().view(np.uint64)
+                else:
+                    buf = np.concatenate([cat_seq.numpy(), np.zeros(1, dtype=np.uint8)])
+                    h, nk_all = model._query(PackedReads(buf, cat_off.numpy().astype(np.uint64)), step)
+                    local = torch.from_numpy(np.ascontiguousarray(h).astype(np.int32))
+                    nk = np.asarray(nk_all, dtype=np.uint64)[lo:lo + n]
+            except Exception as e:  # noqa: BLE001 - raised on every rank by agree_or_raise
+                err = e
+            agree_or_raise(err)
+            cols = exchange_doc_columns(local, counts, dims, wire)
             hc = cols.cpu().numpy()
             hc = hc.view(np.uint16) if wire == torch.int16 else hc.view(np.uint32) if wire == torch.int32 else hc
             if n:
@@ -852,13 +859,18 @@ def _predict_doc_columns(model, input_file: Path, step: int, display_name: bool,
     finally:
         batches.close()
     D = len(labels)
-    if hits:
-        dt = max((h.dtype for h in hits), key=lambda t: t.itemsize)
-        hm = np.concatenate([h.astype(dt, copy=False) for h in hits]) if len(hits) > 1 else hits[0]
-        nk = np.concatenate(nks)
-    else:
-        hm, nk = np.zeros((0, D), np.uint8), np.zeros(0, np.uint64)
-    res = MatrixResult(slug, PackedIds.concat(ids) if ids else [], labels, hm, nk, sparse_sampling_step=step)
+    res, err = None, None
+    try:
+        if hits:
+            dt = max((h.dtype for h in hits), key=lambda t: t.itemsize)
+            hm = np.concatenate([h.astype(dt, copy=False) for h in hits]) if len(hits) > 1 else hits[0]
+            nk = np.concatenate(nks)
+        else:
+            hm, nk = np.zeros((0, D), np.uint8), np.zeros(0, np.uint64)
+        res = MatrixResult(slug, PackedIds.concat(ids) if ids else [], labels, hm, nk, sparse_sampling_step=step)
+    except Exception as e:  # noqa: BLE001 - raised on every rank by agree_or_raise
+        err = e
+    agree_or_raise(err)
     resolve_cross_shard_duplicates(res)
     set_job_totals(res, dev if on_device else None)
     res.input_source = input_file.name
