@@ -2,8 +2,10 @@
 config 2's 1M x 150 bp reads from pageable host memory against the D=100
 species bank, best of --reps calls each:
 
-  u32_fresh      xs_query: uint32 matrix into a fresh pageable array (bench's hits_u32_pageable)
-  u32_touched    the same into a reused (already faulted) pageable array
+  u32_pooled     Bank.query's default: xs_query's uint32 matrix into a pageable array from the
+                 recycled host pool (bench's hits_u32_pageable)
+  u32_fresh      the same into a never-touched np.empty array (bench's hits_u32_fresh_pageable)
+  u32_touched    the same into one reused (already faulted) pageable array
   u8_fresh       xs_query_hits uint8 into a fresh pageable array
   u8_pinned      xs_query_hits uint8 into a reused pinned array (bench's hits)
   totals         xs_query_totals (no matrix)
@@ -60,7 +62,8 @@ def main():
         a.reshape(-1).view(np.uint8)[::4096] = 0
 
     out = {
-        "u32_fresh": best(lambda: bank.query(pr)),
+        "u32_pooled": best(lambda: bank.query(pr)),
+        "u32_fresh": best(lambda: bank.query(pr, out=np.empty((pr.n, D), np.uint32))),
         "u32_touched": best(lambda: bank.query(pr, out=touched)),
         "u8_fresh": best(lambda: bank.query(pr, hit_dtype=np.uint8)),
         "u8_pinned": best(lambda: bank.query(pr, hit_dtype=np.uint8, out=pin8)),
