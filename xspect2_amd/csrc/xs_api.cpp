@@ -21,7 +21,6 @@
 #include "../../include/xspect_hip.h"
 
 #include <hip/hip_runtime.h>
-#include <sys/mman.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -748,7 +747,6 @@ class HitSink {
     ~HitSink() { (void)finish(); }
 
     int start(uint64_t total_bytes_out) {
-        total_ = total_bytes_out;
         if (wire_ == out_ && total_bytes_out >= 2 * kSinkPiece) {
             hipPointerAttribute_t attr;
             if (hipPointerGetAttributes(&attr, host_) == hipSuccess) direct_ = attr.type == hipMemoryTypeHost;
@@ -809,30 +807,8 @@ class HitSink {
             err_ = what;
         }
     }
-    // A fresh pageable output faults on first touch (the kernel zeroes each page
-    // as the copy-out reaches it, ~3x the copy's own time); touch every page in
-    // parallel first, while the bank stream probes the first chunks, asking for
-    // transparent huge pages where the kernel offers them.
-    void prefault() {
-        if (direct_ || total_ < (64u << 20)) return;
-        const uintptr_t pg = 4096, huge = 2u << 20;
-        const uintptr_t a = (reinterpret_cast<uintptr_t>(host_) + huge - 1) & ~(huge - 1);
-        const uintptr_t e = (reinterpret_cast<uintptr_t>(host_) + total_) & ~(huge - 1);
-        if (e > a) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
-        const uint64_t pages = (total_ + pg - 1) / pg;
-        const int t = threads_;
-        auto run = [&](uint64_t p0, uint64_t p1) {
-            for (uint64_t q = p0; q < p1; ++q) reinterpret_cast<volatile uint8_t*>(host_)[q * pg] = 0;
-        };
-        std::vector<std::thread> th;
-        const uint64_t per = (pages + t - 1) / t;
-        for (int i = 1; i < t && per * i < pages; ++i) th.emplace_back(run, per * i, std::min(pages, per * (i + 1)));
-        run(0, std::min(per, pages));
-        for (auto& x : th) x.join();
-    }
     void run() {
         if (hipSetDevice(b_->device) != hipSuccess) return fail_with(XS_ERR_HIP, "hipSetDevice failed in the hit copier");
-        prefault();
         std::deque<Piece> inflight;
         int next_slot = 0;
         for (;;) {
@@ -879,7 +855,6 @@ class HitSink {
     const uint8_t* src_;
     uint64_t cols_;
     int wire_, out_;
-    uint64_t total_ = 0;
     bool direct_ = false;
     int threads_ = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
     std::thread th_;
