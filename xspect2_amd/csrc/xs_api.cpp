@@ -914,13 +914,19 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         // partitions into L2 per chunk)
         const uint64_t per = hits_host ? std::max<uint64_t>(kDevChunkReads, (n + 3) / 4) : n;
         while (cut.back() < n) cut.push_back(std::min(n, cut.back() + per));
-        if (int rc = b->cut_ofs.ensure(cut.size() * 8)) return rc;
-        cut_ofs.resize(cut.size());
-        for (size_t j = 0; j < cut.size(); ++j)
-            HIPCHK(hipMemcpyAsync(static_cast<uint64_t*>(b->cut_ofs.p) + j, dev->offs + cut[j], 8, hipMemcpyDeviceToHost,
-                                  b->stream));
-        HIPCHK(hipStreamSynchronize(b->stream));
-        memcpy(cut_ofs.data(), b->cut_ofs.p, cut.size() * 8);
+        if (cut.size() == 2) {
+            // one chunk: its bytes are the batch's (offsets start at 0; seq_bytes bounds the
+            // last offset, which is all the probe's planner needs), no round trip to the device
+            cut_ofs = {0, dev->seq_bytes};
+        } else {
+            if (int rc = b->cut_ofs.ensure(cut.size() * 8)) return rc;
+            cut_ofs.resize(cut.size());
+            for (size_t j = 0; j < cut.size(); ++j)
+                HIPCHK(hipMemcpyAsync(static_cast<uint64_t*>(b->cut_ofs.p) + j, dev->offs + cut[j], 8,
+                                      hipMemcpyDeviceToHost, b->stream));
+            HIPCHK(hipStreamSynchronize(b->stream));
+            memcpy(cut_ofs.data(), b->cut_ofs.p, cut.size() * 8);
+        }
     } else {
         for (size_t limit = kHostFirst; cut.back() < n; limit = kHostChunk) {
             const uint64_t r0 = cut.back();
