@@ -302,6 +302,11 @@ int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int
  * probabilistic_filter_model.py:310, and sums totals over that dict,
  * result.py:76-90).  Any bytes (not only ASCII). */
 int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* out);
+/* out[i] = 1 if keys[i] is one of the m values of `set`, else 0: the owner
+ * rank of a read-sharded job finding the records whose key half another
+ * record shares (the candidates of a repeated id), in one pass over n keys
+ * with a hash set of the (few) shared values.  set may hold repeats. */
+int xs_u64_member_mask(const uint64_t* keys, uint64_t n, const uint64_t* set, uint64_t m, uint8_t* out);
 
 /* ---- FASTA/FASTQ reader (host; replaces Bio.SeqIO.parse via
  * get_record_iterator, src/xspect/file_io.py:47-79, on the predict path

@@ -102,3 +102,38 @@ def test_take_keeps_the_selected_ids_packed():
     for idx in ([], [0], [5, 0, 2], [1, 1, 3], list(range(6))):
         t = p.take(np.array(idx, dtype=np.int64))
         assert isinstance(t, PackedIds) and t.tolist() == [ids[i] for i in idx]
+
+
+def test_drop_keeps_every_other_id_in_order():
+    """PackedIds.drop (the repeated-id resolution of sharded jobs) equals the
+    list without the dropped positions: none, some, repeated indices, all."""
+    import numpy as np
+    from xspect2_amd.packing import PackedIds
+    rng = np.random.default_rng(3)
+    ids = [f"read_{i}" + "x" * int(rng.integers(0, 5)) for i in range(500)] + ["", "é", ""]
+    p = PackedIds.of(ids)
+    for drop in ([], [0], [502], [5, 5, 7, 499, 0], list(range(0, 503, 3)), list(range(503))):
+        keep = [s for i, s in enumerate(ids) if i not in set(drop)]
+        q = p.drop(np.array(drop, dtype=np.int64))
+        assert q.tolist() == keep and len(q) == len(keep)
+        assert q.tolist() == p.take(np.array([i for i in range(503) if i not in set(drop)], dtype=np.int64)).tolist()
+
+
+def test_u64_member_mask_matches_isin():
+    """xs_u64_member_mask (the owner's candidate search of a sharded job) =
+    numpy's isin, for random keys, repeats in the set, 0 and 2^64-1."""
+    import numpy as np
+    from xspect2_amd._lib import check, load
+    rng = np.random.default_rng(9)
+    keys = rng.integers(0, 1 << 62, 200_000, dtype=np.int64).view(np.uint64)
+    keys[:4] = [0, np.uint64(2**64 - 1), 5, 5]
+    for m in (0, 1, 7, 5000):
+        st = np.concatenate([keys[rng.integers(0, keys.size, m)], rng.integers(0, 1 << 62, m, dtype=np.int64)
+                             .view(np.uint64)]) if m else np.zeros(0, np.uint64)
+        if m:
+            st[:2] = [0, np.uint64(2**64 - 1)]
+        st = np.ascontiguousarray(st)
+        out = np.empty(keys.size, dtype=np.uint8)
+        check(load().xs_u64_member_mask(keys.ctypes.data, keys.size, st.ctypes.data if st.size else None, st.size,
+                                        out.ctypes.data))
+        assert np.array_equal(out.astype(bool), np.isin(keys, st))

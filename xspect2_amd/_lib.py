@@ -144,6 +144,7 @@ SIGNATURES = {
     "xs_ids_json_quote": (_int, [ctypes.c_char_p, _vp, _u64, _vp, _u64, _vp]),
     "xs_ids_has_duplicates": (_int, [ctypes.c_char_p, _vp, _u64, ctypes.POINTER(_int)]),
     "xs_ids_hash128": (_int, [ctypes.c_char_p, _vp, _u64, _vp]),
+    "xs_u64_member_mask": (_int, [_vp, _u64, _vp, _u64, _vp]),
     "xs_fastx_open": (_int, [ctypes.c_char_p, _int, _int, _int, _pp]),
     "xs_fastx_open_range": (_int, [ctypes.c_char_p, _int, _int, _int, _u32, _u32, _pp]),
     "xs_fastx_next": (_int, [_vp, _u64, ctypes.POINTER(FastxBatch)]),

@@ -183,12 +183,15 @@ def resolve_cross_shard_duplicates(res) -> int:
     k0 = np.concatenate(got) if got else np.zeros(0, np.int64)
     src = np.repeat(np.arange(world, dtype=np.int64), [g.shape[0] for g in got])
     pos = np.concatenate([np.arange(g.shape[0], dtype=np.int64) for g in got]) if got else np.zeros(0, np.int64)
-    o = np.argsort(k0, kind="stable")
-    eq = k0[o][1:] == k0[o][:-1]
-    mark = np.zeros(k0.size, dtype=bool)
-    mark[1:] |= eq
-    mark[:-1] |= eq
-    cand = np.sort(o[mark])                                        # by source rank, then position
+    srt = np.sort(k0)
+    shared = srt[1:][srt[1:] == srt[:-1]]                          # key halves held more than once
+    cand = np.zeros(0, np.int64)
+    if shared.size:                                                # their records, by source rank then position
+        from ._lib import check, load
+        hit = np.empty(k0.size, dtype=np.uint8)
+        shared = np.ascontiguousarray(shared)
+        check(load().xs_u64_member_mask(k0.ctypes.data, k0.size, shared.ctypes.data, shared.size, hit.ctypes.data))
+        cand = np.flatnonzero(hit)
     # round 2: half 1 and the read index of each candidate, from its source
     req = alltoallv([torch.from_numpy(np.ascontiguousarray(pos[cand][src[cand] == q])) for q in range(world)])
     answers = []
@@ -233,7 +236,7 @@ def resolve_cross_shard_duplicates(res) -> int:
         keep = np.ones(n, dtype=bool)
         keep[drop] = False
         rows = np.flatnonzero(keep)
-        res.ids = ids.take(rows) if isinstance(res.ids, PackedIds) else [res.ids[i] for i in rows.tolist()]
+        res.ids = ids.drop(drop) if isinstance(res.ids, PackedIds) else [res.ids[i] for i in rows.tolist()]
         res.hits = np.ascontiguousarray(res.hits[rows])
         res.num_kmers = np.ascontiguousarray(res.num_kmers[rows])
     return int(drop.size)

@@ -173,6 +173,25 @@ class PackedIds(Sequence):
                                            ctypes.byref(flag)))
         return bool(flag.value)
 
+    def drop(self, index) -> "PackedIds":
+        """All ids but those at `index` (int array), in order, still packed:
+        one pass over the bytes that stay (a few dropped ids of a large shard
+        cost what they are, not a gather of every kept byte)."""
+        idx = np.unique(np.asarray(index, dtype=np.int64))
+        n = len(self)
+        lens = (self.offs[1:] - self.offs[:-1]).astype(np.int64)
+        starts = self.offs[:-1][idx].astype(np.int64)
+        dl = lens[idx]
+        cut = np.zeros(dl.size + 1, dtype=np.int64)
+        np.cumsum(dl, out=cut[1:])
+        gone = np.repeat(starts - cut[:-1], dl) + np.arange(int(cut[-1]), dtype=np.int64)
+        buf = np.delete(np.frombuffer(self.buf, dtype=np.uint8), gone).tobytes()
+        keep = np.ones(n, dtype=bool)
+        keep[idx] = False
+        offs = np.zeros(n - idx.size + 1, dtype=np.uint64)
+        np.cumsum(lens[keep], out=offs[1:])
+        return PackedIds(buf, offs)
+
     def take(self, index) -> "PackedIds":
         """The ids at `index` (int array), in that order, still packed."""
         idx = np.asarray(index, dtype=np.int64)
