@@ -1,0 +1,12 @@
+# Round 5: the whole GPU suite after the host-output sink tests, the one-chunk
+# device batches and the repeated-id changes; the default bench line.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+F=gpurun_out/r05d; mkdir -p $F
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $F/smoke.log 2>&1 || { tail -20 $F/smoke.log; exit 10; }
+tail -1 $F/smoke.log
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $F/gpu_tests.log 2>&1 || { tail -40 $F/gpu_tests.log; exit 11; }
+tail -2 $F/gpu_tests.log
+timeout -k 10 600 python -u bench.py > $F/species.json 2> $F/species.err || { tail -30 $F/species.err; exit 12; }
+cut -c1-300 $F/species.json
