@@ -283,3 +283,28 @@ def test_host_pool_recycles_only_dropped_blocks():
     g = p.empty((2000, 4096), np.uint32)            # 32 MB: free blocks make room for it
     assert g.nbytes == 2000 * 4096 * 4 and sum(x.size for x in p.blocks) <= 64 << 20
     assert p.empty((3, 3), np.uint8).base is None   # small requests: plain arrays
+
+
+def test_host_pool_never_hands_one_block_to_two_threads():
+    """Bank.query runs from several threads (the reference's web workers):
+    arrays alive at the same time never share a block."""
+    import threading
+    import numpy as np
+    from xspect2_amd.bank import _HostPool
+    p = _HostPool(cap=1 << 30, min_bytes=1 << 20)
+    bad = []
+
+    def work(t):
+        for i in range(200):
+            a = p.empty((256, 4096), np.uint8)
+            a[:] = t
+            if not (a == t).all():
+                bad.append((t, i))
+            del a
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(8)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad and sum(b.size for b in p.blocks) <= 1 << 30

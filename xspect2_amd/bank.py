@@ -103,7 +103,9 @@ class _HostPool:
 
     def __init__(self, cap: int = 4 << 30, min_bytes: int = 8 << 20):
         import sys
+        import threading
         self._refs = sys.getrefcount
+        self._lock = threading.Lock()  # queries from several threads (the reference's web workers)
         self.blocks: list[np.ndarray] = []
         self.cap, self.min_bytes = cap, min_bytes
 
@@ -116,6 +118,10 @@ class _HostPool:
         n = int(np.prod(shape)) * dtype.itemsize
         if n < self.min_bytes:
             return np.empty(shape, dtype)
+        with self._lock:  # a block is checked free and handed out in one step
+            return self._take(n, shape, dtype)
+
+    def _take(self, n: int, shape, dtype) -> np.ndarray:
         for i in range(len(self.blocks)):
             if n <= self.blocks[i].size <= 2 * n and self._free(i):
                 return self.blocks[i][:n].view(dtype).reshape(shape)
