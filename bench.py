@@ -727,7 +727,7 @@ def self_check(wl, args, rank, world, dev):
             b.query_device(wl.d_seqs, wl.seq_bytes, wl.d_offs, wl.n, args.step, h, wl.d_nk, lt,
                            stream=wl.stream)
             torch.cuda.synchronize(dev)
-            want = torch.cat([h.view(torch.int32).to(torch.int64).sum(0), wl.d_nk.sum().reshape(1)])
+            want = torch.cat([h.sum(0, dtype=torch.int64), wl.d_nk.sum().reshape(1)])
             bad_local += int((lt != want).sum().item())
             local.append(lt)
         mine.update(oracle_sample())  # the hit rows this query wrote (also under --totals-only)

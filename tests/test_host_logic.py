@@ -283,6 +283,8 @@ def test_host_pool_recycles_only_dropped_blocks():
     g = p.empty((2000, 4096), np.uint32)            # 32 MB: free blocks make room for it
     assert g.nbytes == 2000 * 4096 * 4 and sum(x.size for x in p.blocks) <= 64 << 20
     assert p.empty((3, 3), np.uint8).base is None   # small requests: plain arrays
+    kept = sum(x.size for x in p.blocks)
+    assert p.release() == kept - g.nbytes and [b.size for b in p.blocks] == [g.nbytes]  # g's block stays
 
 
 def test_host_pool_never_hands_one_block_to_two_threads():

@@ -138,7 +138,25 @@ class _HostPool:
         return self.blocks[-1][:n].view(dtype).reshape(shape)
 
 
+    def release(self) -> int:
+        """Forget every block no array refers to any more; returns the bytes let go."""
+        with self._lock:
+            freed, i = 0, 0
+            while i < len(self.blocks):
+                if self._free(i):
+                    freed += self.blocks.pop(i).size
+                else:
+                    i += 1
+            return freed
+
+
 _HOST_POOL = _HostPool()
+
+
+def release_host_memory() -> int:
+    """Give back the host blocks ``Bank.query`` keeps for reuse (those no
+    result array still uses); returns the bytes released."""
+    return _HOST_POOL.release()
 
 
 class Bank:
