@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -187,7 +188,50 @@ int main() {
         std::vector<uint64_t> key(2 * (off.size() - 1));
         if (xs_ids_hash128(exact.data(), off.data(), off.size() - 1, key.data())) ++unexpected;
     }
+    // a large batch takes the threaded path (n / 2^16 threads): keys equal the per-id ones;
+    // a null offsets argument with ids is refused, not dereferenced
+    {
+        const uint64_t n = 300000;
+        std::vector<uint64_t> off{0};
+        std::string buf;
+        for (uint64_t i = 0; i < n; ++i) {
+            buf += "read_" + std::to_string(i);
+            off.push_back(buf.size());
+        }
+        std::vector<char> exact(buf.begin(), buf.end());
+        std::vector<uint64_t> key(2 * n), one(2);
+        if (xs_ids_hash128(exact.data(), off.data(), n, key.data())) ++unexpected;
+        for (uint64_t i = 0; i < n; i += 997) {
+            const uint64_t o2[2] = {0, off[i + 1] - off[i]};
+            if (xs_ids_hash128(exact.data() + off[i], o2, 1, one.data()) || one[0] != key[2 * i] ||
+                one[1] != key[2 * i + 1])
+                ++unexpected;
+        }
+        if (xs_ids_hash128(nullptr, nullptr, 5, key.data()) == 0) ++unexpected;
+        else ++errors;
+    }
+    // member mask (xs_u64_member_mask): threaded pass over 400 k keys against sets with repeats,
+    // 0 and 2^64-1, checked against std::set
+    for (int trial = 0; trial < 6; ++trial) {
+        const uint64_t n = 400000, m = trial == 0 ? 0 : 1000u * (uint64_t)trial;
+        std::vector<uint64_t> keys(n), set;
+        for (auto& k : keys) k = ((uint64_t)rng() << 32) ^ rng();
+        keys[0] = 0;
+        keys[1] = ~0ull;
+        for (uint64_t j = 0; j < m; ++j) set.push_back(j % 2 ? keys[rng() % n] : ((uint64_t)rng() << 32) ^ rng());
+        if (m) {
+            set.push_back(0);
+            set.push_back(~0ull);
+            set.push_back(set[0]);
+        }
+        std::vector<uint8_t> out(n, 7);
+        if (xs_u64_member_mask(keys.data(), n, set.empty() ? nullptr : set.data(), set.size(), out.data())) ++unexpected;
+        std::set<uint64_t> ref(set.begin(), set.end());
+        for (uint64_t i = 0; i < n; ++i)
+            if (out[i] != (ref.count(keys[i]) ? 1 : 0)) ++unexpected;
+    }
     printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices, "
-           "20 id-key batches; %d clean error returns, %d on well-formed input\n", files, errors, unexpected);
+           "20 id-key batches + a threaded one, 6 member masks; %d clean error returns, %d on well-formed input\n",
+           files, errors, unexpected);
     return unexpected ? 1 : 0;
 }
