@@ -53,12 +53,18 @@ class GpuSearch:
         self.names = [(_lib.xs_bank_doc_name(self.h, d) or str(d).encode()).decode()
                       for d in range(self.D)]
 
-    def search_batch(self, seqs, step=1):
-        """seqs: list[str] -> (hits uint32 [n, D], num_kmers uint64 [n])."""
+    def search_batch(self, seqs, step=1, out=None):
+        """seqs: list[str] -> (hits uint32 [n, D], num_kmers uint64 [n]).
+        out: a reused C-contiguous uint32 [n, D] array; a serving loop passes
+        one to skip the OS's first-touch faults of a fresh matrix, which cost
+        more than the query itself at 10^6 reads."""
         data = [s.encode() for s in seqs]
         offs = np.zeros(len(data) + 1, np.uint64)
         offs[1:] = np.cumsum([len(b) for b in data])
-        hits = np.empty((len(data), self.D), np.uint32)
+        if out is not None and (out.shape != (len(data), self.D) or out.dtype != np.uint32
+                                or not out.flags.c_contiguous):
+            raise ValueError("out must be a C-contiguous uint32 [n, D] array")
+        hits = np.empty((len(data), self.D), np.uint32) if out is None else out
         nk = np.empty(len(data), np.uint64)
         _check(_lib.xs_query(self.h, b"".join(data),
                              offs.ctypes.data_as(C.POINTER(C.c_uint64)), len(data), step,

@@ -93,10 +93,15 @@ def test_stub_search_matches_oracle(oracle_mod, tmp_path):
     s = mod.GpuSearch(path)
     assert (s.k, s.D, s.names) == (k, D, [f"sp{i}" for i in range(D)])
     reads = [q[o:o + 150].decode() for q in seqs for o in (0, 100)] + ["ACGT", ""]
+    reuse = np.zeros((len(reads), D), np.uint32)
     for step in (1, 3):
         got, nk = s.search_batch(reads, step)
         want, want_n = ob.query([r.encode() for r in reads], step=step)
         assert np.array_equal(got, want.reshape(got.shape)) and np.array_equal(nk, want_n)
+        got2, _ = s.search_batch(reads, step, out=reuse)        # a serving loop's reused matrix
+        assert got2 is reuse and np.array_equal(reuse, want.reshape(got.shape))
+    with pytest.raises(ValueError):
+        s.search_batch(reads, 1, out=np.zeros((len(reads), D), np.uint16))
     res = s.search(reads[0])
     assert res[0].doc_name == "sp0" and res[0].score == 130
     assert [r.score for r in res] == sorted((r.score for r in res), reverse=True)
