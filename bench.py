@@ -484,9 +484,7 @@ def main():
     per_rank = None
     if world > 1:
         # every rank's own timed region and probe time; the line's time is the max
-        mine = torch.tensor([elapsed, probe_ms], dtype=torch.float64, device=dev if not SHARE_GPU else "cpu")
-        parts = [torch.zeros_like(mine) for _ in range(world)]
-        dist.all_gather(parts, mine)
+        parts = all_gather_host(torch.tensor([elapsed, probe_ms], dtype=torch.float64), world)
         el = [float(p[0].item()) for p in parts]
         pm = [float(p[1].item()) for p in parts]
         elapsed = max(el)
@@ -674,6 +672,19 @@ def oracle_banks(wl):
     return wl._obanks
 
 
+def all_gather_host(t, world: int) -> list:
+    """Every rank's copy of tensor `t`, in rank order, on the host: the
+    collective runs on the current GPU under RCCL (nccl wants device tensors
+    for input and outputs alike) and on the CPU under gloo."""
+    import torch
+    import torch.distributed as dist
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    src = t.to(dev)
+    parts = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(parts, src)
+    return [p.cpu() for p in parts]
+
+
 def _checksum(x, row0: int):
     """Position-weighted int64 checksum of an integer matrix block whose first
     row is row `row0` of its job-wide matrix (equal blocks <=> equal sums, up to
@@ -734,9 +745,8 @@ def self_check(wl, args, rank, world, dev):
         mine["local_totals_mismatches"] = bad_local
         loc = torch.cat(local).cpu()
         if world > 1:
-            parts = [torch.zeros_like(loc) for _ in range(world)]
-            dist.all_gather(parts, loc.to(dev) if dist.get_backend() == "nccl" else loc)
-            host_sum = np.sum([p.cpu().numpy().view(np.uint64) for p in parts], axis=0, dtype=np.uint64)
+            parts = all_gather_host(loc, world)
+            host_sum = np.sum([p.numpy().view(np.uint64) for p in parts], axis=0, dtype=np.uint64)
         else:
             host_sum = loc.numpy().view(np.uint64)
         reduced = torch.cat([t.cpu() for t in wl.d_tot]).numpy().view(np.uint64)
@@ -747,8 +757,7 @@ def self_check(wl, args, rank, world, dev):
         from xspect2_amd.distributed import shard_range
         sent = torch.tensor([_checksum(wl.d_hits[0][a:b], a) for a, b in
                              (shard_range(wl.n, q, world) for q in range(world))], dtype=torch.int64)
-        got = [torch.zeros_like(sent) for _ in range(world)]
-        dist.all_gather(got, sent.to(dev) if dist.get_backend() == "nccl" else sent)
+        got = all_gather_host(sent, world)
         a, _ = shard_range(wl.n, rank, world)
         bad, c0 = 0, 0
         for r, d in enumerate(wl.layout[0]):

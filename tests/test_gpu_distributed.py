@@ -191,3 +191,19 @@ def test_exchange_doc_columns_on_device(pg, wire):
     out = distributed.exchange_doc_columns(hits, [3001], [37], dt)
     assert out.dtype == dt and out.device == hits.device and tuple(out.shape) == (3001, 37)
     assert torch.equal(out.to(torch.int64), hits.to(torch.int64))
+
+
+def test_bench_gathers_run_on_the_device_under_rccl(pg):
+    """bench.py's per-rank gathers (timings, local totals, exchange checksums)
+    under an RCCL group: input and outputs on the device, results on the host
+    (world 1 here; the driver's 8-GPU run takes the same call)."""
+    import sys
+    from pathlib import Path
+    import torch
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+    import bench
+    t = torch.arange(7, dtype=torch.int64) * 3
+    out = bench.all_gather_host(t, 1)
+    assert len(out) == 1 and out[0].device.type == "cpu" and torch.equal(out[0], t)
+    f = bench.all_gather_host(torch.tensor([1.5, 2.5], dtype=torch.float64), 1)
+    assert torch.equal(f[0], torch.tensor([1.5, 2.5], dtype=torch.float64))
