@@ -120,6 +120,10 @@ def parse():
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r04_traffic.json"))
+    ap.add_argument("--rccl-world1", action="store_true",
+                    help="rehearsal: a one-rank RCCL process group running every collective of the N>1 path "
+                         "(the all-reduce of totals or the column exchange, the per-rank gathers and checks) "
+                         "on a one-GPU box")
     ap.add_argument("--launch-timeout", type=float, default=1800.0,
                     help="self-launched N>1 runs: seconds before the parent kills every rank")
     args = ap.parse_args()
@@ -212,12 +216,13 @@ def log(rank, *a):
 class Workload:
     """Banks + a step closure for one benchmark configuration."""
 
-    def __init__(self, args, rank, world, dev, stream):
+    def __init__(self, args, rank, world, dev, stream, pg=False):
         import torch
         from xspect2_amd.bank import Bank, bloom_parameters, cobs_signature_size
         from xspect2_amd.synth import make_genomes, make_reads
 
         self.args, self.rank, self.world, self.dev = args, rank, world, dev
+        self.pg = pg  # a process group: the N>1 collectives run (also at world 1 under --rccl-world1)
         s = stream.cuda_stream
         self.stream = s
         w = args.workload
@@ -283,7 +288,7 @@ class Workload:
         self.d_tot = [torch.zeros(d + 1, dtype=torch.int64, device=dev) for d in self.docs]
         self.nk_read = (args.read_len - self.k + args.step) // args.step
         self.kmers = self.n * self.nk_read
-        if w == "multigenus" and world > 1:
+        if w == "multigenus" and pg:
             # the library's docs-sharded gather (xspect2_amd.distributed): hit rows
             # travel in the narrowest type that holds a read's k-mer count (1 byte
             # for 150 bp reads), narrowed and widened on the device; the layout
@@ -358,7 +363,7 @@ class Workload:
         for b, h, t in zip(self.banks, self.d_hits, self.d_tot):
             b.query_device(self.d_seqs, self.seq_bytes, self.d_offs, self.n, self.args.step,
                            None if self.args.totals_only else h, self.d_nk, t, stream=self.stream)
-        if self.world > 1:
+        if self.pg:
             from xspect2_amd import distributed
             if self.args.workload == "multigenus":
                 # docs sharded, output sharded by reads: every rank's hit columns of
@@ -434,7 +439,13 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist_info = {"dist_backend": None, "rccl_world": None, "rank_devices": None}
-    if world > 1:
+    pg = world > 1 or args.rccl_world1
+    if pg:
+        if world == 1:  # --rccl-world1
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if SHARE_GPU:
             dist.init_process_group("gloo")
         else:
@@ -445,7 +456,7 @@ def main():
             raise RuntimeError(f"process group has {dist_info['rccl_world']} ranks, WORLD_SIZE={world}")
     stream = torch.cuda.current_stream(dev)
     t_setup = time.time()
-    wl = Workload(args, rank, world, dev, stream)
+    wl = Workload(args, rank, world, dev, stream, pg)
     log(rank, f"{args.workload}: {len(wl.banks)} bank(s), docs={wl.docs}, "
               f"{sum(b.info.device_bytes for b in wl.banks) / 1e9:.2f} GB in HBM, setup {time.time() - t_setup:.1f}s")
 
@@ -457,14 +468,14 @@ def main():
         b.probe_stats()  # reset
         b.probe_rows()
         b.pass_stats()
-    if world > 1:
+    if pg:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         wl.step()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launches, probe_ms_total, probe_ms_max = 0, 0.0, 0.0
@@ -482,7 +493,7 @@ def main():
         probe_ms_max = max(probe_ms_max, mx)
     probe_ms = probe_ms_total / max(1, launches)
     per_rank = None
-    if world > 1:
+    if pg:
         # every rank's own timed region and probe time; the line's time is the max
         parts = all_gather_host(torch.tensor([elapsed, probe_ms], dtype=torch.float64), world)
         el = [float(p[0].item()) for p in parts]
@@ -498,7 +509,7 @@ def main():
     if args.workload == "genus":  # member k-mers / sampled k-mers (steers the rbloom probe path)
         wl.config["member_fraction"] = round(int(tot[0]) / max(1, int(tot[-1])), 4)
     # every rank checks its own values (oracle sample, totals, exchanged columns); outside the timed region
-    checks = self_check(wl, args, rank, world, dev)
+    checks = self_check(wl, args, rank, world, dev, pg)
 
     value = wl.probes_per_step() * args.steps / elapsed
     from xspect2_amd._lib import XS_PATH_PARTITIONED
@@ -650,7 +661,7 @@ def main():
         print(json.dumps(line), flush=True)
     for b in wl.banks:
         b.close()
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
     if not checks["ok"]:
         sys.exit(3)
@@ -696,7 +707,7 @@ def _checksum(x, row0: int):
     return int((x.to(torch.int64) * (r * 1000003 + c + 1)).sum().item())
 
 
-def self_check(wl, args, rank, world, dev):
+def self_check(wl, args, rank, world, dev, pg=None):
     """Every rank checks the values of its last step (outside the timed region):
 
     * its GPU hit rows of `--check-reads` reads spread over its shard against
@@ -744,7 +755,7 @@ def self_check(wl, args, rank, world, dev):
         mine.update(oracle_sample())  # the hit rows this query wrote (also under --totals-only)
         mine["local_totals_mismatches"] = bad_local
         loc = torch.cat(local).cpu()
-        if world > 1:
+        if pg:
             parts = all_gather_host(loc, world)
             host_sum = np.sum([p.numpy().view(np.uint64) for p in parts], axis=0, dtype=np.uint64)
         else:
@@ -753,7 +764,7 @@ def self_check(wl, args, rank, world, dev):
         mine["allreduce_vs_host_sum_mismatches"] = int(np.count_nonzero(reduced != host_sum))
     else:
         mine.update(oracle_sample())
-    if args.workload == "multigenus" and world > 1:
+    if args.workload == "multigenus" and pg:
         from xspect2_amd.distributed import shard_range
         sent = torch.tensor([_checksum(wl.d_hits[0][a:b], a) for a, b in
                              (shard_range(wl.n, q, world) for q in range(world))], dtype=torch.int64)
@@ -765,7 +776,7 @@ def self_check(wl, args, rank, world, dev):
             c0 += d
         mine["exchange_block_mismatches"] = bad
     keys = sorted(k for k in mine if k.endswith("mismatches"))
-    if world > 1:
+    if pg:
         allm: list = [None] * world
         dist.all_gather_object(allm, mine)
     else:
