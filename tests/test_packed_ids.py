@@ -137,3 +137,17 @@ def test_u64_member_mask_matches_isin():
         check(load().xs_u64_member_mask(keys.ctypes.data, keys.size, st.ctypes.data if st.size else None, st.size,
                                         out.ctypes.data))
         assert np.array_equal(out.astype(bool), np.isin(keys, st))
+
+
+def test_index_finds_the_first_equal_id():
+    """PackedIds.index (the sharded totals' search for a read named
+    "misclassified") = list.index, also for prefixes, suffixes and repeats."""
+    import pytest
+    from xspect2_amd.packing import PackedIds
+    ids = ["amisclassified", "misclassifiedx", "mis", "misclassified", "", "misclassified", "é"]
+    p = PackedIds.of(ids[:-1])
+    for s in ("misclassified", "mis", "", "amisclassified", "misclassifiedx"):
+        assert p.index(s) == ids.index(s)
+    with pytest.raises(ValueError):
+        p.index("classified")
+    assert PackedIds.of(ids).index("é") == 6

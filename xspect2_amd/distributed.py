@@ -437,7 +437,7 @@ def _misclassified_row(res):
     ids = res.ids
     if "misclassified" not in ids:
         return None
-    return (ids.tolist() if isinstance(ids, PackedIds) else list(ids)).index("misclassified")
+    return ids.index("misclassified")
 
 
 def _job_first_row(res, D: int) -> np.ndarray:

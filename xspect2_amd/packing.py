@@ -132,6 +132,22 @@ class PackedIds(Sequence):
     def __iter__(self):
         return iter(self.tolist())
 
+    def index(self, s: str) -> int:
+        """Position of the first id equal to `s` (ValueError if none), found by
+        a byte search of the buffer for ASCII ids: no Python string per id."""
+        if not isinstance(s, str) or not (self.is_ascii and s.isascii()) or self._list is not None or not s:
+            return self.tolist().index(s)
+        key = s.encode("ascii")
+        starts = self.offs[:-1]
+        pos = self.buf.find(key)
+        while pos >= 0:
+            lo, hi = np.searchsorted(starts, pos, side="left"), np.searchsorted(starts, pos, side="right")
+            for i in range(int(lo), int(hi)):
+                if int(self.offs[i + 1]) == pos + len(key):
+                    return i
+            pos = self.buf.find(key, pos + 1)
+        raise ValueError(f"{s!r} is not in the ids")
+
     def __contains__(self, s) -> bool:
         if not isinstance(s, str):
             return False
