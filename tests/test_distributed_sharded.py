@@ -56,7 +56,7 @@ class OracleIndex:
 
 
 def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int = 0, short_at: int = -1,
-           mis_at: int = -1):
+           mis_at: int = -1, name: str = "misclassified"):
     """A species model over 6 synthetic genomes (oracle bank), its reads as a
     FASTQ file (written by the parent before the ranks start: a rank must not
     rewrite a file another rank is reading)."""
@@ -92,7 +92,7 @@ def _setup(tmp: Path, n_reads: int, svm: bool, write: bool = True, id_mod: int =
         g = genomes[i % 6] if i % 7 else acgt[rng.integers(0, 4, 3000)].tobytes()
         L = int(rng.integers(K + 1, 200)) if i != short_at else K  # len <= k: the reference raises
         s = int(rng.integers(0, len(g) - L))
-        rid = "misclassified" if i == mis_at else f"read_{i % id_mod if id_mod else i}"
+        rid = name if i == mis_at else f"read_{i % id_mod if id_mod else i}"
         reads.append((rid, g[s:s + L].decode()))
     fq = tmp / "reads.fq"
     if write:
@@ -193,7 +193,7 @@ def test_repeated_ids_across_shards_follow_the_reference_dict(tmp_path, world, i
     assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "single.json").read_bytes()
 
 
-def _mis_worker(rank: int, world: int, port: int, tmp: str, n_reads: int, mis_at: int):
+def _mis_worker(rank: int, world: int, port: int, tmp: str, n_reads: int, mis_at: int, name: str = "misclassified"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, str(ROOT))
     import torch.distributed as dist
@@ -201,8 +201,12 @@ def _mis_worker(rank: int, world: int, port: int, tmp: str, n_reads: int, mis_at
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        model, fq = _setup(Path(tmp), n_reads, True, write=False, mis_at=mis_at)
-        distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / "mis.json")
+        model, fq = _setup(Path(tmp), n_reads, True, write=False, mis_at=mis_at, name=name)
+        try:
+            distributed.classify_species_sharded(model, fq, Path(tmp) / "out" / "mis.json")
+            (Path(tmp) / f"rank{rank}.txt").write_text("ok")
+        except Exception as e:  # noqa: BLE001
+            (Path(tmp) / f"rank{rank}.txt").write_text(f"{type(e).__name__}: {e}")
     finally:
         dist.destroy_process_group()
 
@@ -230,6 +234,23 @@ def test_read_named_misclassified_in_any_shard(tmp_path, world, mis_at):
     assert distributed.merge_result_shards(shards) == want
     distributed.merge_result_files(shards, tmp_path / "merged.json")
     assert (tmp_path / "merged.json").read_bytes() == (tmp_path / "single.json").read_bytes()
+
+
+@pytest.mark.timeout(180)
+@pytest.mark.parametrize("world,at", [(3, 590), (2, 0)])
+def test_read_named_total_raises_on_every_rank(tmp_path, world, at):
+    """A read named "total" is the reference's reserved key (result.py:33-36:
+    ValueError); in whichever shard it falls, every rank raises that error
+    instead of the others waiting in the totals' all-reduce."""
+    import torch.multiprocessing as mp
+    from xspect2_amd.result import ModelResult
+    n_reads = 600
+    with pytest.raises(ValueError) as want:
+        ModelResult("m", {"total": {"a": 1}}, {"total": 1})
+    _setup(tmp_path, n_reads, True, mis_at=at, name="total")
+    mp.spawn(_mis_worker, args=(world, _free_port(), str(tmp_path), n_reads, at, "total"), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f"rank{r}.txt").read_text() == f"ValueError: {want.value}"
 
 
 @pytest.mark.timeout(180)
