@@ -253,6 +253,39 @@ def test_read_named_total_raises_on_every_rank(tmp_path, world, at):
         assert (tmp_path / f"rank{r}.txt").read_text() == f"ValueError: {want.value}"
 
 
+def _empty_worker(rank: int, world: int, port: int, tmp: str):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, str(ROOT))
+    import torch.distributed as dist
+    from xspect2_amd import distributed
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model, _ = _setup(Path(tmp), 10, True, write=False)
+        try:
+            distributed.classify_species_sharded(model, Path(tmp) / "empty.fq", Path(tmp) / "out" / "e.json")
+            (Path(tmp) / f"rank{rank}.txt").write_text("ok")
+        except Exception as e:  # noqa: BLE001
+            (Path(tmp) / f"rank{rank}.txt").write_text(f"{type(e).__name__}: {e}")
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_empty_input_raises_index_error_on_every_rank(tmp_path):
+    """An input without records: the reference's get_total_hits indexes the
+    first hit row of an empty dict (result.py:86, IndexError); the sharded job
+    raises that on every rank, as one process's save does."""
+    import torch.multiprocessing as mp
+    model, _ = _setup(tmp_path, 10, True)
+    (tmp_path / "empty.fq").write_text("")
+    with pytest.raises(IndexError) as want:  # the SVM model's predict already asks for the totals
+        model.predict_columnar(tmp_path / "empty.fq").save(tmp_path / "single.json")
+    mp.spawn(_empty_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert (tmp_path / f"rank{r}.txt").read_text() == f"IndexError: {want.value}"
+
+
 @pytest.mark.timeout(180)
 @pytest.mark.parametrize("world", [2, 3])
 def test_an_error_on_one_rank_raises_on_every_rank(tmp_path, world):
