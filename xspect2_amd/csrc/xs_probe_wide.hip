@@ -22,13 +22,10 @@ struct ChunkLanes {  // bits r of a 32-row column with r % C == 0
 };
 
 // Min blocks per CU = waves per SIMD the register budget is sized for.  4/5/6
-// force spills and run slower on every workload (profiles/r01_wide_occupancy.txt);
-// overridable for A/B builds (tools/build_variant.sh).
-#ifndef XS_WIDE_MIN_BLOCKS
-#define XS_WIDE_MIN_BLOCKS 2
-#endif
+// force spills and run slower on every workload (profiles/r01_wide_occupancy.txt).
+constexpr int kWideMinBlocks = 2;
 template <int KT, int HT, int C, int P, int GM>
-__global__ void __launch_bounds__(kProbeThreads, XS_WIDE_MIN_BLOCKS) probe_cobs_wide(ReadView rv, CobsView bv,
+__global__ void __launch_bounds__(kProbeThreads, kWideMinBlocks) probe_cobs_wide(ReadView rv, CobsView bv,
                                                                     uint32_t* __restrict__ hits,
                                                                     uint64_t* __restrict__ partials,
                                                                     uint32_t dpad) {
