@@ -64,12 +64,12 @@ def _windows(genomes, per_doc=20, seed=11):
     return seqs, np.asarray(docs)
 
 
-def _query(bank, torch, dev, r, r_offs, cols):
+def _query(bank, torch, dev, r, r_offs, cols, step=1):
     hits = torch.empty((N, cols), dtype=torch.int32, device=dev)
     nk = torch.empty(N, dtype=torch.int64, device=dev)
     tot = torch.zeros(cols + 1, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev)
-    bank.query_device(r, N * L, r_offs, N, 1, hits, nk, tot, stream=s.cuda_stream)
+    bank.query_device(r, N * L, r_offs, N, step, hits, nk, tot, stream=s.cuda_stream)
     torch.cuda.synchronize(dev)
     return (hits.cpu().numpy().view(np.uint32), nk.cpu().numpy().view(np.uint64),
             tot.cpu().numpy().view(np.uint64), bank.probe_path())
@@ -111,6 +111,17 @@ def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
     assert np.array_equal(h1[ids], want_h) and np.array_equal(n1[ids], want_n)
     wo, _ = ob.query(seqs)
     assert np.array_equal(wo, wh)
+
+    # sparse sampling (step 3: 44 k-mers per read, probabilistic_filter_model.py:462) at full
+    # size: both paths equal, the counts and totals consistent, the oracle sample equal
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    s0, m0, u0, _ = _query(bank, torch, dev, r, r_offs, D, step=3)
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
+    s1, m1, u1, q1 = _query(bank, torch, dev, r, r_offs, D, step=3)
+    assert q1 == _lib.XS_PATH_PARTITIONED and np.array_equal(s0, s1) and np.array_equal(m0, m1)
+    assert (m1 == (NK + 2) // 3).all() and np.array_equal(u1[:D], s1.sum(axis=0, dtype=np.uint64))
+    want_h, want_n = ob.query([reads[i].tobytes() for i in ids], step=3)
+    assert np.array_equal(s1[ids], want_h) and np.array_equal(m1[ids], want_n)
     bank.close()
 
 
