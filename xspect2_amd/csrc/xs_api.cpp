@@ -744,7 +744,8 @@ class HitSink {
           wire_(wire), out_(out) {}
     HitSink(const HitSink&) = delete;
     HitSink& operator=(const HitSink&) = delete;
-    ~HitSink() { (void)finish(); }
+    // an early return of the caller: the copies stop, and the caller's error stays the one reported
+    ~HitSink() { join(); }
 
     int start(uint64_t total_bytes_out) {
         if (wire_ == out_ && total_bytes_out >= 2 * kSinkPiece) {
@@ -772,17 +773,20 @@ class HitSink {
     }
     // no more rows: wait for the copies; the worker's error, if any, becomes this thread's
     int finish() {
-        if (!th_.joinable()) return XS_OK;
+        join();
+        return rc_ ? xs::set_error(rc_, err_.c_str()) : XS_OK;
+    }
+
+  private:
+    void join() {
+        if (!th_.joinable()) return;
         {
             std::lock_guard<std::mutex> g(mu_);
             closed_ = true;
         }
         cv_.notify_one();
         th_.join();
-        return rc_ ? xs::set_error(rc_, err_.c_str()) : XS_OK;
     }
-
-  private:
     struct Job {
         uint64_t r0, r1;
         hipEvent_t ev;
@@ -832,7 +836,10 @@ class HitSink {
                     continue;
                 }
                 if ((int)inflight.size() == kSinkSlots - 1) {  // the oldest piece out of its slot first
-                    if (int rc = copy_out(inflight.front())) return fail_with(rc, "hit copy-out failed");
+                    if (int rc = copy_out(inflight.front())) {
+                        fail_with(rc, "hit copy-out failed");
+                        break;
+                    }
                     inflight.pop_front();
                 }
                 const int slot = next_slot;
@@ -844,9 +851,10 @@ class HitSink {
             if (e != hipSuccess) fail_with(XS_ERR_HIP, hipGetErrorString(e));
         }
         while (!inflight.empty() && !rc_) {
-            if (int rc = copy_out(inflight.front())) return fail_with(rc, "hit copy-out failed");
+            if (int rc = copy_out(inflight.front())) fail_with(rc, "hit copy-out failed");
             inflight.pop_front();
         }
+        // after a failure too: no DMA may still be writing a staging slot when the call returns
         if (hipStreamSynchronize(b_->d2h_stream) != hipSuccess) fail_with(XS_ERR_HIP, "hit D2H failed");
     }
 
