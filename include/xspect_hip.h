@@ -31,7 +31,10 @@
  *
  * Conventions: every int-returning call returns XS_OK (0) or a negative
  * XS_ERR_* code; xs_last_error() returns a thread-local message for the last
- * failure on the calling thread.  Host buffers are borrowed for the duration of
+ * failure on the calling thread.  No C++ exception leaves the library: a failed
+ * host allocation inside a call is XS_ERR_NOMEM, any other C++ runtime failure
+ * XS_ERR_INTERNAL (NULL from a pointer-returning call; nothing from a void
+ * one).  Host buffers are borrowed for the duration of
  * the call only.  A bank handle owns its device memory and one HIP stream;
  * calls on one handle are serialised by an internal mutex, distinct handles are
  * independent.  The handle's device workspace is shared by all its calls: a
@@ -55,6 +58,8 @@ extern "C" {
 #define XS_ERR_FORMAT (-3)
 #define XS_ERR_HIP (-4)
 #define XS_ERR_UNSUPPORTED (-5)
+#define XS_ERR_NOMEM (-6)    /* a host allocation failed inside the call */
+#define XS_ERR_INTERNAL (-7) /* any other C++ runtime failure (e.g. a thread could not be started) */
 
 #define XS_BANK_COBS_CLASSIC 0
 #define XS_BANK_COBS_COMPACT 1

@@ -139,6 +139,24 @@ def test_u64_member_mask_matches_isin():
         assert np.array_equal(out.astype(bool), np.isin(keys, st))
 
 
+def test_c_abi_turns_a_failed_host_allocation_into_an_error_code():
+    """No C++ exception leaves the library (xs::guard around every entry
+    point): a set of 2^55 keys needs a 2^59-byte hash table, whose allocation
+    fails before the set is read; the call returns XS_ERR_NOMEM with a
+    message instead of ending the process."""
+    import numpy as np
+    from xspect2_amd import _lib
+    keys = np.zeros(1, dtype=np.uint64)
+    one = np.zeros(1, dtype=np.uint64)  # stands in for the set: never read
+    out = np.empty(1, dtype=np.uint8)
+    rc = _lib.load().xs_u64_member_mask(keys.ctypes.data, 1, one.ctypes.data, 1 << 55, out.ctypes.data)
+    assert rc == _lib.XS_ERR_NOMEM
+    assert b"allocation" in _lib.load().xs_last_error()
+    # the library still works afterwards
+    _lib.check(_lib.load().xs_u64_member_mask(keys.ctypes.data, 1, one.ctypes.data, 1, out.ctypes.data))
+    assert out[0] == 1
+
+
 def test_index_finds_the_first_equal_id():
     """PackedIds.index (the sharded totals' search for a read named
     "misclassified") = list.index, also for prefixes, suffixes and repeats."""

@@ -18,6 +18,8 @@ XS_ERR_IO = -2
 XS_ERR_FORMAT = -3
 XS_ERR_HIP = -4
 XS_ERR_UNSUPPORTED = -5
+XS_ERR_NOMEM = -6
+XS_ERR_INTERNAL = -7
 
 XS_BANK_COBS_CLASSIC = 0
 XS_BANK_COBS_COMPACT = 1

@@ -1196,161 +1196,171 @@ int xs_version(void) { return 100; }
 const char* xs_last_error(void) { return g_err.c_str(); }
 
 int xs_device_count(int* count) {
-    if (!count) return fail(XS_ERR_ARG, "null count");
-    int n = 0;
-    hipError_t e = hipGetDeviceCount(&n);
-    if (e != hipSuccess) {
-        *count = 0;
-        return fail(XS_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
-    }
-    *count = n;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!count) return fail(XS_ERR_ARG, "null count");
+        int n = 0;
+        hipError_t e = hipGetDeviceCount(&n);
+        if (e != hipSuccess) {
+            *count = 0;
+            return fail(XS_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+        }
+        *count = n;
+        return XS_OK;
+    });
 }
 
 int xs_bank_open(const char* path, int kind, int device, xs_bank** out) {
-    if (!path || !out) return fail(XS_ERR_ARG, "null argument");
-    *out = nullptr;
-    if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT && kind != XS_BANK_RBLOOM)
-        return fail(XS_ERR_ARG, "unknown bank kind %d", kind);
-    Reader rd;
-    rd.f.open(path, std::ios::binary);
-    if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
-    rd.f.seekg(0, std::ios::end);
-    const uint64_t fsize = (uint64_t)rd.f.tellg();
-    rd.f.seekg(0);
-    xs_bank* b = new_bank(device, kind);
-    int rc = XS_OK;
-    if (kind == XS_BANK_RBLOOM) {
-        b->h = (uint32_t)rd.get<uint64_t>();
-        if (!rd.ok || fsize <= 8) rc = fail(XS_ERR_FORMAT, "%s: truncated rbloom file", path);
-        b->nbytes = fsize - 8;
-        b->D = 1;
-        b->names.push_back("0");
-        b->k = 0;  // set by the caller's model metadata through xs_bank_create_bloom
-    } else {
-        rc = read_cobs_header(b, rd, path);
-    }
-    if (rc == XS_OK && kind == XS_BANK_RBLOOM) {
-        // An rbloom file carries no k (the model JSON does); default to XspecT's
-        // k = 21 (train.py:167-174) until xs_bank_set_term_size overrides it.
-        b->k = 21;
-    }
-    if (rc == XS_OK) rc = validate_geometry(b);
-    if (rc == XS_OK) {
-        const uint64_t pos = (uint64_t)rd.f.tellg();
-        if (fsize - pos != b->payload_bytes())
-            rc = fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
-                      (unsigned long long)(fsize - pos), (unsigned long long)b->payload_bytes());
-    }
-    if (rc == XS_OK) rc = alloc_image(b);
-    if (rc == XS_OK) {
-        std::vector<uint8_t> payload(b->payload_bytes());
-        rd.f.read(reinterpret_cast<char*>(payload.data()), (std::streamsize)payload.size());
-        if (!rd.f) rc = fail(XS_ERR_IO, "%s: short read", path);
-        else rc = upload_payload(b, payload.data(), payload.size());
-    }
-    if (rc != XS_OK) {
-        delete b;
-        return rc;
-    }
-    *out = b;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!path || !out) return fail(XS_ERR_ARG, "null argument");
+        *out = nullptr;
+        if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT && kind != XS_BANK_RBLOOM)
+            return fail(XS_ERR_ARG, "unknown bank kind %d", kind);
+        Reader rd;
+        rd.f.open(path, std::ios::binary);
+        if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
+        rd.f.seekg(0, std::ios::end);
+        const uint64_t fsize = (uint64_t)rd.f.tellg();
+        rd.f.seekg(0);
+        xs_bank* b = new_bank(device, kind);
+        int rc = XS_OK;
+        if (kind == XS_BANK_RBLOOM) {
+            b->h = (uint32_t)rd.get<uint64_t>();
+            if (!rd.ok || fsize <= 8) rc = fail(XS_ERR_FORMAT, "%s: truncated rbloom file", path);
+            b->nbytes = fsize - 8;
+            b->D = 1;
+            b->names.push_back("0");
+            b->k = 0;  // set by the caller's model metadata through xs_bank_create_bloom
+        } else {
+            rc = read_cobs_header(b, rd, path);
+        }
+        if (rc == XS_OK && kind == XS_BANK_RBLOOM) {
+            // An rbloom file carries no k (the model JSON does); default to XspecT's
+            // k = 21 (train.py:167-174) until xs_bank_set_term_size overrides it.
+            b->k = 21;
+        }
+        if (rc == XS_OK) rc = validate_geometry(b);
+        if (rc == XS_OK) {
+            const uint64_t pos = (uint64_t)rd.f.tellg();
+            if (fsize - pos != b->payload_bytes())
+                rc = fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
+                          (unsigned long long)(fsize - pos), (unsigned long long)b->payload_bytes());
+        }
+        if (rc == XS_OK) rc = alloc_image(b);
+        if (rc == XS_OK) {
+            std::vector<uint8_t> payload(b->payload_bytes());
+            rd.f.read(reinterpret_cast<char*>(payload.data()), (std::streamsize)payload.size());
+            if (!rd.f) rc = fail(XS_ERR_IO, "%s: short read", path);
+            else rc = upload_payload(b, payload.data(), payload.size());
+        }
+        if (rc != XS_OK) {
+            delete b;
+            return rc;
+        }
+        *out = b;
+        return XS_OK;
+    });
 }
 
 int xs_bank_open_docs(const char* path, int device, uint64_t doc_lo, uint64_t doc_hi, xs_bank** out) {
-    if (!path || !out) return fail(XS_ERR_ARG, "null argument");
-    *out = nullptr;
-    Reader rd;
-    rd.f.open(path, std::ios::binary);
-    if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
-    rd.f.seekg(0, std::ios::end);
-    const uint64_t fsize = (uint64_t)rd.f.tellg();
-    rd.f.seekg(0);
-    xs_bank* full = new_bank(device, XS_BANK_COBS_CLASSIC);
-    std::unique_ptr<xs_bank> keep_full(full);
-    if (int rc = read_cobs_header(full, rd, path)) return rc;
-    const uint64_t D = full->D, R = full->page, S = full->sig[0];
-    if (doc_lo % 8 || doc_lo >= doc_hi || doc_hi > D || (doc_hi % 8 && doc_hi != D))
-        return fail(XS_ERR_ARG, "doc range [%llu, %llu) of %llu docs: bounds must be multiples of 8 (or the end)",
-                    (unsigned long long)doc_lo, (unsigned long long)doc_hi, (unsigned long long)D);
-    const uint64_t pos = (uint64_t)rd.f.tellg();
-    if (fsize - pos != S * R)
-        return fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
-                    (unsigned long long)(fsize - pos), (unsigned long long)(S * R));
-    xs_bank* b = new_bank(device, XS_BANK_COBS_CLASSIC);
-    std::unique_ptr<xs_bank> keep(b);
-    b->k = full->k;
-    b->h = full->h;
-    b->canonicalize = full->canonicalize;
-    b->D = doc_hi - doc_lo;
-    b->G = 1;
-    b->page = (b->D + 7) / 8;
-    b->sig.assign(1, S);
-    b->names.assign(full->names.begin() + (ptrdiff_t)doc_lo, full->names.begin() + (ptrdiff_t)doc_hi);
-    if (int rc = validate_geometry(b)) return rc;
-    if (int rc = alloc_image(b)) return rc;
-    // the rows' byte columns [doc_lo / 8, + page), read in pieces of rows
-    const uint64_t c0 = doc_lo / 8, P = b->page;
-    std::vector<uint8_t> payload(S * P);
-    constexpr uint64_t kRows = 1u << 20;
-    std::vector<uint8_t> piece(std::min(S, kRows) * R);
-    for (uint64_t r0 = 0; r0 < S; r0 += kRows) {
-        const uint64_t m = std::min(kRows, S - r0);
-        rd.f.read(reinterpret_cast<char*>(piece.data()), (std::streamsize)(m * R));
-        if (!rd.f) return fail(XS_ERR_IO, "%s: short read", path);
-        for (uint64_t r = 0; r < m; ++r) memcpy(payload.data() + (r0 + r) * P, piece.data() + r * R + c0, P);
-    }
-    if (int rc = upload_payload(b, payload.data(), payload.size())) return rc;
-    *out = keep.release();
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!path || !out) return fail(XS_ERR_ARG, "null argument");
+        *out = nullptr;
+        Reader rd;
+        rd.f.open(path, std::ios::binary);
+        if (!rd.f) return fail(XS_ERR_IO, "cannot open %s", path);
+        rd.f.seekg(0, std::ios::end);
+        const uint64_t fsize = (uint64_t)rd.f.tellg();
+        rd.f.seekg(0);
+        xs_bank* full = new_bank(device, XS_BANK_COBS_CLASSIC);
+        std::unique_ptr<xs_bank> keep_full(full);
+        if (int rc = read_cobs_header(full, rd, path)) return rc;
+        const uint64_t D = full->D, R = full->page, S = full->sig[0];
+        if (doc_lo % 8 || doc_lo >= doc_hi || doc_hi > D || (doc_hi % 8 && doc_hi != D))
+            return fail(XS_ERR_ARG, "doc range [%llu, %llu) of %llu docs: bounds must be multiples of 8 (or the end)",
+                        (unsigned long long)doc_lo, (unsigned long long)doc_hi, (unsigned long long)D);
+        const uint64_t pos = (uint64_t)rd.f.tellg();
+        if (fsize - pos != S * R)
+            return fail(XS_ERR_FORMAT, "%s: payload is %llu bytes, header implies %llu", path,
+                        (unsigned long long)(fsize - pos), (unsigned long long)(S * R));
+        xs_bank* b = new_bank(device, XS_BANK_COBS_CLASSIC);
+        std::unique_ptr<xs_bank> keep(b);
+        b->k = full->k;
+        b->h = full->h;
+        b->canonicalize = full->canonicalize;
+        b->D = doc_hi - doc_lo;
+        b->G = 1;
+        b->page = (b->D + 7) / 8;
+        b->sig.assign(1, S);
+        b->names.assign(full->names.begin() + (ptrdiff_t)doc_lo, full->names.begin() + (ptrdiff_t)doc_hi);
+        if (int rc = validate_geometry(b)) return rc;
+        if (int rc = alloc_image(b)) return rc;
+        // the rows' byte columns [doc_lo / 8, + page), read in pieces of rows
+        const uint64_t c0 = doc_lo / 8, P = b->page;
+        std::vector<uint8_t> payload(S * P);
+        constexpr uint64_t kRows = 1u << 20;
+        std::vector<uint8_t> piece(std::min(S, kRows) * R);
+        for (uint64_t r0 = 0; r0 < S; r0 += kRows) {
+            const uint64_t m = std::min(kRows, S - r0);
+            rd.f.read(reinterpret_cast<char*>(piece.data()), (std::streamsize)(m * R));
+            if (!rd.f) return fail(XS_ERR_IO, "%s: short read", path);
+            for (uint64_t r = 0; r < m; ++r) memcpy(payload.data() + (r0 + r) * P, piece.data() + r * R + c0, P);
+        }
+        if (int rc = upload_payload(b, payload.data(), payload.size())) return rc;
+        *out = keep.release();
+        return XS_OK;
+    });
 }
 
 int xs_bank_create_cobs(int device, int kind, uint32_t term_size, uint32_t num_hashes,
                         uint64_t num_docs, uint64_t page_size, uint64_t num_groups,
                         const uint64_t* sig, const char* const* doc_names, xs_bank** out) {
-    if (!out || !sig) return fail(XS_ERR_ARG, "null argument");
-    *out = nullptr;
-    if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT)
-        return fail(XS_ERR_ARG, "kind must be a COBS kind");
-    if (kind == XS_BANK_COBS_CLASSIC && (num_groups != 1 || page_size != (num_docs + 7) / 8))
-        return fail(XS_ERR_ARG, "classic banks have one group of ceil(D/8) bytes");
-    xs_bank* b = new_bank(device, kind);
-    b->k = term_size;
-    b->h = num_hashes;
-    b->D = num_docs;
-    b->G = num_groups;
-    b->page = page_size;
-    b->sig.assign(sig, sig + num_groups);
-    for (uint64_t i = 0; i < num_docs; ++i)
-        b->names.push_back(doc_names ? std::string(doc_names[i]) : std::to_string(i));
-    int rc = validate_geometry(b);
-    if (rc == XS_OK) rc = alloc_image(b);
-    if (rc != XS_OK) {
-        delete b;
-        return rc;
-    }
-    *out = b;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!out || !sig) return fail(XS_ERR_ARG, "null argument");
+        *out = nullptr;
+        if (kind != XS_BANK_COBS_CLASSIC && kind != XS_BANK_COBS_COMPACT)
+            return fail(XS_ERR_ARG, "kind must be a COBS kind");
+        if (kind == XS_BANK_COBS_CLASSIC && (num_groups != 1 || page_size != (num_docs + 7) / 8))
+            return fail(XS_ERR_ARG, "classic banks have one group of ceil(D/8) bytes");
+        xs_bank* b = new_bank(device, kind);
+        b->k = term_size;
+        b->h = num_hashes;
+        b->D = num_docs;
+        b->G = num_groups;
+        b->page = page_size;
+        b->sig.assign(sig, sig + num_groups);
+        for (uint64_t i = 0; i < num_docs; ++i)
+            b->names.push_back(doc_names ? std::string(doc_names[i]) : std::to_string(i));
+        int rc = validate_geometry(b);
+        if (rc == XS_OK) rc = alloc_image(b);
+        if (rc != XS_OK) {
+            delete b;
+            return rc;
+        }
+        *out = b;
+        return XS_OK;
+    });
 }
 
 int xs_bank_create_bloom(int device, uint32_t term_size, uint64_t nbytes, uint32_t nhash,
                          xs_bank** out) {
-    if (!out) return fail(XS_ERR_ARG, "null argument");
-    *out = nullptr;
-    xs_bank* b = new_bank(device, XS_BANK_RBLOOM);
-    b->k = term_size;
-    b->h = nhash;
-    b->nbytes = nbytes;
-    b->D = 1;
-    b->names.push_back("0");
-    int rc = validate_geometry(b);
-    if (rc == XS_OK) rc = alloc_image(b);
-    if (rc != XS_OK) {
-        delete b;
-        return rc;
-    }
-    *out = b;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!out) return fail(XS_ERR_ARG, "null argument");
+        *out = nullptr;
+        xs_bank* b = new_bank(device, XS_BANK_RBLOOM);
+        b->k = term_size;
+        b->h = nhash;
+        b->nbytes = nbytes;
+        b->D = 1;
+        b->names.push_back("0");
+        int rc = validate_geometry(b);
+        if (rc == XS_OK) rc = alloc_image(b);
+        if (rc != XS_OK) {
+            delete b;
+            return rc;
+        }
+        *out = b;
+        return XS_OK;
+    });
 }
 
 static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipStream_t s) {
@@ -1367,106 +1377,124 @@ static int build_impl(xs_bank* b, const Inputs& in, const uint32_t* d_doc, hipSt
 
 int xs_bank_build(xs_bank* b, const char* seqs, const uint64_t* offsets, const uint32_t* rec_doc,
                   uint64_t n_rec) {
-    if (!b || (!seqs && n_rec) || !offsets) return fail(XS_ERR_ARG, "null argument");
-    if (b->kind != XS_BANK_RBLOOM && n_rec && !rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    if (n_rec == 0) return XS_OK;
-    if (b->kind != XS_BANK_RBLOOM)
-        for (uint64_t r = 0; r < n_rec; ++r)
-            if (rec_doc[r] >= b->D) return fail(XS_ERR_ARG, "rec_doc[%llu] out of range", (unsigned long long)r);
-    Inputs in;
-    if (int rc = stage_host_reads(b, seqs, offsets, n_rec, &in)) return rc;
-    uint32_t* d_doc = nullptr;
-    if (b->kind != XS_BANK_RBLOOM) {
-        if (int rc = b->tmp.ensure(n_rec * 4)) return rc;
-        d_doc = b->tmp.as<uint32_t>();
-        HIPCHK(hipMemcpyAsync(d_doc, rec_doc, n_rec * 4, hipMemcpyHostToDevice, b->stream));
-    }
-    if (int rc = build_impl(b, in, d_doc, b->stream)) return rc;
-    HIPCHK(hipStreamSynchronize(b->stream));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || (!seqs && n_rec) || !offsets) return fail(XS_ERR_ARG, "null argument");
+        if (b->kind != XS_BANK_RBLOOM && n_rec && !rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        if (n_rec == 0) return XS_OK;
+        if (b->kind != XS_BANK_RBLOOM)
+            for (uint64_t r = 0; r < n_rec; ++r)
+                if (rec_doc[r] >= b->D) return fail(XS_ERR_ARG, "rec_doc[%llu] out of range", (unsigned long long)r);
+        Inputs in;
+        if (int rc = stage_host_reads(b, seqs, offsets, n_rec, &in)) return rc;
+        uint32_t* d_doc = nullptr;
+        if (b->kind != XS_BANK_RBLOOM) {
+            if (int rc = b->tmp.ensure(n_rec * 4)) return rc;
+            d_doc = b->tmp.as<uint32_t>();
+            HIPCHK(hipMemcpyAsync(d_doc, rec_doc, n_rec * 4, hipMemcpyHostToDevice, b->stream));
+        }
+        if (int rc = build_impl(b, in, d_doc, b->stream)) return rc;
+        HIPCHK(hipStreamSynchronize(b->stream));
+        return XS_OK;
+    });
 }
 
 int xs_bank_build_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes,
                          const uint64_t* d_offsets, const uint32_t* d_rec_doc, uint64_t n_rec,
                          void* stream) {
-    if (!b || !d_offsets) return fail(XS_ERR_ARG, "null argument");
-    if (b->kind != XS_BANK_RBLOOM && n_rec && !d_rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    if (n_rec == 0) return XS_OK;
-    Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n_rec};
-    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
-    return build_impl(b, in, d_rec_doc, s);
+    return xs::guard([&]() -> int {
+        if (!b || !d_offsets) return fail(XS_ERR_ARG, "null argument");
+        if (b->kind != XS_BANK_RBLOOM && n_rec && !d_rec_doc) return fail(XS_ERR_ARG, "rec_doc required");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        if (n_rec == 0) return XS_OK;
+        Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n_rec};
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
+        return build_impl(b, in, d_rec_doc, s);
+    });
 }
 
 int xs_bank_save(xs_bank* b, const char* path) {
-    if (!b || !path) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    HIPCHK(hipDeviceSynchronize());
-    return b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, path) : write_cobs_file(b, path);
+    return xs::guard([&]() -> int {
+        if (!b || !path) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        HIPCHK(hipDeviceSynchronize());
+        return b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, path) : write_cobs_file(b, path);
+    });
 }
 
 int xs_bank_download(xs_bank* b, void* host, uint64_t nbytes) {
-    if (!b || !host) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    HIPCHK(hipDeviceSynchronize());
-    return download_payload(b, host, nbytes);
+    return xs::guard([&]() -> int {
+        if (!b || !host) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        HIPCHK(hipDeviceSynchronize());
+        return download_payload(b, host, nbytes);
+    });
 }
 
 int xs_bank_upload(xs_bank* b, const void* host, uint64_t nbytes) {
-    if (!b || !host) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    return upload_payload(b, host, nbytes);
+    return xs::guard([&]() -> int {
+        if (!b || !host) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        return upload_payload(b, host, nbytes);
+    });
 }
 
 int xs_bank_set_term_size(xs_bank* b, uint32_t term_size) {
-    if (!b) return fail(XS_ERR_ARG, "null argument");
-    if (b->kind != XS_BANK_RBLOOM)
-        return fail(XS_ERR_ARG, "COBS banks carry their term size in the file header");
-    if (term_size < 1 || term_size > kMaxK)
-        return fail(XS_ERR_UNSUPPORTED, "term_size %u unsupported on the device (1..%u)", term_size, kMaxK);
-    std::lock_guard<std::mutex> lk(b->mu);
-    b->k = term_size;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b) return fail(XS_ERR_ARG, "null argument");
+        if (b->kind != XS_BANK_RBLOOM)
+            return fail(XS_ERR_ARG, "COBS banks carry their term size in the file header");
+        if (term_size < 1 || term_size > kMaxK)
+            return fail(XS_ERR_UNSUPPORTED, "term_size %u unsupported on the device (1..%u)", term_size, kMaxK);
+        std::lock_guard<std::mutex> lk(b->mu);
+        b->k = term_size;
+        return XS_OK;
+    });
 }
 
 int xs_bank_info(const xs_bank* b, xs_bank_info_t* o) {
-    if (!b || !o) return fail(XS_ERR_ARG, "null argument");
-    memset(o, 0, sizeof(*o));
-    o->kind = b->kind;
-    o->device = b->device;
-    o->term_size = b->k;
-    o->num_hashes = b->h;
-    o->canonicalize = b->canonicalize;
-    o->num_docs = b->D;
-    o->num_groups = b->kind == XS_BANK_RBLOOM ? 0 : b->G;
-    o->page_size = b->page;
-    o->signature_rows = b->sig_total();
-    o->bloom_bits = b->kind == XS_BANK_RBLOOM ? b->nbytes * 8 : 0;
-    o->device_bytes = b->dev_bytes;
-    o->device_row_pitch = b->pitch;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !o) return fail(XS_ERR_ARG, "null argument");
+        memset(o, 0, sizeof(*o));
+        o->kind = b->kind;
+        o->device = b->device;
+        o->term_size = b->k;
+        o->num_hashes = b->h;
+        o->canonicalize = b->canonicalize;
+        o->num_docs = b->D;
+        o->num_groups = b->kind == XS_BANK_RBLOOM ? 0 : b->G;
+        o->page_size = b->page;
+        o->signature_rows = b->sig_total();
+        o->bloom_bits = b->kind == XS_BANK_RBLOOM ? b->nbytes * 8 : 0;
+        o->device_bytes = b->dev_bytes;
+        o->device_row_pitch = b->pitch;
+        return XS_OK;
+    });
 }
 
 int xs_bank_signature_sizes(const xs_bank* b, uint64_t* out, uint64_t n) {
-    if (!b || !out) return fail(XS_ERR_ARG, "null argument");
-    if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "rbloom banks have no signature groups");
-    if (n != b->sig.size()) return fail(XS_ERR_ARG, "bank has %zu groups, %llu requested", b->sig.size(),
-                                        (unsigned long long)n);
-    for (uint64_t g = 0; g < n; ++g) out[g] = b->sig[g];
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !out) return fail(XS_ERR_ARG, "null argument");
+        if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "rbloom banks have no signature groups");
+        if (n != b->sig.size()) return fail(XS_ERR_ARG, "bank has %zu groups, %llu requested", b->sig.size(),
+                                            (unsigned long long)n);
+        for (uint64_t g = 0; g < n; ++g) out[g] = b->sig[g];
+        return XS_OK;
+    });
 }
 
 const char* xs_bank_doc_name(const xs_bank* b, uint64_t i) {
-    if (!b || i >= b->names.size()) {
-        fail(XS_ERR_ARG, "doc index out of range");
-        return nullptr;
-    }
-    return b->names[i].c_str();
+    return xs::guard([&]() -> const char* {
+        if (!b || i >= b->names.size()) {
+            fail(XS_ERR_ARG, "doc index out of range");
+            return nullptr;
+        }
+        return b->names[i].c_str();
+    });
 }
 
 static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
@@ -1515,378 +1543,420 @@ static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uin
 
 int xs_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
              uint32_t* hits_out, uint64_t* num_kmers_out) {
-    return query_impl(b, seqs, offsets, n, step, hits_out, 4, num_kmers_out);
+    return xs::guard([&]() -> int {
+        return query_impl(b, seqs, offsets, n, step, hits_out, 4, num_kmers_out);
+    });
 }
 
 int xs_query_hits(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                   void* hits_out, int hit_bytes, uint64_t* num_kmers_out) {
-    return query_impl(b, seqs, offsets, n, step, hits_out, hit_bytes, num_kmers_out);
+    return xs::guard([&]() -> int {
+        return query_impl(b, seqs, offsets, n, step, hits_out, hit_bytes, num_kmers_out);
+    });
 }
 
 int xs_query_hits_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, const uint64_t* d_offsets, uint64_t n,
                          uint64_t max_len, uint32_t step, void* hits_out, int hit_bytes, uint64_t* num_kmers_out,
                          uint64_t* totals_out) {
-    if (!b || (n && (!d_seqs || !d_offsets))) return fail(XS_ERR_ARG, "null argument");
-    if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
-    if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
-    const uint64_t max_nk = max_len >= b->k ? (max_len - b->k) / step + 1 : 0;
-    if (hits_out && hit_bytes != 4) {
-        const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
-        if (max_nk > cap)
-            return fail(XS_ERR_ARG, "a read has %llu sampled k-mers: counts may not fit %d byte(s)",
-                        (unsigned long long)max_nk, hit_bytes);
-    }
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
-    if (n == 0) {
-        if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
+    return xs::guard([&]() -> int {
+        if (!b || (n && (!d_seqs || !d_offsets))) return fail(XS_ERR_ARG, "null argument");
+        if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return fail(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
+        if (step == 0) return fail(XS_ERR_ARG, "step must be >= 1");
+        const uint64_t max_nk = max_len >= b->k ? (max_len - b->k) / step + 1 : 0;
+        if (hits_out && hit_bytes != 4) {
+            const uint64_t cap = hit_bytes == 1 ? 0xFFu : 0xFFFFu;
+            if (max_nk > cap)
+                return fail(XS_ERR_ARG, "a read has %llu sampled k-mers: counts may not fit %d byte(s)",
+                            (unsigned long long)max_nk, hit_bytes);
+        }
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+        if (n == 0) {
+            if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
+            return XS_OK;
+        }
+        uint32_t* d_hits = nullptr;
+        if (hits_out) {
+            if (int rc = b->hits.ensure(n * cols * 4)) return rc;
+            d_hits = b->hits.as<uint32_t>();
+        }
+        if (num_kmers_out)
+            if (int rc = b->nk.ensure(n * 8)) return rc;
+        std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
+        const DevReads dev{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets};
+        if (int rc = query_host(b, nullptr, nullptr, n, step, d_hits, hits_out, num_kmers_out ? b->nk.as<uint64_t>() : nullptr,
+                                totals_out ? tot.data() : nullptr, hit_bytes, &dev))
+            return rc;
+        if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
         return XS_OK;
-    }
-    uint32_t* d_hits = nullptr;
-    if (hits_out) {
-        if (int rc = b->hits.ensure(n * cols * 4)) return rc;
-        d_hits = b->hits.as<uint32_t>();
-    }
-    if (num_kmers_out)
-        if (int rc = b->nk.ensure(n * 8)) return rc;
-    std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
-    const DevReads dev{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets};
-    if (int rc = query_host(b, nullptr, nullptr, n, step, d_hits, hits_out, num_kmers_out ? b->nk.as<uint64_t>() : nullptr,
-                            totals_out ? tot.data() : nullptr, hit_bytes, &dev))
-        return rc;
-    if (num_kmers_out) HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
-    HIPCHK(hipStreamSynchronize(b->stream));
-    if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
-    return XS_OK;
+    });
 }
 
 int xs_memcpy_to_host(void* host, const void* dev, uint64_t bytes) {
-    if (bytes && (!host || !dev)) return fail(XS_ERR_ARG, "null argument");
-    if (bytes) HIPCHK(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (bytes && (!host || !dev)) return fail(XS_ERR_ARG, "null argument");
+        if (bytes) HIPCHK(hipMemcpy(host, dev, bytes, hipMemcpyDeviceToHost));
+        return XS_OK;
+    });
 }
 
 int xs_memcpy_device(void* dst, const void* src, uint64_t bytes, void* stream) {
-    if (bytes && (!dst || !src)) return fail(XS_ERR_ARG, "null argument");
-    if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (bytes && (!dst || !src)) return fail(XS_ERR_ARG, "null argument");
+        if (bytes) HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, static_cast<hipStream_t>(stream)));
+        return XS_OK;
+    });
 }
 
 int xs_host_alloc(uint64_t bytes, void** out) {
-    if (!out) return fail(XS_ERR_ARG, "null argument");
-    *out = nullptr;
-    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
-    if (e != hipSuccess) {
+    return xs::guard([&]() -> int {
+        if (!out) return fail(XS_ERR_ARG, "null argument");
         *out = nullptr;
-        return fail(XS_ERR_HIP, "hipHostMalloc(%llu) failed: %s", (unsigned long long)bytes, hipGetErrorString(e));
-    }
-    return XS_OK;
+        hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            *out = nullptr;
+            return fail(XS_ERR_HIP, "hipHostMalloc(%llu) failed: %s", (unsigned long long)bytes, hipGetErrorString(e));
+        }
+        return XS_OK;
+    });
 }
 
 void xs_host_free(void* p) {
-    if (p) (void)hipHostFree(p);
+    xs::guard([&] {
+        if (p) (void)hipHostFree(p);
+    });
 }
 
 int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                   uint32_t* best_doc, uint32_t* best_hits, uint64_t* num_kmers_out, uint64_t* totals_out) {
-    if (!b || !offsets || ((!seqs || !best_doc) && n)) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
-    if (n == 0) {
-        if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
-        return XS_OK;
-    }
-    if (n <= kSmallReads && n * cols <= (1u << 16)) {  // a small request: the per-read call made on the host
-        std::vector<uint32_t> rows(n * cols);
-        std::vector<uint64_t> tot(cols + 1);
-        bool done = false;
-        if (int rc = query_small(b, seqs, offsets, n, step, rows.data(), 4, num_kmers_out, tot.data(), &done)) return rc;
-        if (done) {
-            for (uint64_t r = 0; r < n; ++r) {  // best_doc_kernel's rule: a unique maximum, else ambiguous
-                const uint32_t* row = rows.data() + r * cols;
-                uint32_t m = 0, arg = 0, cnt = 0;
-                for (uint64_t c = 0; c < cols; ++c) {
-                    if (cnt == 0 || row[c] > m) {
-                        m = row[c];
-                        arg = (uint32_t)c;
-                        cnt = 1;
-                    } else if (row[c] == m) {
-                        ++cnt;
-                    }
-                }
-                best_doc[r] = cnt == 1 ? arg : kBestAmbiguous;
-                if (best_hits) best_hits[r] = m;
-            }
-            if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
+    return xs::guard([&]() -> int {
+        if (!b || !offsets || ((!seqs || !best_doc) && n)) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+        if (n == 0) {
+            if (totals_out) memset(totals_out, 0, (cols + 1) * 8);
             return XS_OK;
         }
-    }
-    if (int rc = b->hits.ensure(n * cols * 4)) return rc;
-    if (int rc = b->nk.ensure(n * 8)) return rc;
-    if (int rc = b->best.ensure(n * 8)) return rc;
-    uint32_t* d_hits = b->hits.as<uint32_t>();
-    uint32_t* d_best = b->best.as<uint32_t>();
-    uint32_t* d_bhits = d_best + n;
-    std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
-    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, b->nk.as<uint64_t>(),
-                            totals_out ? tot.data() : nullptr))
-        return rc;
-    HIPCHK(launch_best_doc(d_hits, n, cols, d_best, d_bhits, b->stream));
-    HIPCHK(hipMemcpyAsync(best_doc, d_best, n * 4, hipMemcpyDeviceToHost, b->stream));
-    if (best_hits) HIPCHK(hipMemcpyAsync(best_hits, d_bhits, n * 4, hipMemcpyDeviceToHost, b->stream));
-    if (num_kmers_out)
-        HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
-    HIPCHK(hipStreamSynchronize(b->stream));
-    if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
-    return XS_OK;
+        if (n <= kSmallReads && n * cols <= (1u << 16)) {  // a small request: the per-read call made on the host
+            std::vector<uint32_t> rows(n * cols);
+            std::vector<uint64_t> tot(cols + 1);
+            bool done = false;
+            if (int rc = query_small(b, seqs, offsets, n, step, rows.data(), 4, num_kmers_out, tot.data(), &done)) return rc;
+            if (done) {
+                for (uint64_t r = 0; r < n; ++r) {  // best_doc_kernel's rule: a unique maximum, else ambiguous
+                    const uint32_t* row = rows.data() + r * cols;
+                    uint32_t m = 0, arg = 0, cnt = 0;
+                    for (uint64_t c = 0; c < cols; ++c) {
+                        if (cnt == 0 || row[c] > m) {
+                            m = row[c];
+                            arg = (uint32_t)c;
+                            cnt = 1;
+                        } else if (row[c] == m) {
+                            ++cnt;
+                        }
+                    }
+                    best_doc[r] = cnt == 1 ? arg : kBestAmbiguous;
+                    if (best_hits) best_hits[r] = m;
+                }
+                if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
+                return XS_OK;
+            }
+        }
+        if (int rc = b->hits.ensure(n * cols * 4)) return rc;
+        if (int rc = b->nk.ensure(n * 8)) return rc;
+        if (int rc = b->best.ensure(n * 8)) return rc;
+        uint32_t* d_hits = b->hits.as<uint32_t>();
+        uint32_t* d_best = b->best.as<uint32_t>();
+        uint32_t* d_bhits = d_best + n;
+        std::vector<uint64_t> tot(totals_out ? cols + 1 : 0);
+        if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, b->nk.as<uint64_t>(),
+                                totals_out ? tot.data() : nullptr))
+            return rc;
+        HIPCHK(launch_best_doc(d_hits, n, cols, d_best, d_bhits, b->stream));
+        HIPCHK(hipMemcpyAsync(best_doc, d_best, n * 4, hipMemcpyDeviceToHost, b->stream));
+        if (best_hits) HIPCHK(hipMemcpyAsync(best_hits, d_bhits, n * 4, hipMemcpyDeviceToHost, b->stream));
+        if (num_kmers_out)
+            HIPCHK(hipMemcpyAsync(num_kmers_out, b->nk.p, n * 8, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        if (totals_out) memcpy(totals_out, tot.data(), (cols + 1) * 8);
+        return XS_OK;
+    });
 }
 
 int xs_gather_reads_device(const void* d_seqs, const uint64_t* d_offsets, const uint32_t* d_index, uint64_t m,
                            void* d_out_seqs, const uint64_t* d_out_offsets, void* stream) {
-    if (m && (!d_seqs || !d_offsets || !d_index || !d_out_seqs || !d_out_offsets))
-        return fail(XS_ERR_ARG, "null argument");
-    HIPCHK(launch_gather_reads(static_cast<const uint8_t*>(d_seqs), d_offsets, d_index, m,
-                               static_cast<uint8_t*>(d_out_seqs), d_out_offsets, static_cast<hipStream_t>(stream)));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (m && (!d_seqs || !d_offsets || !d_index || !d_out_seqs || !d_out_offsets))
+            return fail(XS_ERR_ARG, "null argument");
+        HIPCHK(launch_gather_reads(static_cast<const uint8_t*>(d_seqs), d_offsets, d_index, m,
+                                   static_cast<uint8_t*>(d_out_seqs), d_out_offsets, static_cast<hipStream_t>(stream)));
+        return XS_OK;
+    });
 }
 
 int xs_best_device(const uint32_t* d_hits, uint64_t n, uint64_t num_docs, uint32_t* d_best_doc,
                    uint32_t* d_best_hits, void* stream) {
-    if ((!d_hits || !d_best_doc) && n) return fail(XS_ERR_ARG, "null argument");
-    if (num_docs == 0) return fail(XS_ERR_ARG, "num_docs must be >= 1");
-    HIPCHK(launch_best_doc(d_hits, n, num_docs, d_best_doc, d_best_hits, static_cast<hipStream_t>(stream)));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if ((!d_hits || !d_best_doc) && n) return fail(XS_ERR_ARG, "null argument");
+        if (num_docs == 0) return fail(XS_ERR_ARG, "num_docs must be >= 1");
+        HIPCHK(launch_best_doc(d_hits, n, num_docs, d_best_doc, d_best_hits, static_cast<hipStream_t>(stream)));
+        return XS_OK;
+    });
 }
 
 int xs_query_totals(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n,
                     uint32_t step, uint64_t* totals_out, uint64_t* total_kmers_out) {
-    if (!b || !offsets || (!seqs && n) || !totals_out) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
-    if (n == 0) {
-        memset(totals_out, 0, cols * 8);
-        if (total_kmers_out) *total_kmers_out = 0;
+    return xs::guard([&]() -> int {
+        if (!b || !offsets || (!seqs && n) || !totals_out) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
+        if (n == 0) {
+            memset(totals_out, 0, cols * 8);
+            if (total_kmers_out) *total_kmers_out = 0;
+            return XS_OK;
+        }
+        std::vector<uint64_t> t(cols + 1);
+        bool done = false;
+        if (int rc = query_small(b, seqs, offsets, n, step, nullptr, 4, nullptr, t.data(), &done)) return rc;
+        if (!done)
+            if (int rc = query_host(b, seqs, offsets, n, step, nullptr, nullptr, nullptr, t.data())) return rc;
+        memcpy(totals_out, t.data(), cols * 8);
+        if (total_kmers_out) *total_kmers_out = t[cols];
         return XS_OK;
-    }
-    std::vector<uint64_t> t(cols + 1);
-    bool done = false;
-    if (int rc = query_small(b, seqs, offsets, n, step, nullptr, 4, nullptr, t.data(), &done)) return rc;
-    if (!done)
-        if (int rc = query_host(b, seqs, offsets, n, step, nullptr, nullptr, nullptr, t.data())) return rc;
-    memcpy(totals_out, t.data(), cols * 8);
-    if (total_kmers_out) *total_kmers_out = t[cols];
-    return XS_OK;
+    });
 }
 
 int xs_query_device(xs_bank* b, const void* d_seqs, uint64_t seq_bytes, const uint64_t* d_offsets,
                     uint64_t n, uint32_t step, uint32_t* d_hits, uint64_t* d_num_kmers,
                     uint64_t* d_totals, void* stream) {
-    if (!b || !d_offsets || (!d_seqs && n)) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
-    if (n == 0) {
-        if (d_totals) {
-            const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
-            HIPCHK(hipMemsetAsync(d_totals, 0, cols * 8, s));
+    return xs::guard([&]() -> int {
+        if (!b || !d_offsets || (!d_seqs && n)) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        hipStream_t s = static_cast<hipStream_t>(stream);  // NULL = the null (legacy default) stream
+        if (n == 0) {
+            if (d_totals) {
+                const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 2 : b->D + 1;
+                HIPCHK(hipMemsetAsync(d_totals, 0, cols * 8, s));
+            }
+            return XS_OK;
         }
-        return XS_OK;
-    }
-    Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n};
-    return run_query(b, in, step, d_hits, d_num_kmers, d_totals, s);
+        Inputs in{static_cast<const uint8_t*>(d_seqs), seq_bytes, d_offsets, n};
+        return run_query(b, in, step, d_hits, d_num_kmers, d_totals, s);
+    });
 }
 
 int xs_mlst_sum(xs_bank* b, const uint32_t* hits, const uint32_t* seq_of_chunk, uint64_t n_chunks,
                 uint64_t n_seqs, uint32_t threshold, uint64_t* scores) {
-    if (!b || (!hits && n_chunks) || (!seq_of_chunk && n_chunks) || !scores)
-        return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    const uint64_t D = b->D;
-    for (uint64_t c = 0; c < n_chunks; ++c)
-        if (seq_of_chunk[c] >= n_seqs) return fail(XS_ERR_ARG, "seq_of_chunk[%llu] out of range", (unsigned long long)c);
-    if (n_seqs == 0) return XS_OK;
-    if (int rc = ws_enter(b, b->stream)) return rc;
-    if (int rc = b->hits.ensure(n_chunks * D * 4 + 4)) return rc;
-    if (int rc = b->tmp.ensure(n_chunks * 4 + 4)) return rc;
-    if (int rc = b->totals.ensure(n_seqs * D * 8)) return rc;
-    if (n_chunks) {
-        HIPCHK(hipMemcpyAsync(b->hits.p, hits, n_chunks * D * 4, hipMemcpyHostToDevice, b->stream));
-        HIPCHK(hipMemcpyAsync(b->tmp.p, seq_of_chunk, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
-    }
-    HIPCHK(hipMemsetAsync(b->totals.p, 0, n_seqs * D * 8, b->stream));
-    HIPCHK(launch_mlst_sum(b->hits.as<uint32_t>(), b->tmp.as<uint32_t>(), n_chunks, D, threshold,
-                           b->totals.as<unsigned long long>(), nullptr, nullptr, b->stream));
-    HIPCHK(hipMemcpyAsync(scores, b->totals.p, n_seqs * D * 8, hipMemcpyDeviceToHost, b->stream));
-    HIPCHK(hipStreamSynchronize(b->stream));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || (!hits && n_chunks) || (!seq_of_chunk && n_chunks) || !scores)
+            return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        const uint64_t D = b->D;
+        for (uint64_t c = 0; c < n_chunks; ++c)
+            if (seq_of_chunk[c] >= n_seqs) return fail(XS_ERR_ARG, "seq_of_chunk[%llu] out of range", (unsigned long long)c);
+        if (n_seqs == 0) return XS_OK;
+        if (int rc = ws_enter(b, b->stream)) return rc;
+        if (int rc = b->hits.ensure(n_chunks * D * 4 + 4)) return rc;
+        if (int rc = b->tmp.ensure(n_chunks * 4 + 4)) return rc;
+        if (int rc = b->totals.ensure(n_seqs * D * 8)) return rc;
+        if (n_chunks) {
+            HIPCHK(hipMemcpyAsync(b->hits.p, hits, n_chunks * D * 4, hipMemcpyHostToDevice, b->stream));
+            HIPCHK(hipMemcpyAsync(b->tmp.p, seq_of_chunk, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
+        }
+        HIPCHK(hipMemsetAsync(b->totals.p, 0, n_seqs * D * 8, b->stream));
+        HIPCHK(launch_mlst_sum(b->hits.as<uint32_t>(), b->tmp.as<uint32_t>(), n_chunks, D, threshold,
+                               b->totals.as<unsigned long long>(), nullptr, nullptr, b->stream));
+        HIPCHK(hipMemcpyAsync(scores, b->totals.p, n_seqs * D * 8, hipMemcpyDeviceToHost, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        return XS_OK;
+    });
 }
 
 int xs_mlst_query(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n_direct, uint64_t n_chunks,
                   const uint32_t* chunk_owner, uint64_t n_owners, uint32_t step, uint32_t threshold,
                   uint32_t* direct_hits, uint64_t* owner_scores, uint32_t* owner_first,
                   uint32_t* owner_first_score) {
-    const uint64_t n = n_direct + n_chunks;
-    if (!b || !offsets || (!seqs && n) || (n_chunks && !chunk_owner)) return fail(XS_ERR_ARG, "null argument");
-    if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "MLST queries need a COBS bank");
-    if (owner_first_score && !owner_first) return fail(XS_ERR_ARG, "owner_first_score needs owner_first");
-    for (uint64_t c = 0; c < n_chunks; ++c)
-        if (chunk_owner[c] >= n_owners || (c && chunk_owner[c] < chunk_owner[c - 1]))
-            return fail(XS_ERR_ARG, "chunk_owner must be non-decreasing and < n_owners (chunk %llu)",
-                        (unsigned long long)c);
-    if (n_chunks >= (1ull << 32) - 1) return fail(XS_ERR_ARG, "at most 2^32-2 chunks per call");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    const uint64_t D = b->D, od = n_owners * D;
-    if (n_owners) {
-        if (owner_scores) memset(owner_scores, 0, od * 8);
-        if (owner_first) memset(owner_first, 0xFF, od * 4);
-        if (owner_first_score) memset(owner_first_score, 0, od * 4);
-    }
-    if (n == 0) return XS_OK;
-    if (int rc = ws_enter(b, b->stream)) return rc;
-    if (int rc = b->hits.ensure(n * D * 4)) return rc;
-    uint32_t* d_hits = b->hits.as<uint32_t>();
-    // every record probed in one pass; only the direct rows cross to the host
-    if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, nullptr, nullptr)) return rc;
-    if (n_direct && direct_hits)
-        if (int rc = d2h_pageable(b, direct_hits, d_hits, n_direct * D * 4, b->stream)) return rc;
-    if (n_chunks && n_owners) {
+    return xs::guard([&]() -> int {
+        const uint64_t n = n_direct + n_chunks;
+        if (!b || !offsets || (!seqs && n) || (n_chunks && !chunk_owner)) return fail(XS_ERR_ARG, "null argument");
+        if (b->kind == XS_BANK_RBLOOM) return fail(XS_ERR_ARG, "MLST queries need a COBS bank");
+        if (owner_first_score && !owner_first) return fail(XS_ERR_ARG, "owner_first_score needs owner_first");
+        for (uint64_t c = 0; c < n_chunks; ++c)
+            if (chunk_owner[c] >= n_owners || (c && chunk_owner[c] < chunk_owner[c - 1]))
+                return fail(XS_ERR_ARG, "chunk_owner must be non-decreasing and < n_owners (chunk %llu)",
+                            (unsigned long long)c);
+        if (n_chunks >= (1ull << 32) - 1) return fail(XS_ERR_ARG, "at most 2^32-2 chunks per call");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        const uint64_t D = b->D, od = n_owners * D;
+        if (n_owners) {
+            if (owner_scores) memset(owner_scores, 0, od * 8);
+            if (owner_first) memset(owner_first, 0xFF, od * 4);
+            if (owner_first_score) memset(owner_first_score, 0, od * 4);
+        }
+        if (n == 0) return XS_OK;
         if (int rc = ws_enter(b, b->stream)) return rc;
-        if (int rc = b->tmp.ensure(n_chunks * 4)) return rc;
-        if (int rc = b->totals.ensure(od * 8)) return rc;
-        if (int rc = b->best.ensure(od * 8)) return rc;
-        uint32_t* d_first = b->best.as<uint32_t>();
-        uint32_t* d_fscore = d_first + od;
-        HIPCHK(hipMemcpyAsync(b->tmp.p, chunk_owner, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
-        HIPCHK(hipMemsetAsync(b->totals.p, 0, od * 8, b->stream));
-        HIPCHK(hipMemsetAsync(d_first, 0xFF, od * 4, b->stream));
-        HIPCHK(hipMemsetAsync(d_fscore, 0, od * 4, b->stream));
-        HIPCHK(launch_mlst_sum(d_hits + n_direct * D, b->tmp.as<uint32_t>(), n_chunks, D, threshold,
-                               b->totals.as<unsigned long long>(), d_first, d_fscore, b->stream));
-        if (owner_scores) HIPCHK(hipMemcpyAsync(owner_scores, b->totals.p, od * 8, hipMemcpyDeviceToHost, b->stream));
-        if (owner_first) HIPCHK(hipMemcpyAsync(owner_first, d_first, od * 4, hipMemcpyDeviceToHost, b->stream));
-        if (owner_first_score)
-            HIPCHK(hipMemcpyAsync(owner_first_score, d_fscore, od * 4, hipMemcpyDeviceToHost, b->stream));
-        if (int rc = ws_leave(b, b->stream)) return rc;
-    }
-    HIPCHK(hipStreamSynchronize(b->stream));
-    return XS_OK;
+        if (int rc = b->hits.ensure(n * D * 4)) return rc;
+        uint32_t* d_hits = b->hits.as<uint32_t>();
+        // every record probed in one pass; only the direct rows cross to the host
+        if (int rc = query_host(b, seqs, offsets, n, step, d_hits, nullptr, nullptr, nullptr)) return rc;
+        if (n_direct && direct_hits)
+            if (int rc = d2h_pageable(b, direct_hits, d_hits, n_direct * D * 4, b->stream)) return rc;
+        if (n_chunks && n_owners) {
+            if (int rc = ws_enter(b, b->stream)) return rc;
+            if (int rc = b->tmp.ensure(n_chunks * 4)) return rc;
+            if (int rc = b->totals.ensure(od * 8)) return rc;
+            if (int rc = b->best.ensure(od * 8)) return rc;
+            uint32_t* d_first = b->best.as<uint32_t>();
+            uint32_t* d_fscore = d_first + od;
+            HIPCHK(hipMemcpyAsync(b->tmp.p, chunk_owner, n_chunks * 4, hipMemcpyHostToDevice, b->stream));
+            HIPCHK(hipMemsetAsync(b->totals.p, 0, od * 8, b->stream));
+            HIPCHK(hipMemsetAsync(d_first, 0xFF, od * 4, b->stream));
+            HIPCHK(hipMemsetAsync(d_fscore, 0, od * 4, b->stream));
+            HIPCHK(launch_mlst_sum(d_hits + n_direct * D, b->tmp.as<uint32_t>(), n_chunks, D, threshold,
+                                   b->totals.as<unsigned long long>(), d_first, d_fscore, b->stream));
+            if (owner_scores) HIPCHK(hipMemcpyAsync(owner_scores, b->totals.p, od * 8, hipMemcpyDeviceToHost, b->stream));
+            if (owner_first) HIPCHK(hipMemcpyAsync(owner_first, d_first, od * 4, hipMemcpyDeviceToHost, b->stream));
+            if (owner_first_score)
+                HIPCHK(hipMemcpyAsync(owner_first_score, d_fscore, od * 4, hipMemcpyDeviceToHost, b->stream));
+            if (int rc = ws_leave(b, b->stream)) return rc;
+        }
+        HIPCHK(hipStreamSynchronize(b->stream));
+        return XS_OK;
+    });
 }
 
 int xs_bank_set_profiling(xs_bank* b, int on) {
-    if (!b) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (on && !b->profiling) {
-        HIPCHK(hipSetDevice(b->device));
-        if (int rc = b->rows_read.ensure(sizeof(uint64_t))) return rc;
-        HIPCHK(hipMemsetAsync(b->rows_read.p, 0, sizeof(uint64_t), b->stream));
-        HIPCHK(hipStreamSynchronize(b->stream));
-    }
-    if (on != 0 && !b->profiling) {  // a fresh profiling session: no marks left from an earlier one
-        b->pass_used = 0;
-        b->events_used = 0;
-    }
-    b->profiling = on != 0;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (on && !b->profiling) {
+            HIPCHK(hipSetDevice(b->device));
+            if (int rc = b->rows_read.ensure(sizeof(uint64_t))) return rc;
+            HIPCHK(hipMemsetAsync(b->rows_read.p, 0, sizeof(uint64_t), b->stream));
+            HIPCHK(hipStreamSynchronize(b->stream));
+        }
+        if (on != 0 && !b->profiling) {  // a fresh profiling session: no marks left from an earlier one
+            b->pass_used = 0;
+            b->events_used = 0;
+        }
+        b->profiling = on != 0;
+        return XS_OK;
+    });
 }
 
 int xs_bank_probe_rows(xs_bank* b, uint64_t* rows) {
-    if (!b || !rows) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    *rows = 0;
-    if (b->kind != XS_BANK_RBLOOM || !b->rows_read.p) return XS_OK;
-    HIPCHK(hipSetDevice(b->device));
-    HIPCHK(hipDeviceSynchronize());  // probes may have run on a caller's stream
-    HIPCHK(hipMemcpy(rows, b->rows_read.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
-    HIPCHK(hipMemset(b->rows_read.p, 0, sizeof(uint64_t)));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !rows) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        *rows = 0;
+        if (b->kind != XS_BANK_RBLOOM || !b->rows_read.p) return XS_OK;
+        HIPCHK(hipSetDevice(b->device));
+        HIPCHK(hipDeviceSynchronize());  // probes may have run on a caller's stream
+        HIPCHK(hipMemcpy(rows, b->rows_read.p, sizeof(uint64_t), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemset(b->rows_read.p, 0, sizeof(uint64_t)));
+        return XS_OK;
+    });
 }
 
 int xs_bank_probe_path(const xs_bank* b, int* path) {
-    if (!b || !path) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);  // after any query in flight on the handle
-    *path = b->last_path;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !path) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);  // after any query in flight on the handle
+        *path = b->last_path;
+        return XS_OK;
+    });
 }
 
 int xs_bank_last_probe_ms(xs_bank* b, float* ms) {
-    if (!b || !ms) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    if (b->events_used == 0) return fail(XS_ERR_ARG, "no profiled query on this handle");
-    HIPCHK(hipSetDevice(b->device));
-    auto& ev = b->events[b->events_used - 1];
-    HIPCHK(hipEventSynchronize(ev.second));
-    HIPCHK(hipEventElapsedTime(ms, ev.first, ev.second));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !ms) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->events_used == 0) return fail(XS_ERR_ARG, "no profiled query on this handle");
+        HIPCHK(hipSetDevice(b->device));
+        auto& ev = b->events[b->events_used - 1];
+        HIPCHK(hipEventSynchronize(ev.second));
+        HIPCHK(hipEventElapsedTime(ms, ev.first, ev.second));
+        return XS_OK;
+    });
 }
 
 int xs_bank_probe_stats(xs_bank* b, uint64_t* count, double* total_ms, float* max_ms) {
-    if (!b || !count || !total_ms) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    double tot = 0.0;
-    float mx = 0.0f;
-    for (size_t i = 0; i < b->events_used; ++i) {
-        float ms = 0.0f;
-        HIPCHK(hipEventSynchronize(b->events[i].second));
-        HIPCHK(hipEventElapsedTime(&ms, b->events[i].first, b->events[i].second));
-        tot += ms;
-        mx = ms > mx ? ms : mx;
-    }
-    *count = b->events_used;
-    *total_ms = tot;
-    if (max_ms) *max_ms = mx;
-    b->events_used = 0;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !count || !total_ms) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        double tot = 0.0;
+        float mx = 0.0f;
+        for (size_t i = 0; i < b->events_used; ++i) {
+            float ms = 0.0f;
+            HIPCHK(hipEventSynchronize(b->events[i].second));
+            HIPCHK(hipEventElapsedTime(&ms, b->events[i].first, b->events[i].second));
+            tot += ms;
+            mx = ms > mx ? ms : mx;
+        }
+        *count = b->events_used;
+        *total_ms = tot;
+        if (max_ms) *max_ms = mx;
+        b->events_used = 0;
+        return XS_OK;
+    });
 }
 
 int xs_bank_pass_stats(xs_bank* b, double* ms, uint64_t* count) {
-    if (!b || !ms || !count) return fail(XS_ERR_ARG, "null argument");
-    std::lock_guard<std::mutex> lk(b->mu);
-    HIPCHK(hipSetDevice(b->device));
-    for (int t = 0; t < kPassTags; ++t) {
-        ms[t] = 0.0;
-        count[t] = 0;
-    }
-    for (size_t i = 1; i < b->pass_used; ++i) {
-        const int t = b->pass_tag[i];
-        if (t < 0 || t >= kPassTags) continue;  // a query's opening mark
-        float x = 0.0f;
-        HIPCHK(hipEventSynchronize(b->pass_ev[i]));
-        HIPCHK(hipEventElapsedTime(&x, b->pass_ev[i - 1], b->pass_ev[i]));
-        ms[t] += x;
-        ++count[t];
-    }
-    b->pass_used = 0;
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b || !ms || !count) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(b->mu);
+        HIPCHK(hipSetDevice(b->device));
+        for (int t = 0; t < kPassTags; ++t) {
+            ms[t] = 0.0;
+            count[t] = 0;
+        }
+        for (size_t i = 1; i < b->pass_used; ++i) {
+            const int t = b->pass_tag[i];
+            if (t < 0 || t >= kPassTags) continue;  // a query's opening mark
+            float x = 0.0f;
+            HIPCHK(hipEventSynchronize(b->pass_ev[i]));
+            HIPCHK(hipEventElapsedTime(&x, b->pass_ev[i - 1], b->pass_ev[i]));
+            ms[t] += x;
+            ++count[t];
+        }
+        b->pass_used = 0;
+        return XS_OK;
+    });
 }
 
 void xs_bank_close(xs_bank* b) {
-    if (!b) return;
-    (void)hipSetDevice(b->device);
-    if (b->ws_used) (void)hipEventSynchronize(b->ws_ev);  // the last call's stream may be the caller's
-    if (b->ws_ev) (void)hipEventDestroy(b->ws_ev);
-    if (b->stream) (void)hipStreamSynchronize(b->stream);
-    for (hipStream_t st : {b->copy_stream, b->d2h_stream})
-        if (st) (void)hipStreamSynchronize(st);
-    for (auto& ev : b->stage_ev)
-        if (ev) (void)hipEventDestroy(ev);
-    for (auto& ev : b->hstage_ev)
-        if (ev) (void)hipEventDestroy(ev);
-    if (b->bloom_ev) (void)hipEventDestroy(b->bloom_ev);
-    for (auto& ev : b->chunk_ev) (void)hipEventDestroy(ev);
-    for (auto& ev : b->events) {
-        (void)hipEventDestroy(ev.first);
-        (void)hipEventDestroy(ev.second);
-    }
-    for (auto& ev : b->pass_ev) (void)hipEventDestroy(ev);
-    for (hipStream_t st : {b->stream, b->copy_stream, b->d2h_stream})
-        if (st) (void)hipStreamDestroy(st);
-    delete b;  // DevBuf destructors free device memory
+    xs::guard([&] {
+        if (!b) return;
+        (void)hipSetDevice(b->device);
+        if (b->ws_used) (void)hipEventSynchronize(b->ws_ev);  // the last call's stream may be the caller's
+        if (b->ws_ev) (void)hipEventDestroy(b->ws_ev);
+        if (b->stream) (void)hipStreamSynchronize(b->stream);
+        for (hipStream_t st : {b->copy_stream, b->d2h_stream})
+            if (st) (void)hipStreamSynchronize(st);
+        for (auto& ev : b->stage_ev)
+            if (ev) (void)hipEventDestroy(ev);
+        for (auto& ev : b->hstage_ev)
+            if (ev) (void)hipEventDestroy(ev);
+        if (b->bloom_ev) (void)hipEventDestroy(b->bloom_ev);
+        for (auto& ev : b->chunk_ev) (void)hipEventDestroy(ev);
+        for (auto& ev : b->events) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+        for (auto& ev : b->pass_ev) (void)hipEventDestroy(ev);
+        for (hipStream_t st : {b->stream, b->copy_stream, b->d2h_stream})
+            if (st) (void)hipStreamDestroy(st);
+        delete b;  // DevBuf destructors free device memory
+    });
 }
 
 }  // extern "C"

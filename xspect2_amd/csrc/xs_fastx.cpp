@@ -1190,265 +1190,279 @@ int upload_host_batch(xs_fastx* r, const xs_fastx_batch& hb, int slot, xs_fastx_
 extern "C" {
 
 int xs_fastx_open(const char* path, int format, int threads, int flags, xs_fastx** out) {
-    return xs_fastx_open_range(path, format, threads, flags, 0, 1, out);
+    return xs::guard([&]() -> int {
+        return xs_fastx_open_range(path, format, threads, flags, 0, 1, out);
+    });
 }
 
 int xs_fastx_open_range(const char* path, int format, int threads, int flags, uint32_t part, uint32_t parts,
                         xs_fastx** out) {
-    if (!path || !out) return xs::set_error(XS_ERR_ARG, "null argument");
-    if (parts == 0 || part >= parts) return xs::set_error(XS_ERR_ARG, "part must be < parts");
-    if (format != XS_FASTX_FASTA && format != XS_FASTX_FASTQ)
-        return xs::set_error(XS_ERR_ARG, "format must be XS_FASTX_FASTA or XS_FASTX_FASTQ");
-    *out = nullptr;
-    auto* r = new xs_fastx();
-    r->format = format;
-    r->fd = open(path, O_RDONLY);
-    if (r->fd < 0) {
-        delete r;
-        return xs::set_error(XS_ERR_IO, (std::string("cannot open ") + path).c_str());
-    }
-    struct stat st;
-    if (fstat(r->fd, &st) != 0) {
-        delete r;
-        return xs::set_error(XS_ERR_IO, (std::string("cannot stat ") + path).c_str());
-    }
-    r->size = (size_t)st.st_size;
-    if (r->size) {
-        void* m = mmap(nullptr, r->size, PROT_READ, MAP_PRIVATE, r->fd, 0);
-        if (m == MAP_FAILED) {
+    return xs::guard([&]() -> int {
+        if (!path || !out) return xs::set_error(XS_ERR_ARG, "null argument");
+        if (parts == 0 || part >= parts) return xs::set_error(XS_ERR_ARG, "part must be < parts");
+        if (format != XS_FASTX_FASTA && format != XS_FASTX_FASTQ)
+            return xs::set_error(XS_ERR_ARG, "format must be XS_FASTX_FASTA or XS_FASTX_FASTQ");
+        *out = nullptr;
+        auto* r = new xs_fastx();
+        r->format = format;
+        r->fd = open(path, O_RDONLY);
+        if (r->fd < 0) {
             delete r;
-            return xs::set_error(XS_ERR_IO, (std::string("cannot map ") + path).c_str());
+            return xs::set_error(XS_ERR_IO, (std::string("cannot open ") + path).c_str());
         }
-        r->base = static_cast<const char*>(m);
-        (void)madvise(m, r->size, MADV_SEQUENTIAL);
-    }
-    int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
-    r->threads = std::min(t, 64);
-    if (format == XS_FASTX_FASTQ && r->size) r->wrapped = fastq_wrapped(r->base, r->base + r->size);
-    // Part p of P: the records whose first byte lies in [cut(p), cut(p+1)), cut(i)
-    // = the first record start at or after size*i/P (cut(0) = 0, cut(P) = size).
-    // Every record belongs to exactly one part, in file order.
-    r->stop = r->size;
-    if (parts > 1 && r->size) {
-        const char* lo = r->base;
-        const char* end = r->base + r->size;
-        auto cut = [&](uint64_t i) -> size_t {
-            if (i == 0) return 0;
-            if (i >= parts) return r->size;
-            const char* pos = lo + (size_t)((unsigned __int128)r->size * i / parts);
-            const char* c = format == XS_FASTX_FASTA ? fasta_boundary(lo, pos, end)
-                            : r->wrapped             ? fastq_boundary_sequential(lo, pos, end)
-                                                     : fastq_boundary(lo, pos, end);
-            return (size_t)(c - lo);
-        };
-        r->cur = cut(part);
-        r->stop = std::max(r->cur, cut((uint64_t)part + 1));
-    }
-    for (auto& b : r->batch) {
-        const bool pinned = (flags & XS_FASTX_PINNED) != 0;
-        b.seqs.pinned = b.offs.pinned = pinned;
-    }
-    r->parts.resize((size_t)r->threads);
-    *out = r;
-    return XS_OK;
+        struct stat st;
+        if (fstat(r->fd, &st) != 0) {
+            delete r;
+            return xs::set_error(XS_ERR_IO, (std::string("cannot stat ") + path).c_str());
+        }
+        r->size = (size_t)st.st_size;
+        if (r->size) {
+            void* m = mmap(nullptr, r->size, PROT_READ, MAP_PRIVATE, r->fd, 0);
+            if (m == MAP_FAILED) {
+                delete r;
+                return xs::set_error(XS_ERR_IO, (std::string("cannot map ") + path).c_str());
+            }
+            r->base = static_cast<const char*>(m);
+            (void)madvise(m, r->size, MADV_SEQUENTIAL);
+        }
+        int t = threads > 0 ? threads : (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        r->threads = std::min(t, 64);
+        if (format == XS_FASTX_FASTQ && r->size) r->wrapped = fastq_wrapped(r->base, r->base + r->size);
+        // Part p of P: the records whose first byte lies in [cut(p), cut(p+1)), cut(i)
+        // = the first record start at or after size*i/P (cut(0) = 0, cut(P) = size).
+        // Every record belongs to exactly one part, in file order.
+        r->stop = r->size;
+        if (parts > 1 && r->size) {
+            const char* lo = r->base;
+            const char* end = r->base + r->size;
+            auto cut = [&](uint64_t i) -> size_t {
+                if (i == 0) return 0;
+                if (i >= parts) return r->size;
+                const char* pos = lo + (size_t)((unsigned __int128)r->size * i / parts);
+                const char* c = format == XS_FASTX_FASTA ? fasta_boundary(lo, pos, end)
+                                : r->wrapped             ? fastq_boundary_sequential(lo, pos, end)
+                                                         : fastq_boundary(lo, pos, end);
+                return (size_t)(c - lo);
+            };
+            r->cur = cut(part);
+            r->stop = std::max(r->cur, cut((uint64_t)part + 1));
+        }
+        for (auto& b : r->batch) {
+            const bool pinned = (flags & XS_FASTX_PINNED) != 0;
+            b.seqs.pinned = b.offs.pinned = pinned;
+        }
+        r->parts.resize((size_t)r->threads);
+        *out = r;
+        return XS_OK;
+    });
 }
 
 int xs_fastx_next(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_batch* out) {
-    if (!r || !out) return xs::set_error(XS_ERR_ARG, "null argument");
-    memset(out, 0, sizeof(*out));
-    Batch& bt = r->batch[r->flip];
-    r->flip ^= 1;
-    bt.n = bt.seq_bytes = 0;
-    const char* end = r->base + r->stop;
-    int nparts = 0;
-    // a window can hold no record (text before the first one): go on until
-    // records are found or the file ends
-    for (;;) {
-        const char* lo = r->base + r->cur;
-        const size_t budget = window_budget(max_text_bytes, r->windows);
-        nparts = 0;
-        if (lo < end) {
-            ++r->windows;
-            if (r->format == XS_FASTX_FASTQ && r->wrapped) {
-                // sequential: the parser itself stops at the first record past the budget
-                Part& pt = r->parts[0];
-                pt.clear();
-                parse_fastq(lo, end, budget, pt);
-                nparts = 1;
-                if (!pt.err.empty()) return xs::set_error(XS_ERR_FORMAT, pt.err.c_str());
-            } else if (int rc = parse_window(r, lo, window_end(r, lo, end, budget), &nparts)) {
-                return rc;
+    return xs::guard([&]() -> int {
+        if (!r || !out) return xs::set_error(XS_ERR_ARG, "null argument");
+        memset(out, 0, sizeof(*out));
+        Batch& bt = r->batch[r->flip];
+        r->flip ^= 1;
+        bt.n = bt.seq_bytes = 0;
+        const char* end = r->base + r->stop;
+        int nparts = 0;
+        // a window can hold no record (text before the first one): go on until
+        // records are found or the file ends
+        for (;;) {
+            const char* lo = r->base + r->cur;
+            const size_t budget = window_budget(max_text_bytes, r->windows);
+            nparts = 0;
+            if (lo < end) {
+                ++r->windows;
+                if (r->format == XS_FASTX_FASTQ && r->wrapped) {
+                    // sequential: the parser itself stops at the first record past the budget
+                    Part& pt = r->parts[0];
+                    pt.clear();
+                    parse_fastq(lo, end, budget, pt);
+                    nparts = 1;
+                    if (!pt.err.empty()) return xs::set_error(XS_ERR_FORMAT, pt.err.c_str());
+                } else if (int rc = parse_window(r, lo, window_end(r, lo, end, budget), &nparts)) {
+                    return rc;
+                }
             }
+            if (nparts) r->cur = (size_t)(r->parts[nparts - 1].stop - r->base);
+            size_t got = 0;
+            for (int i = 0; i < nparts; ++i) got += r->parts[i].lens.size();
+            if (got || r->cur >= r->stop || !nparts) break;
         }
-        if (nparts) r->cur = (size_t)(r->parts[nparts - 1].stop - r->base);
-        size_t got = 0;
-        for (int i = 0; i < nparts; ++i) got += r->parts[i].lens.size();
-        if (got || r->cur >= r->stop || !nparts) break;
-    }
-    if (int rc = pack_parts(r, bt, nparts)) return rc;
-    r->records += bt.n;
-    fill_host_batch(r, bt, out);
-    return XS_OK;
+        if (int rc = pack_parts(r, bt, nparts)) return rc;
+        r->records += bt.n;
+        fill_host_batch(r, bt, out);
+        return XS_OK;
+    });
 }
 
 int xs_fastx_open_device(const char* path, int format, int threads, int device, uint32_t part, uint32_t parts,
                          xs_fastx** out) {
-    if (int rc = xs_fastx_open_range(path, format, threads, 0, part, parts, out)) return rc;
-    xs_fastx* r = *out;
-    auto fail = [&](hipError_t e) {
-        xs_fastx_close(r);
-        *out = nullptr;
-        return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
-    };
-    hipError_t e = hipSetDevice(device);
-    if (e != hipSuccess) return fail(e);
-    if ((r->dev = take_devside(device))) return XS_OK;
-    r->dev = new DevSide();
-    r->dev->set_device(device);
-    if (take_streams(*r->dev)) return XS_OK;
-    // The parse kernels are short and sit between the caller's probes of the
-    // previous batch: a high-priority stream lets their workgroups in as soon
-    // as the probe frees a slot, instead of after the whole probe.  The text
-    // DMA has a stream of its own, so the next window's copy never queues
-    // behind this window's parse.
-    int least = 0, greatest = 0;
-    if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    (void)least;
-    if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
-    for (hipEvent_t* ev : {&r->dev->text_ev[0], &r->dev->text_ev[1], &r->dev->kern_ev, &r->dev->host_ev[0],
-                           &r->dev->host_ev[1]})
-        if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-    if (e != hipSuccess) return fail(e);
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (int rc = xs_fastx_open_range(path, format, threads, 0, part, parts, out)) return rc;
+        xs_fastx* r = *out;
+        auto fail = [&](hipError_t e) {
+            xs_fastx_close(r);
+            *out = nullptr;
+            return xs::set_error(XS_ERR_HIP, hipGetErrorString(e));
+        };
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess) return fail(e);
+        if ((r->dev = take_devside(device))) return XS_OK;
+        r->dev = new DevSide();
+        r->dev->set_device(device);
+        if (take_streams(*r->dev)) return XS_OK;
+        // The parse kernels are short and sit between the caller's probes of the
+        // previous batch: a high-priority stream lets their workgroups in as soon
+        // as the probe frees a slot, instead of after the whole probe.  The text
+        // DMA has a stream of its own, so the next window's copy never queues
+        // behind this window's parse.
+        int least = 0, greatest = 0;
+        if (e == hipSuccess) e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+        (void)least;
+        if (e == hipSuccess) e = hipStreamCreateWithPriority(&r->dev->stream, hipStreamNonBlocking, greatest);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&r->dev->copy, hipStreamNonBlocking);
+        for (hipEvent_t* ev : {&r->dev->text_ev[0], &r->dev->text_ev[1], &r->dev->kern_ev, &r->dev->host_ev[0],
+                               &r->dev->host_ev[1]})
+            if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
+        if (e != hipSuccess) return fail(e);
+        return XS_OK;
+    });
 }
 
 int xs_fastx_wait_host(const xs_fastx_dbatch* b) {
-    if (!b) return xs::set_error(XS_ERR_ARG, "null argument");
-    if (b->host_ready) FXCHK(hipEventSynchronize(static_cast<hipEvent_t>(b->host_ready)));
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!b) return xs::set_error(XS_ERR_ARG, "null argument");
+        if (b->host_ready) FXCHK(hipEventSynchronize(static_cast<hipEvent_t>(b->host_ready)));
+        return XS_OK;
+    });
 }
 
 int xs_fastx_next_device(xs_fastx* r, uint64_t max_text_bytes, xs_fastx_dbatch* out) {
-    if (!r || !out) return xs::set_error(XS_ERR_ARG, "null argument");
-    if (!r->dev) return xs::set_error(XS_ERR_ARG, "reader was not opened with xs_fastx_open_device");
-    memset(out, 0, sizeof(*out));
-    DevSide& d = *r->dev;
-    FXCHK(hipSetDevice(d.device));
-    if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f next_device\n", fx_ms());
-    const int slot = d.flip;
-    d.flip ^= 1;
-    if (r->format == XS_FASTX_FASTQ && r->wrapped) {  // records cannot be cut by pattern: host parser
-        xs_fastx_batch hb;
-        if (int rc = xs_fastx_next(r, max_text_bytes, &hb)) return rc;
-        if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
-        out->text_offset = hb.text_offset;
-        out->text_bytes = hb.text_bytes;
-        return XS_OK;
-    }
-    const char* end = r->base + r->stop;
-    for (;;) {
-        if (r->cur >= r->stop) {
-            drain_loads(d);
-            out->text_offset = r->cur;
-            out->text_bytes = r->stop;
-            return XS_OK;
-        }
-        const char* lo = r->base + r->cur;
-        const char* hi = window_end(r, lo, end, window_budget(max_text_bytes, r->windows));
-        const size_t flo = (size_t)(lo - r->base), fhi = (size_t)(hi - r->base);
-        const double t0 = fx_ms();
-        bool prefetched = false;
-        int ts = 0;
-        if (int rc = text_for(r, flo, fhi, &ts, &prefetched)) return rc;
-        const double t1 = fx_ms();
-        r->cur = fhi;
-        ++r->windows;
-        // The next window's text loads into the other slot while this one is
-        // parsed and the caller works on the batch; the one after it goes
-        // into this window's slot once this parse is done.
-        size_t n1_hi = 0;  // end of the next window
-        if (r->cur < r->stop)
-            n1_hi = (size_t)(window_end(r, r->base + r->cur, end, window_budget(max_text_bytes, r->windows)) - r->base);
-        auto queue_next = [&] {
-            if (n1_hi && !is_queued(d, r->cur)) queue_window(r, r->cur, n1_hi);
-        };
-        queue_next();
-        bool ok = false;
-        g_fx = FxTimes{};
-        if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
-        if (n1_hi && n1_hi < r->stop && !is_queued(d, n1_hi))  // this slot's text is free now
-            queue_window(r, n1_hi,
-                         (size_t)(window_end(r, r->base + n1_hi, end, window_budget(max_text_bytes, r->windows + 1)) -
-                                  r->base));
-        if (fx_trace())
-            fprintf(stderr,
-                    "[fastx-device] t=%.2f window %zu+%zu: text %s load %.2f ms, wait %.2f ms | count %.2f records %.2f "
-                    "copy %.2f ms | %s\n",
-                    t0, flo, fhi - flo, prefetched ? "prefetched" : "inline", d.load_ms[ts], t1 - t0, g_fx.count,
-                    g_fx.records, g_fx.copy, ok ? "device" : "host parser");
-        if (!ok) {  // the host parser's batch for exactly this window
-            int nparts = 0;
-            if (int rc = parse_window(r, lo, hi, &nparts)) return rc;
-            Batch& bt = r->batch[r->flip];
-            r->flip ^= 1;
-            if (int rc = pack_parts(r, bt, nparts)) return rc;
+    return xs::guard([&]() -> int {
+        if (!r || !out) return xs::set_error(XS_ERR_ARG, "null argument");
+        if (!r->dev) return xs::set_error(XS_ERR_ARG, "reader was not opened with xs_fastx_open_device");
+        memset(out, 0, sizeof(*out));
+        DevSide& d = *r->dev;
+        FXCHK(hipSetDevice(d.device));
+        if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f next_device\n", fx_ms());
+        const int slot = d.flip;
+        d.flip ^= 1;
+        if (r->format == XS_FASTX_FASTQ && r->wrapped) {  // records cannot be cut by pattern: host parser
             xs_fastx_batch hb;
-            memset(&hb, 0, sizeof(hb));
-            fill_host_batch(r, bt, &hb);
+            if (int rc = xs_fastx_next(r, max_text_bytes, &hb)) return rc;
             if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
-        }
-        if (out->n) {
-            r->records += out->n;
-            out->text_offset = r->cur;
-            out->text_bytes = r->stop;
-            if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f return n=%llu\n", fx_ms(), (unsigned long long)out->n);
+            out->text_offset = hb.text_offset;
+            out->text_bytes = hb.text_bytes;
             return XS_OK;
         }
-        memset(out, 0, sizeof(*out));  // no record in this window (text before the first one)
-    }
+        const char* end = r->base + r->stop;
+        for (;;) {
+            if (r->cur >= r->stop) {
+                drain_loads(d);
+                out->text_offset = r->cur;
+                out->text_bytes = r->stop;
+                return XS_OK;
+            }
+            const char* lo = r->base + r->cur;
+            const char* hi = window_end(r, lo, end, window_budget(max_text_bytes, r->windows));
+            const size_t flo = (size_t)(lo - r->base), fhi = (size_t)(hi - r->base);
+            const double t0 = fx_ms();
+            bool prefetched = false;
+            int ts = 0;
+            if (int rc = text_for(r, flo, fhi, &ts, &prefetched)) return rc;
+            const double t1 = fx_ms();
+            r->cur = fhi;
+            ++r->windows;
+            // The next window's text loads into the other slot while this one is
+            // parsed and the caller works on the batch; the one after it goes
+            // into this window's slot once this parse is done.
+            size_t n1_hi = 0;  // end of the next window
+            if (r->cur < r->stop)
+                n1_hi = (size_t)(window_end(r, r->base + r->cur, end, window_budget(max_text_bytes, r->windows)) - r->base);
+            auto queue_next = [&] {
+                if (n1_hi && !is_queued(d, r->cur)) queue_window(r, r->cur, n1_hi);
+            };
+            queue_next();
+            bool ok = false;
+            g_fx = FxTimes{};
+            if (int rc = parse_on_device(r, flo, fhi, slot, ts, &ok, out)) return rc;
+            if (n1_hi && n1_hi < r->stop && !is_queued(d, n1_hi))  // this slot's text is free now
+                queue_window(r, n1_hi,
+                             (size_t)(window_end(r, r->base + n1_hi, end, window_budget(max_text_bytes, r->windows + 1)) -
+                                      r->base));
+            if (fx_trace())
+                fprintf(stderr,
+                        "[fastx-device] t=%.2f window %zu+%zu: text %s load %.2f ms, wait %.2f ms | count %.2f records %.2f "
+                        "copy %.2f ms | %s\n",
+                        t0, flo, fhi - flo, prefetched ? "prefetched" : "inline", d.load_ms[ts], t1 - t0, g_fx.count,
+                        g_fx.records, g_fx.copy, ok ? "device" : "host parser");
+            if (!ok) {  // the host parser's batch for exactly this window
+                int nparts = 0;
+                if (int rc = parse_window(r, lo, hi, &nparts)) return rc;
+                Batch& bt = r->batch[r->flip];
+                r->flip ^= 1;
+                if (int rc = pack_parts(r, bt, nparts)) return rc;
+                xs_fastx_batch hb;
+                memset(&hb, 0, sizeof(hb));
+                fill_host_batch(r, bt, &hb);
+                if (int rc = upload_host_batch(r, hb, slot, out)) return rc;
+            }
+            if (out->n) {
+                r->records += out->n;
+                out->text_offset = r->cur;
+                out->text_bytes = r->stop;
+                if (fx_trace()) fprintf(stderr, "[fastx-device] t=%.2f return n=%llu\n", fx_ms(), (unsigned long long)out->n);
+                return XS_OK;
+            }
+            memset(out, 0, sizeof(*out));  // no record in this window (text before the first one)
+        }
+    });
 }
 
 void xs_fastx_close(xs_fastx* r) { delete r; }
 
 int xs_write_fasta(const char* path, int append, const char* seqs, const uint64_t* offsets, const char* descs,
                    const uint64_t* desc_offsets, const uint32_t* index, uint64_t n, uint32_t width) {
-    if (!path || (n && (!seqs || !offsets || !desc_offsets))) return xs::set_error(XS_ERR_ARG, "null argument");
-    if (width == 0) return xs::set_error(XS_ERR_ARG, "width must be >= 1");
-    FILE* f = fopen(path, append ? "ab" : "wb");
-    if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot open ") + path).c_str());
-    const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, n / 4096));
-    const uint64_t block = 1 << 15;
-    std::vector<std::string> out((size_t)T);
-    bool ok = true;
-    for (uint64_t b0 = 0; b0 < n && ok; b0 += block) {
-        const uint64_t b1 = std::min(n, b0 + block), per = (b1 - b0 + T - 1) / T;
-        auto work = [&](int t) {
-            std::string& o = out[t];
-            o.clear();
-            const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
-            for (uint64_t i = lo; i < hi; ++i) {
-                const uint64_t r = index ? index[i] : i;
-                o += '>';
-                o.append(descs + desc_offsets[r], (size_t)(desc_offsets[r + 1] - desc_offsets[r]));
-                o += '\n';
-                const char* s = seqs + offsets[r];
-                const uint64_t len = offsets[r + 1] - offsets[r];
-                for (uint64_t p = 0; p < len; p += width) {
-                    o.append(s + p, (size_t)std::min<uint64_t>(width, len - p));
+    return xs::guard([&]() -> int {
+        if (!path || (n && (!seqs || !offsets || !desc_offsets))) return xs::set_error(XS_ERR_ARG, "null argument");
+        if (width == 0) return xs::set_error(XS_ERR_ARG, "width must be >= 1");
+        FILE* f = fopen(path, append ? "ab" : "wb");
+        if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot open ") + path).c_str());
+        const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, n / 4096));
+        const uint64_t block = 1 << 15;
+        std::vector<std::string> out((size_t)T);
+        bool ok = true;
+        for (uint64_t b0 = 0; b0 < n && ok; b0 += block) {
+            const uint64_t b1 = std::min(n, b0 + block), per = (b1 - b0 + T - 1) / T;
+            auto work = [&](int t) {
+                std::string& o = out[t];
+                o.clear();
+                const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
+                for (uint64_t i = lo; i < hi; ++i) {
+                    const uint64_t r = index ? index[i] : i;
+                    o += '>';
+                    o.append(descs + desc_offsets[r], (size_t)(desc_offsets[r + 1] - desc_offsets[r]));
                     o += '\n';
+                    const char* s = seqs + offsets[r];
+                    const uint64_t len = offsets[r + 1] - offsets[r];
+                    for (uint64_t p = 0; p < len; p += width) {
+                        o.append(s + p, (size_t)std::min<uint64_t>(width, len - p));
+                        o += '\n';
+                    }
                 }
-            }
-        };
-        std::vector<std::thread> th;
-        for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-        work(0);
-        for (auto& x : th) x.join();
-        for (int t = 0; t < T && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
-    }
-    if (fclose(f) != 0) ok = false;
-    if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
-    return XS_OK;
+            };
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; ++t) th.emplace_back(work, t);
+            work(0);
+            for (auto& x : th) x.join();
+            for (int t = 0; t < T && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
+        }
+        if (fclose(f) != 0) ok = false;
+        if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
+        return XS_OK;
+    });
 }
 
 }  // extern "C"

@@ -3,6 +3,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <exception>
+#include <new>
+#include <type_traits>
 #include <vector>
 #include <stdint.h>
 
@@ -254,5 +257,31 @@ hipError_t launch_max_u64(void* temp, size_t temp_bytes, const uint64_t* in, uin
 
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
+
+// Every C-ABI entry point runs its body under guard(): a C++ exception (a
+// host vector that cannot be allocated, a worker thread that cannot start)
+// becomes XS_ERR_NOMEM / XS_ERR_INTERNAL and a message instead of unwinding
+// into the caller's C frames, where it would end the process.
+template <class R>
+R guard_failed(int code, const char* msg) noexcept {
+    const int rc = set_error(code, msg);
+    if constexpr (std::is_same_v<R, int>) return rc;
+    else if constexpr (std::is_pointer_v<R>) return nullptr;
+    else if constexpr (!std::is_void_v<R>) return R{};
+}
+
+template <class F>
+auto guard(F&& f) noexcept -> decltype(f()) {
+    using R = decltype(f());
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        return guard_failed<R>(-6 /* XS_ERR_NOMEM */, "host memory allocation failed");
+    } catch (const std::exception& e) {
+        return guard_failed<R>(-7 /* XS_ERR_INTERNAL */, e.what());
+    } catch (...) {
+        return guard_failed<R>(-7 /* XS_ERR_INTERNAL */, "unknown C++ exception");
+    }
+}
 
 }  // namespace xs

@@ -300,20 +300,22 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
                              const char* labels_json, const uint64_t* labels_off, const uint8_t* doc_mask,
                              const uint64_t* total_hits, uint64_t total_kmers, const uint32_t* total_order_row,
                              int threads) {
-    if (!path || (n && (!hits || !num_kmers || !ids_json || !ids_off)) || !labels_json || !labels_off)
-        return xs::set_error(XS_ERR_ARG, "null argument");
-    if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return xs::set_error(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
-    if (total_hits) {
-        if (!total_order_row) return xs::set_error(XS_ERR_ARG, "total_hits needs total_order_row");
-        if (total_kmers == 0) return xs::set_error(XS_ERR_ARG, "total_kmers must be > 0 (scores divide by it)");
-    } else if (n == 0) {
-        return xs::set_error(XS_ERR_ARG, "a result needs at least one read");
-    }
-    for (uint64_t r = 0; r < n; ++r)
-        if (num_kmers[r] == 0) return xs::set_error(XS_ERR_ARG, "a read has no k-mers (scores divide by zero)");
-    auto w = hit_bytes == 1 ? write_typed<uint8_t> : hit_bytes == 2 ? write_typed<uint16_t> : write_typed<uint32_t>;
-    return w(path, n, num_docs, hits, num_kmers, ids_json, ids_off, labels_json, labels_off, doc_mask, total_hits,
-             total_kmers, total_order_row, threads);
+    return xs::guard([&]() -> int {
+        if (!path || (n && (!hits || !num_kmers || !ids_json || !ids_off)) || !labels_json || !labels_off)
+            return xs::set_error(XS_ERR_ARG, "null argument");
+        if (hit_bytes != 1 && hit_bytes != 2 && hit_bytes != 4) return xs::set_error(XS_ERR_ARG, "hit_bytes must be 1, 2 or 4");
+        if (total_hits) {
+            if (!total_order_row) return xs::set_error(XS_ERR_ARG, "total_hits needs total_order_row");
+            if (total_kmers == 0) return xs::set_error(XS_ERR_ARG, "total_kmers must be > 0 (scores divide by it)");
+        } else if (n == 0) {
+            return xs::set_error(XS_ERR_ARG, "a result needs at least one read");
+        }
+        for (uint64_t r = 0; r < n; ++r)
+            if (num_kmers[r] == 0) return xs::set_error(XS_ERR_ARG, "a read has no k-mers (scores divide by zero)");
+        auto w = hit_bytes == 1 ? write_typed<uint8_t> : hit_bytes == 2 ? write_typed<uint16_t> : write_typed<uint32_t>;
+        return w(path, n, num_docs, hits, num_kmers, ids_json, ids_off, labels_json, labels_off, doc_mask, total_hits,
+                 total_kmers, total_order_row, threads);
+    });
 }
 
 }  // extern "C"
@@ -329,40 +331,42 @@ int xs_write_result_sections(const char* path, uint64_t n, uint64_t num_docs, co
 // (< 0x20, 0x7f) as \u00xx (lower-case hex); everything else as is.
 int xs_ids_json_quote(const char* buf, const uint64_t* offs, uint64_t n, char* out, uint64_t out_cap,
                       uint64_t* out_offs) {
-    if ((!buf && n && offs[n]) || !offs || (!out && n) || !out_offs) return xs::set_error(XS_ERR_ARG, "null argument");
-    static const char hex[] = "0123456789abcdef";
-    uint64_t o = 0;
-    out_offs[0] = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
-        const uint64_t len = offs[i + 1] - offs[i];
-        if (o + 2 + 6 * len > out_cap) return xs::set_error(XS_ERR_ARG, "output buffer too small");
-        out[o++] = '"';
-        const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
-        for (uint64_t j = 0; j < len; ++j) {
-            const unsigned char c = s[j];
-            if (c >= 0x80) return xs::set_error(XS_ERR_ARG, "non-ASCII id");
-            if (c == '"' || c == '\\') {
-                out[o++] = '\\';
-                out[o++] = (char)c;
-            } else if (c >= 0x20 && c < 0x7f) {
-                out[o++] = (char)c;
-            } else if (c == '\n' || c == '\r' || c == '\t' || c == '\b' || c == '\f') {
-                out[o++] = '\\';
-                out[o++] = c == '\n' ? 'n' : c == '\r' ? 'r' : c == '\t' ? 't' : c == '\b' ? 'b' : 'f';
-            } else {
-                out[o++] = '\\';
-                out[o++] = 'u';
-                out[o++] = '0';
-                out[o++] = '0';
-                out[o++] = hex[c >> 4];
-                out[o++] = hex[c & 15];
+    return xs::guard([&]() -> int {
+        if (!offs || !out_offs || (!out && n) || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
+        static const char hex[] = "0123456789abcdef";
+        uint64_t o = 0;
+        out_offs[0] = 0;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
+            const uint64_t len = offs[i + 1] - offs[i];
+            if (o + 2 + 6 * len > out_cap) return xs::set_error(XS_ERR_ARG, "output buffer too small");
+            out[o++] = '"';
+            const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+            for (uint64_t j = 0; j < len; ++j) {
+                const unsigned char c = s[j];
+                if (c >= 0x80) return xs::set_error(XS_ERR_ARG, "non-ASCII id");
+                if (c == '"' || c == '\\') {
+                    out[o++] = '\\';
+                    out[o++] = (char)c;
+                } else if (c >= 0x20 && c < 0x7f) {
+                    out[o++] = (char)c;
+                } else if (c == '\n' || c == '\r' || c == '\t' || c == '\b' || c == '\f') {
+                    out[o++] = '\\';
+                    out[o++] = c == '\n' ? 'n' : c == '\r' ? 'r' : c == '\t' ? 't' : c == '\b' ? 'b' : 'f';
+                } else {
+                    out[o++] = '\\';
+                    out[o++] = 'u';
+                    out[o++] = '0';
+                    out[o++] = '0';
+                    out[o++] = hex[c >> 4];
+                    out[o++] = hex[c & 15];
+                }
             }
+            out[o++] = '"';
+            out_offs[i + 1] = o;
         }
-        out[o++] = '"';
-        out_offs[i + 1] = o;
-    }
-    return XS_OK;
+        return XS_OK;
+    });
 }
 
 // XXH64 (the published xxHash 64-bit algorithm), host side, for id keys.
@@ -410,109 +414,115 @@ uint64_t xxh64(const unsigned char* p, uint64_t len, uint64_t seed) {
 // key per id, for finding ids repeated across the shards of a read-sharded
 // job without moving the ids themselves.
 int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* out) {
-    if (!offs || (!out && n) || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
-    for (uint64_t i = 0; i < n; ++i)
-        if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
-    // a read-sharded job hashes every id of its shard (12.5 M at config 3): spread over threads
-    auto run = [=](uint64_t a, uint64_t e) {
-        for (uint64_t i = a; i < e; ++i) {
-            const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
-            const uint64_t len = offs[i + 1] - offs[i];
-            out[2 * i] = xxh64(s, len, 0);
-            out[2 * i + 1] = xxh64(s, len, kP5);
-        }
-    };
-    const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
-    const uint64_t per = (n + T - 1) / T;
-    std::vector<std::thread> th;
-    for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
-    run(0, std::min(n, per));
-    for (auto& x : th) x.join();
-    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!offs || (!out && n) || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
+        for (uint64_t i = 0; i < n; ++i)
+            if (offs[i + 1] < offs[i]) return xs::set_error(XS_ERR_ARG, "id offsets must be non-decreasing");
+        // a read-sharded job hashes every id of its shard (12.5 M at config 3): spread over threads
+        auto run = [=](uint64_t a, uint64_t e) {
+            for (uint64_t i = a; i < e; ++i) {
+                const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+                const uint64_t len = offs[i + 1] - offs[i];
+                out[2 * i] = xxh64(s, len, 0);
+                out[2 * i + 1] = xxh64(s, len, kP5);
+            }
+        };
+        const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
+        const uint64_t per = (n + T - 1) / T;
+        std::vector<std::thread> th;
+        for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
+        run(0, std::min(n, per));
+        for (auto& x : th) x.join();
+        return XS_OK;
+    });
 }
 
 int xs_u64_member_mask(const uint64_t* keys, uint64_t n, const uint64_t* set, uint64_t m, uint8_t* out) {
-    if ((n && (!keys || !out)) || (m && !set)) return xs::set_error(XS_ERR_ARG, "null argument");
-    if (!m) {
-        if (n) memset(out, 0, n);
-        return XS_OK;
-    }
-    // open addressing over 2^b >= 2m slots; a slot holds value + 1 (0 = empty) and
-    // the value ~0 is checked apart
-    unsigned b = 1;
-    while ((1ull << b) < 2 * m) ++b;
-    const uint64_t mask = (1ull << b) - 1;
-    std::vector<uint64_t> slot(mask + 1, 0);
-    bool has_max = false;
-    auto mix = [](uint64_t x) { return (x ^ (x >> 31)) * 0x9E3779B97F4A7C15ull; };
-    for (uint64_t j = 0; j < m; ++j) {
-        const uint64_t v = set[j];
-        if (v == ~0ull) {
-            has_max = true;
-            continue;
+    return xs::guard([&]() -> int {
+        if ((n && (!keys || !out)) || (m && !set)) return xs::set_error(XS_ERR_ARG, "null argument");
+        if (!m) {
+            if (n) memset(out, 0, n);
+            return XS_OK;
         }
-        uint64_t h = mix(v) >> (64 - b);
-        while (slot[h] && slot[h] != v + 1) h = (h + 1) & mask;
-        slot[h] = v + 1;
-    }
-    auto run = [&](uint64_t a, uint64_t e) {
-        for (uint64_t i = a; i < e; ++i) {
-            const uint64_t v = keys[i];
-            uint8_t hit = 0;
+        // open addressing over 2^b >= 2m slots; a slot holds value + 1 (0 = empty) and
+        // the value ~0 is checked apart
+        unsigned b = 1;
+        while ((1ull << b) < 2 * m) ++b;
+        const uint64_t mask = (1ull << b) - 1;
+        std::vector<uint64_t> slot(mask + 1, 0);
+        bool has_max = false;
+        auto mix = [](uint64_t x) { return (x ^ (x >> 31)) * 0x9E3779B97F4A7C15ull; };
+        for (uint64_t j = 0; j < m; ++j) {
+            const uint64_t v = set[j];
             if (v == ~0ull) {
-                hit = has_max;
-            } else {
-                uint64_t h = mix(v) >> (64 - b);
-                while (slot[h]) {
-                    if (slot[h] == v + 1) {
-                        hit = 1;
-                        break;
-                    }
-                    h = (h + 1) & mask;
-                }
+                has_max = true;
+                continue;
             }
-            out[i] = hit;
+            uint64_t h = mix(v) >> (64 - b);
+            while (slot[h] && slot[h] != v + 1) h = (h + 1) & mask;
+            slot[h] = v + 1;
         }
-    };
-    const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
-    const uint64_t per = (n + T - 1) / T;
-    std::vector<std::thread> th;
-    for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
-    run(0, std::min(n, per));
-    for (auto& x : th) x.join();
-    return XS_OK;
+        auto run = [&](uint64_t a, uint64_t e) {
+            for (uint64_t i = a; i < e; ++i) {
+                const uint64_t v = keys[i];
+                uint8_t hit = 0;
+                if (v == ~0ull) {
+                    hit = has_max;
+                } else {
+                    uint64_t h = mix(v) >> (64 - b);
+                    while (slot[h]) {
+                        if (slot[h] == v + 1) {
+                            hit = 1;
+                            break;
+                        }
+                        h = (h + 1) & mask;
+                    }
+                }
+                out[i] = hit;
+            }
+        };
+        const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
+        const uint64_t per = (n + T - 1) / T;
+        std::vector<std::thread> th;
+        for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
+        run(0, std::min(n, per));
+        for (auto& x : th) x.join();
+        return XS_OK;
+    });
 }
 
 // *has_dup = 1 when two of the n ids are equal (byte for byte).  Open addressing
 // over a 64-bit FNV-1a of each id; equal hashes are compared in full.
 int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int* has_dup) {
-    if ((!buf && n && offs[n]) || !offs || !has_dup) return xs::set_error(XS_ERR_ARG, "null argument");
-    *has_dup = 0;
-    if (n < 2) return XS_OK;
-    uint64_t cap = 16;
-    while (cap < 2 * n) cap <<= 1;
-    std::vector<uint64_t> slot(cap, ~0ull);  // id index + 1 of the occupant, ~0 = empty
-    std::vector<uint64_t> hv(cap);
-    for (uint64_t i = 0; i < n; ++i) {
-        const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
-        const uint64_t len = offs[i + 1] - offs[i];
-        uint64_t hsh = 1469598103934665603ull;
-        for (uint64_t j = 0; j < len; ++j) hsh = (hsh ^ s[j]) * 1099511628211ull;
-        hsh ^= hsh >> 29;
-        for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
-            if (slot[p] == ~0ull) {
-                slot[p] = i;
-                hv[p] = hsh;
-                break;
-            }
-            if (hv[p] == hsh) {
-                const uint64_t k = slot[p];
-                if (offs[k + 1] - offs[k] == len && memcmp(buf + offs[k], s, len) == 0) {
-                    *has_dup = 1;
-                    return XS_OK;
+    return xs::guard([&]() -> int {
+        if (!offs || !has_dup || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
+        *has_dup = 0;
+        if (n < 2) return XS_OK;
+        uint64_t cap = 16;
+        while (cap < 2 * n) cap <<= 1;
+        std::vector<uint64_t> slot(cap, ~0ull);  // id index + 1 of the occupant, ~0 = empty
+        std::vector<uint64_t> hv(cap);
+        for (uint64_t i = 0; i < n; ++i) {
+            const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+            const uint64_t len = offs[i + 1] - offs[i];
+            uint64_t hsh = 1469598103934665603ull;
+            for (uint64_t j = 0; j < len; ++j) hsh = (hsh ^ s[j]) * 1099511628211ull;
+            hsh ^= hsh >> 29;
+            for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
+                if (slot[p] == ~0ull) {
+                    slot[p] = i;
+                    hv[p] = hsh;
+                    break;
+                }
+                if (hv[p] == hsh) {
+                    const uint64_t k = slot[p];
+                    if (offs[k + 1] - offs[k] == len && memcmp(buf + offs[k], s, len) == 0) {
+                        *has_dup = 1;
+                        return XS_OK;
+                    }
                 }
             }
         }
-    }
-    return XS_OK;
+        return XS_OK;
+    });
 }
