@@ -516,8 +516,7 @@ def main():
     wl.partitioned = args.workload == "genus" and wl.banks[0].probe_path() == XS_PATH_PARTITIONED
     if args.workload in ("species", "multigenus") and wl.banks[0].probe_path() == XS_PATH_PARTITIONED:
         wl.partitioned = "cobs"
-        ck = os.environ.get("XSPECT2_AMD_CP_CK", "2048")
-        wl.kernel = (f"COBS partitioned: cobs_bucket<{wl.k},{wl.rows_per_kmer},{ck}> (hash, bin rows by 2 MiB bank "
+        wl.kernel = (f"COBS partitioned: cobs_bucket<{wl.k},{wl.rows_per_kmer},2048> (hash, bin rows by 2 MiB bank "
                      "partition) -> cobs_lookup (per-XCD L2-resident partition, rows back in entry order) -> "
                      "cobs_resolve (AND per k-mer in LDS, per-read counts)")
         wl.row_bytes = SURVEY_ROW_BYTES
@@ -553,7 +552,7 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu/gpu_pmc_traffic_part.sh, gpu_cp_pmc2.sh)
+    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu/gpu_r05_final.sh -> profiles/r05_traffic.json)
         traffic = None
         try:
             key = "species_partitioned" if wl.partitioned == "cobs" else "genus_partitioned"
