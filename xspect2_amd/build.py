@@ -29,7 +29,7 @@ HEADER_NAMES = ["xs_internal.h", "xs_device.h", "xs_part.h"]
 SOURCES = [CSRC / s for s in SOURCE_NAMES]
 HEADERS = [CSRC / h for h in HEADER_NAMES] + [INCLUDE / "xspect_hip.h"]
 OBJ_DIR = PKG / "_build"
-ARCH = os.environ.get("XSPECT2_AMD_ARCH", "gfx950")
+ARCH = "gfx950"  # MI355X only: the kernels use gfx950 instructions (LDS-DMA dwordx4, v_bitop3)
 ID_TAG = b"xspect2-build-id:"
 
 
