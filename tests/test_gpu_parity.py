@@ -817,6 +817,34 @@ def test_concurrent_handles_from_threads(xs, oracle_mod):
         gb.close()
 
 
+def test_concurrent_large_host_queries_from_threads(xs, oracle_mod):
+    """The same contract on the large-call path: batches of 40 k reads go
+    through query_host (chunked H2D, the hit rows back on each call's own
+    HitSink thread, narrowed and widened) into arrays of the shared host pool
+    (bank._HostPool, its lock), four threads over two handles at once;
+    every matrix equals the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    pairs = [_pair(xs, oracle_mod, D, 21, 7, [sig], seed=D + 1) for D, sig in ((100, 12_007), (60, 9_001))]
+    rng = np.random.default_rng(13)
+    batches = [_reads(rng, 40_000, 21, max_len=200) for _ in range(3)]
+    want = {(i, j): pairs[i][0].query(b) for i in range(len(pairs)) for j, b in enumerate(batches)}
+
+    def job(args):
+        i, j = args
+        h, nk = pairs[i][1].query(batches[j])
+        ok = np.array_equal(h, want[(i, j)][0]) and np.array_equal(nk, want[(i, j)][1])
+        return (i, j), ok, int(h.sum())
+
+    work = [(i, j) for i in range(len(pairs)) for j in range(len(batches))] * 2
+    with ThreadPoolExecutor(4) as pool:
+        for key, ok, s in pool.map(job, work):
+            assert ok, key
+            assert s == int(want[key][0].sum())
+    for _, gb, _, _ in pairs:
+        gb.close()
+
+
 def test_host_batches_staged_in_chunks(xs, oracle_mod):
     """Host batches larger than one staging chunk (8 MiB first, then 32 MiB)
     are copied and probed chunk by chunk, and their hit rows come back through
