@@ -827,8 +827,13 @@ def test_concurrent_large_host_queries_from_threads(xs, oracle_mod):
 
     pairs = [_pair(xs, oracle_mod, D, 21, 7, [sig], seed=D + 1) for D, sig in ((100, 12_007), (60, 9_001))]
     rng = np.random.default_rng(13)
-    batches = [_reads(rng, 40_000, 21, max_len=200) for _ in range(3)]
+    genome = b"".join(pairs[0][2])
+    batches = []
+    for _ in range(3):  # half random reads, half windows of the first bank's documents
+        starts = rng.integers(0, len(genome) - 150, 20_000)
+        batches.append(_reads(rng, 20_000, 21, max_len=200) + [genome[o:o + 150] for o in starts])
     want = {(i, j): pairs[i][0].query(b) for i in range(len(pairs)) for j, b in enumerate(batches)}
+    assert int(want[(0, 0)][0].sum()) > 0
 
     def job(args):
         i, j = args
