@@ -978,8 +978,17 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     const uint8_t* d_seqs = dev ? dev->seqs : b->seqs.as<uint8_t>();
     const uint64_t* d_offs = dev ? dev->offs : b->offs.as<uint64_t>();
     std::vector<uint64_t> rebased(dev ? 0 : n + 1);
+    // whatever way the call ends (an error return included), no H2D copy may still be
+    // reading `rebased` or the caller's reads once it has: the copy stream drains on exit
+    struct DrainOnExit {
+        hipStream_t s = nullptr;
+        ~DrainOnExit() {
+            if (s) (void)hipStreamSynchronize(s);
+        }
+    } drain;
     if (!dev) {
         for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
+        drain.s = b->copy_stream;
         HIPCHK(hipMemcpyAsync(b->offs.p, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
     }
     const int threads = host_threads();
