@@ -387,7 +387,12 @@ def test_config1_classify_species_on_an_assembly(tmp_path, species_dir, genomes,
     fa = tmp_path / "assembly.fna"
     write_fasta(contigs, fa, width=70)
     out = tmp_path / "out" / "result.json"
+    from xspect2_amd.bank import Bank
+    closed = []
+    real_close = Bank.close
+    monkeypatch.setattr(Bank, "close", lambda self: (closed.append(self._h is not None), real_close(self))[1])
     classify.classify_species("Acinetobacter", fa, out)
+    assert closed and closed[0], "classify_species left its bank open"  # released on return, not at GC
     got = json.loads(out.read_text())
 
     ob, names = _oracle_species(oracle_mod, species_dir)

@@ -57,14 +57,17 @@ def classify_genus(model_genus: str, input_path: Path, output_path: Path, step: 
     from .probabilistic_single_filter_model import ProbabilisticSingleFilterModel
 
     model = ProbabilisticSingleFilterModel.load(genus_model_path(model_genus))
-    inputs, out_path = prepare_input_output_paths(Path(input_path))
-    for idx, current in enumerate(inputs):
-        # columnar result: same JSON as ModelResult.save, no per-read dicts
-        result = model.predict_columnar(current, step=step)
-        result.input_source = current.name
-        path = out_path(idx, Path(output_path))
-        result.save(path)
-        print(f"Saved result as {path.name}")
+    try:
+        inputs, out_path = prepare_input_output_paths(Path(input_path))
+        for idx, current in enumerate(inputs):
+            # columnar result: same JSON as ModelResult.save, no per-read dicts
+            result = model.predict_columnar(current, step=step)
+            result.input_source = current.name
+            path = out_path(idx, Path(output_path))
+            result.save(path)
+            print(f"Saved result as {path.name}")
+    finally:
+        model.close()  # the filter's HBM goes back now, not at garbage collection (a serving process)
 
 
 def classify_species(model_genus: str, input_path: Path, output_path: Path, step: int = 1,
@@ -76,19 +79,22 @@ def classify_species(model_genus: str, input_path: Path, output_path: Path, step
     path = species_model_path(model_genus)
     cls = ProbabilisticFilterSVMModel if is_svm_model(path) else ProbabilisticFilterModel
     model = cls.load(path)
-    inputs, out_path = prepare_input_output_paths(Path(input_path))
-    for idx, current in enumerate(inputs):
-        if validation:
-            result = model.predict(current, exclude_ids=exclude_ids, step=step,
-                                   display_name=display_name, validation=validation)
-        else:
-            # columnar result: same JSON as ModelResult.save, no per-read dicts
-            result = model.predict_columnar(current, exclude_ids=exclude_ids, step=step,
-                                            display_name=display_name)
-        result.input_source = current.name
-        path_out = out_path(idx, Path(output_path))
-        result.save(path_out)
-        print(f"Saved result as {path_out.name}")
+    try:
+        inputs, out_path = prepare_input_output_paths(Path(input_path))
+        for idx, current in enumerate(inputs):
+            if validation:
+                result = model.predict(current, exclude_ids=exclude_ids, step=step,
+                                       display_name=display_name, validation=validation)
+            else:
+                # columnar result: same JSON as ModelResult.save, no per-read dicts
+                result = model.predict_columnar(current, exclude_ids=exclude_ids, step=step,
+                                                display_name=display_name)
+            result.input_source = current.name
+            path_out = out_path(idx, Path(output_path))
+            result.save(path_out)
+            print(f"Saved result as {path_out.name}")
+    finally:
+        model.close()
 
 
 def classify_species_sharded(model_genus: str, input_path: Path, output_path: Path, step: int = 1,
@@ -107,14 +113,16 @@ def classify_species_sharded(model_genus: str, input_path: Path, output_path: Pa
     path = species_model_path(model_genus)
     cls = ProbabilisticFilterSVMModel if is_svm_model(path) else ProbabilisticFilterModel
     model = cls.load(path)
-    inputs, out_path = prepare_input_output_paths(Path(input_path))
-    outs = []
-    for idx, current in enumerate(inputs):
-        target = out_path(idx, Path(output_path))
-        distributed.classify_species_sharded(model, current, target, step=step, display_name=display_name,
-                                             exclude_ids=exclude_ids)
-        outs.append(target)
-    model.close()
+    try:
+        inputs, out_path = prepare_input_output_paths(Path(input_path))
+        outs = []
+        for idx, current in enumerate(inputs):
+            target = out_path(idx, Path(output_path))
+            distributed.classify_species_sharded(model, current, target, step=step, display_name=display_name,
+                                                 exclude_ids=exclude_ids)
+            outs.append(target)
+    finally:
+        model.close()
     return outs
 
 
@@ -123,13 +131,16 @@ def classify_mlst(input_path: Path, organism: str, mlst_scheme: str, output_path
     from .probabilistic_filter_mlst_model import ProbabilisticFilterMlstSchemeModel
 
     model = ProbabilisticFilterMlstSchemeModel.load(mlst_model_path(organism, mlst_scheme))
-    inputs, out_path = prepare_input_output_paths(Path(input_path))
-    for idx, current in enumerate(inputs):
-        result = model.predict(current, step=1, limit=limit)
-        result.input_source = current.name
-        path = out_path(idx, Path(output_path))
-        result.save(path)
-        print(f"Saved result as {path.name}")
+    try:
+        inputs, out_path = prepare_input_output_paths(Path(input_path))
+        for idx, current in enumerate(inputs):
+            result = model.predict(current, step=1, limit=limit)
+            result.input_source = current.name
+            path = out_path(idx, Path(output_path))
+            result.save(path)
+            print(f"Saved result as {path.name}")
+    finally:
+        model.close()
 
 
 def classify_pipeline(model_genus: str, input_path: Path, output_dir: Path | None = None, threshold: float = 0.7,
@@ -156,5 +167,10 @@ def classify_pipeline(model_genus: str, input_path: Path, output_dir: Path | Non
         p = mlst_model_path("abaumannii", mlst_scheme)
         if p.exists():
             mlst = ProbabilisticFilterMlstSchemeModel.load(p)
-    return run_pipeline(genus, species, Path(input_path), output_dir, threshold, sparse_sampling_step,
-                        display_names, mlst=mlst)
+    try:
+        return run_pipeline(genus, species, Path(input_path), output_dir, threshold, sparse_sampling_step,
+                            display_names, mlst=mlst)
+    finally:
+        for m in (genus, species, mlst):
+            if m is not None:
+                m.close()
