@@ -60,10 +60,3 @@ def make_reads(genomes: np.ndarray, n_reads: int, read_len: int = 150, seed: int
     src = sp.astype(np.int32)
     src[ridx] = -1
     return reads, src
-
-
-def random_seqs(rng: np.random.Generator, n: int, min_len: int, max_len: int,
-                alphabet: bytes = b"ACGT") -> list[bytes]:
-    alph = np.frombuffer(alphabet, dtype=np.uint8)
-    lens = rng.integers(min_len, max_len + 1, n)
-    return [alph[rng.integers(0, alph.size, int(L))].tobytes() for L in lens]
