@@ -519,11 +519,11 @@ static int cached_grid(std::atomic<int>& slot, F compute) {
     return v;
 }
 
-static int kh_variant(uint32_t k, uint32_t h) { return (k == 21 && h == 7) ? 0 : (k == 31 && h == 1) ? 1 : 2; }
+inline int kh_variant(uint32_t k, uint32_t h) { return (k == 21 && h == 7) ? 0 : (k == 31 && h == 1) ? 1 : 2; }
 
 
 // Bytes of the per-block doc totals (u64) the multi-chunk COBS kernels keep in LDS.
-static size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128 * 128) * sizeof(uint64_t); }
+inline size_t slots_lds(const CobsView& bv) { return (size_t)((bv.D + 127) / 128 * 128) * sizeof(uint64_t); }
 
 // ---- COBS probe families (one translation unit each) ---------------------
 // xs_probe_fast.hip: classic D <= 128, species (21, 7) / MLST (31, 1)
