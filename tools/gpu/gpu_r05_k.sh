@@ -17,3 +17,5 @@ for f in ("species", "species_rccl1"):
     r = d["roofline"]
     print(f, d["value"], d["ms_per_step"], d["checks"]["ok"], r["frac"], r.get("traffic_frac"), (r.get("lookup_l2") or {}).get("frac"), (r.get("lookup_l2") or {}).get("kernel"))
 PY
+# host only: first-touch cost with and without transparent huge pages (tools/thp_probe.py)
+timeout -k 10 120 python3 tools/thp_probe.py > gpurun_out/r05k/thp.json && cat gpurun_out/r05k/thp.json
