@@ -21,6 +21,7 @@
 #include "../../include/xspect_hip.h"
 
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -136,6 +137,21 @@ void par_memcpy(void* dst, const void* src, size_t n, int threads) {
     }
     memcpy(dst, src, std::min(per, n));
     for (auto& x : th) x.join();
+}
+
+// Ask for transparent huge pages over the page-aligned part of a pageable
+// host destination the library is about to fill.  On the MI355X boxes the
+// first write to fresh 4 KiB pages costs ~70 ms per 400 MB from one thread and
+// ~34 ms from eight (the faults serialise); over 2 MiB pages it is ~25 ms from
+// one thread and ~3.6 ms from eight (profiles/r05k_thp.json,
+// tools/thp_probe.py), and the copy-out already writes from eight threads.
+// Advisory only: pages already present stay as they are, and a mapping that
+// cannot take the advice (file-backed, hugetlbfs) is left alone.
+void advise_huge_pages(void* p, size_t bytes) {
+    constexpr uintptr_t kPage = 4096;
+    const uintptr_t a = (reinterpret_cast<uintptr_t>(p) + kPage - 1) & ~(kPage - 1);
+    const uintptr_t e = (reinterpret_cast<uintptr_t>(p) + bytes) & ~(kPage - 1);
+    if (e > a + (4u << 20)) (void)madvise(reinterpret_cast<void*>(a), e - a, MADV_HUGEPAGE);
 }
 
 }  // namespace
@@ -755,11 +771,13 @@ class HitSink {
         } else if (wire_ == out_) {
             direct_ = true;  // small: one DMA into pageable memory is as fast as staging it
         }
-        if (!direct_)
+        if (!direct_) {  // a pageable destination, filled by the copy-out threads
+            advise_huge_pages(host_, total_bytes_out);
             for (int s = 0; s < kSinkSlots; ++s) {
                 if (int rc = b_->stage[s].ensure(kSinkPiece)) return rc;
                 if (!b_->stage_ev[s]) HIPCHK(hipEventCreateWithFlags(&b_->stage_ev[s], hipEventDisableTiming));
             }
+        }
         th_ = std::thread([this] { run(); });
         return XS_OK;
     }
