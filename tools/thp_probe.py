@@ -55,6 +55,25 @@ def case(nbytes: int, huge: bool, threads: int) -> dict:
     return {"first_touch_ms": min(firsts), "rewrite_ms": min(seconds)}
 
 
+def case_numpy(nbytes: int, threads: int) -> dict:
+    """The same on an np.empty array (glibc's mmap'd chunk: page aligned plus a
+    16-byte header), advised from its first whole page, as HitSink does."""
+    import numpy as np
+    firsts, seconds = [], []
+    for _ in range(3):
+        arr = np.empty(nbytes, np.uint8)
+        p = arr.ctypes.data
+        a = (p + 4095) & ~4095
+        e = (p + nbytes) & ~4095
+        rc = libc.madvise(a, e - a, MADV_HUGEPAGE)
+        if rc != 0:
+            return {"error": f"madvise errno {ctypes.get_errno()}"}
+        firsts.append(_fill(p, nbytes, threads))
+        seconds.append(_fill(p, nbytes, threads))
+        del arr
+    return {"first_touch_ms": min(firsts), "rewrite_ms": min(seconds), "addr_mod_2MiB": p % (2 << 20)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mb", type=int, default=400)
@@ -68,6 +87,7 @@ def main():
     for huge in (False, True):
         for t in (1, 8):
             out[f"{'huge' if huge else 'plain'}_t{t}"] = case(n, huge, t)
+    out["numpy_huge_t8"] = case_numpy(n, 8)
     print(json.dumps(out), flush=True)
 
 
