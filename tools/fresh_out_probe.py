@@ -78,6 +78,17 @@ def main():
         huge.append(anon_huge_kb() - h0)
         del a
     out["fresh_ms"], out["fresh_anon_huge_kb"] = min(fresh), huge
+    cyc, frees = [], []
+    for _ in range(3):  # as bench.py's leg: allocate, query, drop (the unmap inside the time)
+        t0 = time.perf_counter()
+        a = np.empty(shape, np.uint32)
+        bank.query(pr, out=a)
+        t1 = time.perf_counter()
+        del a
+        t2 = time.perf_counter()
+        cyc.append((t2 - t0) * 1e3)
+        frees.append((t2 - t1) * 1e3)
+    out["fresh_cycle_ms"], out["free_ms"] = cyc, frees
     pre, q = [], []
     for _ in range(3):
         a = np.empty(shape, np.uint32)
