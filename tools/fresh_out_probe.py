@@ -100,6 +100,16 @@ def main():
     h0 = anon_huge_kb()
     out["touch8_alone_ms"] = touch8(a)
     out["touch8_anon_huge_kb"] = anon_huge_kb() - h0
+    t0 = time.perf_counter()
+    del a
+    out["free_after_touch8_ms"] = (time.perf_counter() - t0) * 1e3
+    a = np.empty(shape, np.uint32)
+    t0 = time.perf_counter()
+    libc.memset(a.ctypes.data, 0, a.nbytes)
+    out["touch1_ms"] = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    del a
+    out["free_after_touch1_ms"] = (time.perf_counter() - t0) * 1e3
     print(json.dumps(out), flush=True)
     bank.close()
 
