@@ -876,23 +876,32 @@ def host_path(wl, args, reps=3):
                      ("totals", lambda b: b.query_totals(pr, step=args.step))):
         for b in wl.banks:  # warm
             fn(b)
-        t = time.perf_counter()
+        dt, release = 0.0, 0.0
         for _ in range(reps):
             for b in wl.banks:
-                fn(b)
-        dt = (time.perf_counter() - t) / reps
+                t = time.perf_counter()
+                res = fn(b)
+                t1 = time.perf_counter()
+                del res  # the caller dropping its result: timed apart (a fresh array's unmap)
+                dt += t1 - t
+                release += time.perf_counter() - t1
+        dt, release = dt / reps, release / reps
         out[name] = {"ms_per_step": dt * 1e3}
         if not name.startswith("first_touch"):
             out[name]["probes_per_s"] = wl.probes_per_step() / wl.world / dt
+        if name == "hits_u32_fresh_pageable":
+            out[name]["release_ms_per_step"] = release * 1e3
     out["hit_dtype"] = np.dtype(hdt).name
     out["note"] = ("per GPU, reads from pageable host memory: H2D + probe + D2H.  hits: the n x D matrix in "
                    f"{np.dtype(hdt).name} (narrowed on the device; counts <= k-mers per read) into a reused pinned "
                    "buffer (xs_query_hits); hits_u32_pageable: Bank.query's default, xs_query's uint32 matrix into "
                    "a pageable array from the recycled host pool (bank._HostPool: pages faulted once), the rows "
                    "crossing PCIe as uint8 and widened on the host behind the probe; hits_u32_fresh_pageable: the "
-                   "same into a never-touched np.empty array, which adds the OS's first-touch faults, measured "
-                   "alone as first_touch_u32_matrix (no probe); totals: D+1 counters.  The headline value starts "
-                   "with the reads in HBM")
+                   "same into a never-touched np.empty array allocated inside the time, which adds the OS's "
+                   "first-touch faults (taken as 2 MiB pages by the copy-out's 8 threads), the array's release "
+                   "(the OS unmapping it when the caller drops it) timed apart as release_ms_per_step; "
+                   "first_touch_u32_matrix: allocate, one write per 4 KiB page from one thread and release, no "
+                   "probe; totals: D+1 counters.  The headline value starts with the reads in HBM")
     return out
 
 
