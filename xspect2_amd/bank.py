@@ -91,10 +91,11 @@ def pinned_empty(shape, dtype=np.uint32) -> np.ndarray:
 class _HostPool:
     """Recycled pageable host blocks for the arrays Bank.query returns.
 
-    The first write to fresh pageable memory faults every page, and on the
-    MI355X boxes those faults neither batch nor spread over threads: 400 MB
-    (config 2's uint32 hit matrix) costs ~28 ms of first touch, more than the
-    whole query (profiles/r05_host_out.json).  So result arrays are views of
+    A fresh pageable array costs its pages twice: faulting them in on the
+    first write (cheap inside the call now: the copy-out's eight threads take
+    2 MiB pages, +0.5 ms per 400 MB) and unmapping them when the caller drops
+    the array (14-23 ms per 400 MB on the MI355X boxes, more than the query's
+    17 ms; profiles/r05m_fresh_out.json).  So result arrays are views of
     blocks kept here; a block goes back into service once no array refers to
     it any more (every numpy view of a block holds the block itself as its
     base, so the block's reference count says whether one is alive), and a
