@@ -21,6 +21,12 @@ int set_error(int code, const char* msg) {  // the library's version lives in xs
     (void)msg;
     return code;
 }
+// likewise (xs_api.cpp pins host memory; no GPU here, so plain host memory)
+int pinned_alloc(size_t bytes, void** out) {
+    *out = malloc(bytes ? bytes : 1);
+    return *out ? 0 : -6;
+}
+void pinned_free(void* p) { free(p); }
 }  // namespace xs
 extern "C" const char* xs_last_error(void) { return ""; }  // likewise
 

@@ -34,6 +34,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "xs_internal.h"
@@ -109,17 +110,14 @@ struct PinnedBuf {
     size_t cap = 0;
     int ensure(size_t bytes) {
         if (bytes <= cap && p) return XS_OK;
-        if (p) (void)hipHostFree(p);
+        xs::pinned_free(p);
         p = nullptr;
         cap = 0;
-        hipError_t e = hipHostMalloc(&p, bytes, hipHostMallocDefault);
-        if (e != hipSuccess) return fail(XS_ERR_HIP, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+        if (int rc = xs::pinned_alloc(bytes, &p)) return rc;
         cap = bytes;
         return XS_OK;
     }
-    ~PinnedBuf() {
-        if (p) (void)hipHostFree(p);
-    }
+    ~PinnedBuf() { xs::pinned_free(p); }
 };
 
 // memcpy on up to `threads` host threads.
@@ -1216,6 +1214,70 @@ int xs::set_error(int code, const char* msg) {
     return code;
 }
 
+namespace {
+std::mutex g_pin_mu;
+std::unordered_map<void*, size_t> g_pins;  // registered mappings: start -> length
+}  // namespace
+
+int xs::pinned_alloc(size_t bytes, void** out) {
+    *out = nullptr;
+    constexpr size_t kHuge = size_t(2) << 20;
+    const size_t n = (std::max<size_t>(bytes, 1) + kHuge - 1) & ~(kHuge - 1);
+    if (bytes >= kHuge) {
+        const size_t len = n + kHuge;  // room to align the start to a 2 MiB page
+        void* raw = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (raw != MAP_FAILED) {
+            char* r = static_cast<char*>(raw);
+            char* p = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(r) + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+            if (p > r) (void)munmap(r, (size_t)(p - r));           // the unaligned head
+            if (r + len > p + n) (void)munmap(p + n, (size_t)(r + len - (p + n)));  // and tail
+            (void)madvise(p, n, MADV_HUGEPAGE);
+            // fault every page now, from several threads (2 MiB pages fault in parallel; the
+            // registration below would otherwise fault them one by one)
+            const int threads = (int)std::min<size_t>(8, std::max<size_t>(1, n / (size_t(16) << 20)));
+            const size_t per = (n / kHuge + threads - 1) / threads * kHuge;
+            std::vector<std::thread> th;
+            for (int t = 1; t < threads && per * t < n; ++t)
+                th.emplace_back([=] { memset(p + per * t, 0, std::min(per, n - per * t)); });
+            memset(p, 0, std::min(per, n));
+            for (auto& x : th) x.join();
+            if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess) {
+                std::lock_guard<std::mutex> g(g_pin_mu);
+                g_pins[p] = n;
+                *out = p;
+                return XS_OK;
+            }
+            (void)hipGetLastError();
+            (void)munmap(p, n);
+        }
+    }
+    const hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) {
+        *out = nullptr;
+        return fail(XS_ERR_HIP, "hipHostMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    }
+    return XS_OK;
+}
+
+void xs::pinned_free(void* p) {
+    if (!p) return;
+    size_t n = 0;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        auto it = g_pins.find(p);
+        if (it != g_pins.end()) {
+            n = it->second;
+            g_pins.erase(it);
+        }
+    }
+    if (n) {
+        (void)hipHostUnregister(p);
+        (void)munmap(p, n);
+    } else {
+        (void)hipHostFree(p);
+    }
+}
+
 extern "C" {
 
 int xs_version(void) { return 100; }
@@ -1641,20 +1703,12 @@ int xs_memcpy_device(void* dst, const void* src, uint64_t bytes, void* stream) {
 int xs_host_alloc(uint64_t bytes, void** out) {
     return xs::guard([&]() -> int {
         if (!out) return fail(XS_ERR_ARG, "null argument");
-        *out = nullptr;
-        hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
-        if (e != hipSuccess) {
-            *out = nullptr;
-            return fail(XS_ERR_HIP, "hipHostMalloc(%llu) failed: %s", (unsigned long long)bytes, hipGetErrorString(e));
-        }
-        return XS_OK;
+        return xs::pinned_alloc(bytes, out);
     });
 }
 
 void xs_host_free(void* p) {
-    xs::guard([&] {
-        if (p) (void)hipHostFree(p);
-    });
+    xs::guard([&] { xs::pinned_free(p); });
 }
 
 int xs_query_best(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,

@@ -88,9 +88,9 @@ struct HostBuf {
         release();
         size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
         if (pinned) {
-            if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
+            if (xs::pinned_alloc(want, reinterpret_cast<void**>(&p)) != XS_OK) {
                 p = nullptr;
-                return xs::set_error(XS_ERR_HIP, "hipHostMalloc failed for the reader's batch buffer");
+                return xs::set_error(XS_ERR_HIP, "pinned allocation failed for the reader's batch buffer");
             }
         } else {
             p = static_cast<char*>(malloc(want));
@@ -101,7 +101,7 @@ struct HostBuf {
     }
     void release() {
         if (p) {
-            if (pinned) (void)hipHostFree(p);
+            if (pinned) xs::pinned_free(p);
             else free(p);
         }
         p = nullptr;
@@ -361,7 +361,7 @@ struct Batch {
 bool fx_trace();
 double fx_ms();
 // Pinned host and device buffers outlive their reader in a process-wide pool:
-// a hipHostMalloc of a few MiB costs milliseconds and a hipFree synchronises
+// pinning host memory costs (xs::pinned_alloc) and a hipFree synchronises
 // the device, so a reader per input file would otherwise pay more for its
 // buffers than for its parse.  Reuse takes the smallest pooled buffer that
 // fits and is at most 4x the request.
@@ -412,9 +412,9 @@ struct PinBuf {
         if ((p = static_cast<char*>(g_pool.take(bytes, -1, &cap)))) return XS_OK;
         const size_t want = std::max<size_t>(exact ? bytes : bytes + bytes / 8, 1 << 16);
         const double t0 = fx_ms();
-        if (hipHostMalloc(reinterpret_cast<void**>(&p), want, hipHostMallocDefault) != hipSuccess) {
+        if (xs::pinned_alloc(want, reinterpret_cast<void**>(&p)) != XS_OK) {
             p = nullptr;
-            return xs::set_error(XS_ERR_HIP, "hipHostMalloc failed for the device reader");
+            return xs::set_error(XS_ERR_HIP, "pinned allocation failed for the device reader");
         }
         if (fx_trace()) fprintf(stderr, "[fastx-device] pinned %zu B in %.2f ms\n", want, fx_ms() - t0);
         cap = want;
@@ -423,7 +423,7 @@ struct PinBuf {
     void release() {
         if (p && !g_pool.give(p, cap, -1)) {
             if (fx_trace()) fprintf(stderr, "[fastx-device] unpinned %zu B\n", cap);
-            (void)hipHostFree(p);
+            xs::pinned_free(p);
         }
         p = nullptr;
         cap = 0;
@@ -489,9 +489,10 @@ struct DevSide {
     hipEvent_t kern_ev = nullptr;                // a batch's device data complete
     hipEvent_t host_ev[2] = {nullptr, nullptr};  // slot s's host arrays complete
     // Window text goes to HBM through a ring of pinned pieces (ring_pieces()
-    // x kPieceBytes): pinning costs ~0.19 ms per MiB (hipHostMalloc), so
-    // whole-window pinned buffers (two of up to 288 MiB) cost tens of ms on a
-    // process's first file; the ring is 128 MiB whatever the window.
+    // x kPieceBytes): pinning cost ~0.19 ms per MiB with hipHostMalloc (~0.02
+    // with xs::pinned_alloc's registered 2 MiB pages), and whole-window pinned
+    // buffers (two of up to 288 MiB) are more than a window needs at once; the
+    // ring is 128 MiB whatever the window.
     PinBuf ring;
     PinBuf pin[2];                     // XSPECT2_AMD_FX_RING=0: a window's whole text per slot
     hipEvent_t ring_ev[kRingMax] = {};  // the DMA out of ring piece r done (recorded on `copy`)

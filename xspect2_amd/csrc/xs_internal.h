@@ -258,6 +258,17 @@ hipError_t launch_max_u64(void* temp, size_t temp_bytes, const uint64_t* in, uin
 // Set the thread-local message xs_last_error() returns; returns `code`.
 int set_error(int code, const char* msg);
 
+// Page-locked host memory for DMA staging and callers' outputs.  Requests of
+// 2 MiB and more are anonymous mappings backed by 2 MiB pages, faulted by up
+// to 8 threads and registered with HIP (hipHostRegister): 2.2 ms per 128 MiB
+// against 22.5 ms for hipHostMalloc on the MI355X boxes, at the same DMA rate
+// (profiles/r05o_pin.json, tools/pin_probe.py).  Smaller requests, and any
+// mapping HIP refuses to register, take hipHostMalloc.  Memory from
+// pinned_alloc goes back through pinned_free only.  Contents start zeroed for
+// the mapped kind, unspecified for the hipHostMalloc kind.
+int pinned_alloc(size_t bytes, void** out);
+void pinned_free(void* p);
+
 // Every C-ABI entry point runs its body under guard(): a C++ exception (a
 // host vector that cannot be allocated, a worker thread that cannot start)
 // becomes XS_ERR_NOMEM / XS_ERR_INTERNAL and a message instead of unwinding
