@@ -20,11 +20,14 @@
 // (128 docs each) and never straddles a 128-byte line.
 #include "../../include/xspect_hip.h"
 
+#include <fcntl.h>
 #include <hip/hip_runtime.h>
 #include <sys/mman.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -99,6 +102,12 @@ struct DevBuf {
     }
     template <class T>
     T* as() const { return static_cast<T*>(p); }
+    // give the memory back now (the caller has synchronised every stream that used it)
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
     ~DevBuf() {
         if (p) (void)hipFree(p);
     }
@@ -357,6 +366,98 @@ int download_payload(xs_bank* b, void* host, uint64_t nbytes) {
                              b->sig_total(), b->page, b->stream));
         HIPCHK(hipMemcpyAsync(host, b->tmp.p, nbytes, hipMemcpyDeviceToHost, b->stream));
     }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+// ---- bank payloads straight from their files ------------------------------
+// A model load (ProbabilisticFilterModel.load, probabilistic_filter_model.py:
+// 351-391: cobs.Search(path) reads the whole index) moved the payload through
+// a zero-filled std::vector, one ifstream read and a pageable H2D copy: 169 ms
+// for config 2's 0.5 GB file (2.9 GB/s, profiles/r05q_open.json).  Here the
+// file is read in pieces by up to 8 threads (pread) into a ring of pinned
+// slots, each piece sent by DMA while the next is read.
+constexpr uint64_t kLoadPiece = 32u << 20;
+constexpr int kLoadSlots = 3;
+
+// [off, off + n) of fd into dst, split over up to `threads` threads; false on a
+// read error or a short file
+bool pread_all(int fd, uint8_t* dst, uint64_t n, uint64_t off, int threads) {
+    auto run = [=](uint64_t a, uint64_t e, bool* ok) {
+        while (a < e) {
+            const ssize_t got = pread(fd, dst + a, (size_t)(e - a), (off_t)(off + a));
+            if (got <= 0) {
+                if (got < 0 && errno == EINTR) continue;
+                *ok = false;
+                return;
+            }
+            a += (uint64_t)got;
+        }
+        *ok = true;
+    };
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n / (4u << 20)));
+    const uint64_t per = (n + T - 1) / T;
+    std::vector<std::thread> th;
+    bool ok[8] = {true, true, true, true, true, true, true, true};
+    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)), &ok[t]);
+    run(0, std::min(n, per), &ok[0]);
+    for (auto& x : th) x.join();
+    for (bool o : ok)
+        if (!o) return false;
+    return true;
+}
+
+// nbytes of `path` from byte `pos` to the device at dst, on b->stream (synchronised on return)
+int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, uint8_t* dst) {
+    const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return fail(XS_ERR_IO, "cannot open %s", path);
+    struct Closer {
+        int fd;
+        ~Closer() { ::close(fd); }
+    } closer{fd};
+    PinnedBuf ring[kLoadSlots];
+    hipEvent_t ev[kLoadSlots] = {};
+    // on every exit path: no DMA may still read a slot when the ring is freed
+    struct Drain {
+        hipStream_t s;
+        hipEvent_t* ev;
+        ~Drain() {
+            (void)hipStreamSynchronize(s);
+            for (int i = 0; i < kLoadSlots; ++i)
+                if (ev[i]) (void)hipEventDestroy(ev[i]);
+        }
+    } drain{b->stream, ev};
+    const uint64_t piece = std::min<uint64_t>(kLoadPiece, std::max<uint64_t>(nbytes, 1));
+    for (int i = 0; i < kLoadSlots; ++i) {
+        if (int rc = ring[i].ensure(piece)) return rc;
+        HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    }
+    const int threads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    uint64_t i = 0;
+    for (uint64_t off = 0; off < nbytes; off += piece, ++i) {
+        const int s = (int)(i % kLoadSlots);
+        if (i >= (uint64_t)kLoadSlots) HIPCHK(hipEventSynchronize(ev[s]));  // the slot's last DMA is done
+        const uint64_t m = std::min(piece, nbytes - off);
+        if (!pread_all(fd, static_cast<uint8_t*>(ring[s].p), m, pos + off, threads))
+            return fail(XS_ERR_IO, "%s: short read", path);
+        HIPCHK(hipMemcpyAsync(dst + off, ring[s].p, m, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(hipEventRecord(ev[s], b->stream));
+    }
+    HIPCHK(hipStreamSynchronize(b->stream));
+    return XS_OK;
+}
+
+// The bank's payload (the file's bytes after the header, at `pos`) into its image.
+int upload_file_payload(xs_bank* b, const char* path, uint64_t pos) {
+    const uint64_t nbytes = b->payload_bytes();
+    HIPCHK(hipSetDevice(b->device));
+    if (int rc = ws_enter(b, b->stream)) return rc;
+    if (b->kind == XS_BANK_RBLOOM || b->pitch == b->page)
+        return stream_file_to_device(b, path, pos, nbytes, b->image.as<uint8_t>());
+    if (int rc = b->tmp.ensure(nbytes)) return rc;
+    if (int rc = stream_file_to_device(b, path, pos, nbytes, b->tmp.as<uint8_t>())) return rc;
+    HIPCHK(launch_repack(b->tmp.as<uint8_t>(), b->page, b->image.as<uint8_t>(), b->pitch, b->sig_total(), b->page,
+                         b->stream));
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
 }
@@ -1335,12 +1436,7 @@ int xs_bank_open(const char* path, int kind, int device, xs_bank** out) {
                           (unsigned long long)(fsize - pos), (unsigned long long)b->payload_bytes());
         }
         if (rc == XS_OK) rc = alloc_image(b);
-        if (rc == XS_OK) {
-            std::vector<uint8_t> payload(b->payload_bytes());
-            rd.f.read(reinterpret_cast<char*>(payload.data()), (std::streamsize)payload.size());
-            if (!rd.f) rc = fail(XS_ERR_IO, "%s: short read", path);
-            else rc = upload_payload(b, payload.data(), payload.size());
-        }
+        if (rc == XS_OK) rc = upload_file_payload(b, path, (uint64_t)rd.f.tellg());
         if (rc != XS_OK) {
             delete b;
             return rc;
@@ -1383,18 +1479,15 @@ int xs_bank_open_docs(const char* path, int device, uint64_t doc_lo, uint64_t do
         b->names.assign(full->names.begin() + (ptrdiff_t)doc_lo, full->names.begin() + (ptrdiff_t)doc_hi);
         if (int rc = validate_geometry(b)) return rc;
         if (int rc = alloc_image(b)) return rc;
-        // the rows' byte columns [doc_lo / 8, + page), read in pieces of rows
+        // whole rows to the device, then the rows' byte columns [doc_lo / 8, + page) into the image
         const uint64_t c0 = doc_lo / 8, P = b->page;
-        std::vector<uint8_t> payload(S * P);
-        constexpr uint64_t kRows = 1u << 20;
-        std::vector<uint8_t> piece(std::min(S, kRows) * R);
-        for (uint64_t r0 = 0; r0 < S; r0 += kRows) {
-            const uint64_t m = std::min(kRows, S - r0);
-            rd.f.read(reinterpret_cast<char*>(piece.data()), (std::streamsize)(m * R));
-            if (!rd.f) return fail(XS_ERR_IO, "%s: short read", path);
-            for (uint64_t r = 0; r < m; ++r) memcpy(payload.data() + (r0 + r) * P, piece.data() + r * R + c0, P);
-        }
-        if (int rc = upload_payload(b, payload.data(), payload.size())) return rc;
+        HIPCHK(hipSetDevice(b->device));
+        if (int rc = ws_enter(b, b->stream)) return rc;
+        if (int rc = b->tmp.ensure(S * R)) return rc;
+        if (int rc = stream_file_to_device(b, path, pos, S * R, b->tmp.as<uint8_t>())) return rc;
+        HIPCHK(launch_repack(b->tmp.as<uint8_t>() + c0, R, b->image.as<uint8_t>(), b->pitch, S, P, b->stream));
+        HIPCHK(hipStreamSynchronize(b->stream));
+        b->tmp.release();  // the whole rows (all docs) are not kept beside the slice
         *out = keep.release();
         return XS_OK;
     });
