@@ -1,7 +1,7 @@
 """Model-load time (ProbabilisticFilterModel.load reads the
 COBS index, 0.5-1 GB, once per `xspect classify` process): config 2's
 D=100 species bank (0.61 GB) saved as a COBS classic file, then
-Bank.open(path) timed with the file in the page cache, best and all of
+Bank.save (3 times) and Bank.open(path) timed with the file in the page cache, best and all of
 --reps; the opened bank's image is checked against the saved one.  One
 JSON line.
 """
@@ -41,7 +41,11 @@ def main():
     torch.cuda.synchronize(dev)
     del g
     path = Path(a.path)
-    bank.save(path)
+    saves = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        bank.save(path)
+        saves.append((time.perf_counter() - t0) * 1e3)
     want = bank.download()
     bank.close()
     times = []
@@ -55,7 +59,7 @@ def main():
             raise SystemExit("opened bank differs from the saved one")
     size = path.stat().st_size
     path.unlink()
-    print(json.dumps({"file_bytes": size, "open_ms": times, "best_ms": min(times),
+    print(json.dumps({"file_bytes": size, "save_ms": saves, "open_ms": times, "best_ms": min(times),
                       "GBps": size / (min(times) * 1e-3) / 1e9, "image_equal": True}), flush=True)
 
 

@@ -447,6 +447,91 @@ int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t n
     return XS_OK;
 }
 
+// [off, off + n) of fd from src, split over up to `threads` threads; false on a write error
+bool pwrite_all(int fd, const uint8_t* src, uint64_t n, uint64_t off, int threads) {
+    auto run = [=](uint64_t a, uint64_t e, bool* ok) {
+        while (a < e) {
+            const ssize_t put = pwrite(fd, src + a, (size_t)(e - a), (off_t)(off + a));
+            if (put <= 0) {
+                if (put < 0 && errno == EINTR) continue;
+                *ok = false;
+                return;
+            }
+            a += (uint64_t)put;
+        }
+        *ok = true;
+    };
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n / (4u << 20)));
+    const uint64_t per = (n + T - 1) / T;
+    std::vector<std::thread> th;
+    bool ok[8] = {true, true, true, true, true, true, true, true};
+    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)), &ok[t]);
+    run(0, std::min(n, per), &ok[0]);
+    for (auto& x : th) x.join();
+    for (bool o : ok)
+        if (!o) return false;
+    return true;
+}
+
+// nbytes of the device buffer src to `path` from byte `pos` (the header before it is
+// already written): pieces come back by DMA into a ring of pinned slots and are written
+// by up to 8 threads while the next pieces cross
+int stream_device_to_file(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, const uint8_t* src) {
+    const int fd = ::open(path, O_WRONLY | O_CLOEXEC);
+    if (fd < 0) return fail(XS_ERR_IO, "cannot open %s for writing", path);
+    struct Closer {
+        int fd;
+        ~Closer() { ::close(fd); }
+    } closer{fd};
+    PinnedBuf ring[kLoadSlots];
+    hipEvent_t ev[kLoadSlots] = {};
+    struct Drain {  // on every exit path: no DMA may still write a slot when the ring is freed
+        hipStream_t s;
+        hipEvent_t* ev;
+        ~Drain() {
+            (void)hipStreamSynchronize(s);
+            for (int i = 0; i < kLoadSlots; ++i)
+                if (ev[i]) (void)hipEventDestroy(ev[i]);
+        }
+    } drain{b->stream, ev};
+    const uint64_t piece = std::min<uint64_t>(kLoadPiece, std::max<uint64_t>(nbytes, 1));
+    for (int i = 0; i < kLoadSlots; ++i) {
+        if (int rc = ring[i].ensure(piece)) return rc;
+        HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    }
+    const int threads = (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const uint64_t pieces = (nbytes + piece - 1) / piece;
+    auto queue = [&](uint64_t i) -> hipError_t {
+        const int s = (int)(i % kLoadSlots);
+        const uint64_t off = i * piece, m = std::min(piece, nbytes - off);
+        hipError_t e = hipMemcpyAsync(ring[s].p, src + off, m, hipMemcpyDeviceToHost, b->stream);
+        return e == hipSuccess ? hipEventRecord(ev[s], b->stream) : e;
+    };
+    for (uint64_t i = 0; i < std::min<uint64_t>(pieces, kLoadSlots); ++i) HIPCHK(queue(i));
+    for (uint64_t i = 0; i < pieces; ++i) {
+        const int s = (int)(i % kLoadSlots);
+        HIPCHK(hipEventSynchronize(ev[s]));
+        const uint64_t off = i * piece, m = std::min(piece, nbytes - off);
+        if (!pwrite_all(fd, static_cast<const uint8_t*>(ring[s].p), m, pos + off, threads))
+            return fail(XS_ERR_IO, "write to %s failed", path);
+        if (i + kLoadSlots < pieces) HIPCHK(queue(i + kLoadSlots));
+    }
+    return XS_OK;
+}
+
+// The bank's payload in file layout to `path` from byte `pos`.
+int write_file_payload(xs_bank* b, const char* path, uint64_t pos) {
+    const uint64_t nbytes = b->payload_bytes();
+    HIPCHK(hipSetDevice(b->device));
+    if (int rc = ws_enter(b, b->stream)) return rc;
+    if (b->kind == XS_BANK_RBLOOM || b->pitch == b->page)
+        return stream_device_to_file(b, path, pos, nbytes, b->image.as<uint8_t>());
+    if (int rc = b->tmp.ensure(nbytes)) return rc;
+    HIPCHK(launch_repack(b->image.as<uint8_t>(), b->pitch, b->tmp.as<uint8_t>(), b->page, b->sig_total(), b->page,
+                         b->stream));
+    return stream_device_to_file(b, path, pos, nbytes, b->tmp.as<uint8_t>());
+}
+
 // The bank's payload (the file's bytes after the header, at `pos`) into its image.
 int upload_file_payload(xs_bank* b, const char* path, uint64_t pos) {
     const uint64_t nbytes = b->payload_bytes();
@@ -540,8 +625,6 @@ int read_cobs_header(xs_bank* b, Reader& rd, const char* path) {
 }
 
 int write_cobs_file(xs_bank* b, const char* path) {
-    std::vector<uint8_t> payload(b->payload_bytes());
-    if (int rc = download_payload(b, payload.data(), payload.size())) return rc;
     std::ofstream o(path, std::ios::binary | std::ios::trunc);
     if (!o) return fail(XS_ERR_IO, "cannot open %s for writing", path);
     o.write("COBS:", 5);
@@ -574,20 +657,19 @@ int write_cobs_file(xs_bank* b, const char* path) {
         std::vector<char> z(pad, 0);
         o.write(z.data(), (std::streamsize)pad);
     }
-    o.write(reinterpret_cast<const char*>(payload.data()), (std::streamsize)payload.size());
+    const uint64_t pos = (uint64_t)o.tellp();
+    o.close();
     if (!o) return fail(XS_ERR_IO, "write to %s failed", path);
-    return XS_OK;
+    return write_file_payload(b, path, pos);  // the payload after the header, streamed from the device
 }
 
 int write_bloom_file(xs_bank* b, const char* path) {
-    std::vector<uint8_t> payload(b->nbytes);
-    if (int rc = download_payload(b, payload.data(), payload.size())) return rc;
     std::ofstream o(path, std::ios::binary | std::ios::trunc);
     if (!o) return fail(XS_ERR_IO, "cannot open %s for writing", path);
     put<uint64_t>(o, b->h);
-    o.write(reinterpret_cast<const char*>(payload.data()), (std::streamsize)payload.size());
+    o.close();
     if (!o) return fail(XS_ERR_IO, "write to %s failed", path);
-    return XS_OK;
+    return write_file_payload(b, path, 8);
 }
 
 // ---- query / build pipeline --------------------------------------------------
