@@ -19,12 +19,7 @@
 // glibc's printf("%.2f") rounds the same exact value the same way.
 #include "../../include/xspect_hip.h"
 
-#include <fcntl.h>
-#include <unistd.h>
-
 #include <algorithm>
-#include <atomic>
-#include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -203,58 +198,24 @@ void format_block(const Ctx<T>& c, int section, uint64_t lo, uint64_t hi, std::s
     k.finish();
 }
 
-// n bytes at file offset off (retrying short writes)
-bool pwrite_full(int fd, const char* p, size_t n, uint64_t off) {
-    while (n) {
-        const ssize_t w = pwrite(fd, p, n, (off_t)off);
-        if (w <= 0) {
-            if (w < 0 && errno == EINTR) continue;
-            return false;
-        }
-        p += w;
-        n -= (size_t)w;
-        off += (uint64_t)w;
-    }
-    return true;
-}
-
-// The sections are appended to the file the caller started (its leading
-// fields).  Each round's per-thread buffers get their file offsets from a
-// prefix sum and are written by up to 8 threads at once (pwrite) while the
-// next round is formatted: one writing thread was the limit (~9 GB/s on the
-// MI355X boxes' hosts, profiles/r05t_save*.json).
 template <class T>
 int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits, uint64_t total_kmers_in,
                    const uint32_t* total_order_row, int threads) {
     const uint64_t n = c.n, num_docs = c.D;
-    const int fd = ::open(path, O_WRONLY | O_CLOEXEC);
-    if (fd < 0) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
-    const off_t end = lseek(fd, 0, SEEK_END);
-    if (end < 0) {
-        ::close(fd);
-        return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
-    }
-    uint64_t off = (uint64_t)end;
-    auto put = [&](const char* s, size_t len) {
-        const bool r = pwrite_full(fd, s, len, off);
-        off += len;
-        return r;
-    };
-    auto puts_ = [&](const char* s) { return put(s, strlen(s)); };
+    FILE* f = fopen(path, "ab");
+    if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
     const int NT = std::max(1, std::min(threads > 0 ? threads : 16, 64));
-    const int NW = std::min(NT, 8);  // writing threads per round
     const uint64_t block = 1 << 14;  // reads per formatting round
     // two sets of per-thread buffers: round i is formatted while round i-1 is written
     std::vector<std::string> out[2] = {std::vector<std::string>((size_t)NT), std::vector<std::string>((size_t)NT)};
-    std::vector<uint64_t> at[2] = {std::vector<uint64_t>((size_t)NT), std::vector<uint64_t>((size_t)NT)};
     bool ok = true;
     const char* heads[3] = {"\"hits\": ", "\"scores\": ", "\"num_kmers\": "};
     for (int section = 0; section < 3 && ok; ++section) {
         // an empty section is "{}" as json.dumps writes it (a shard without reads)
         const bool empty = n == 0 && section != 1;
-        ok = puts_(heads[section]) && puts_(empty ? "{}" : "{\n");
+        ok = fputs(heads[section], f) >= 0 && fputs(empty ? "{}" : "{\n", f) >= 0;
         std::thread writer;
-        std::atomic<bool> wok{true};
+        bool wok = true;
         int cur = 0;
         for (uint64_t b0 = 0; b0 < n && ok; b0 += block, cur ^= 1) {
             const uint64_t b1 = std::min(n, b0 + block);
@@ -271,19 +232,9 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
             if (writer.joinable()) writer.join();
             ok = wok;
             if (!ok) break;
-            for (int t = 0; t < NT; ++t) {  // this round's place in the file
-                at[cur][t] = off;
-                off += out[cur][t].size();
-            }
             writer = std::thread([&, cur] {
-                auto write_some = [&, cur](int w) {
-                    for (int t = w; t < NT; t += NW)
-                        if (!pwrite_full(fd, out[cur][t].data(), out[cur][t].size(), at[cur][t])) wok = false;
-                };
-                std::vector<std::thread> ws;
-                for (int w = 1; w < NW; ++w) ws.emplace_back(write_some, w);
-                write_some(0);
-                for (auto& x : ws) x.join();
+                for (int t = 0; t < NT && wok; ++t)
+                    wok = fwrite(out[cur][t].data(), 1, out[cur][t].size(), f) == out[cur][t].size();
             });
         }
         if (writer.joinable()) writer.join();
@@ -317,11 +268,12 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
                 }
                 o += "\n        }";
             }
-            ok = put(o.data(), o.size());
+            ok = fwrite(o.data(), 1, o.size(), f) == o.size();
         }
-        if (ok) ok = puts_(empty ? (section < 2 ? ",\n    " : ",\n") : (section < 2 ? "\n    },\n    " : "\n    },\n"));
+        if (ok)
+            ok = fputs(empty ? (section < 2 ? ",\n    " : ",\n") : (section < 2 ? "\n    },\n    " : "\n    },\n"), f) >= 0;
     }
-    if (::close(fd) != 0) ok = false;
+    if (fclose(f) != 0) ok = false;
     if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
     return XS_OK;
 }
