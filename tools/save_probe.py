@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dir", default="/tmp")
+    ap.add_argument("--null", action="store_true", help="also save into /dev/null: the formatting alone")
     a = ap.parse_args()
     from xspect2_amd.packing import PackedIds
     from xspect2_amd.result import MatrixResult
@@ -51,8 +52,16 @@ def main():
         times.append(time.perf_counter() - t0)
     size = path.stat().st_size
     path.unlink()
-    print(json.dumps({"reads": n, "docs": D, "json_bytes": size, "save_s": times, "best_s": min(times),
-                      "GBps": size / min(times) / 1e9, "cpus": os.cpu_count()}), flush=True)
+    out = {"reads": n, "docs": D, "json_bytes": size, "save_s": times, "best_s": min(times),
+           "GBps": size / min(times) / 1e9, "cpus": os.cpu_count()}
+    if a.null:  # the same save with every write discarded
+        null = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            res.save(Path("/dev/null"))
+            null.append(time.perf_counter() - t0)
+        out["devnull_s"] = null
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":
