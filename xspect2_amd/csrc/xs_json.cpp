@@ -19,14 +19,7 @@
 // glibc's printf("%.2f") rounds the same exact value the same way.
 #include "../../include/xspect_hip.h"
 
-#include <fcntl.h>
-#include <sys/mman.h>
-#include <sys/stat.h>
-#include <unistd.h>
-
 #include <algorithm>
-#include <atomic>
-#include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -205,80 +198,24 @@ void format_block(const Ctx<T>& c, int section, uint64_t lo, uint64_t hi, std::s
     k.finish();
 }
 
-// n bytes at file offset off (retrying short writes)
-bool pwrite_full(int fd, const char* p, size_t n, uint64_t off) {
-    while (n) {
-        const ssize_t w = pwrite(fd, p, n, (off_t)off);
-        if (w <= 0) {
-            if (w < 0 && errno == EINTR) continue;
-            return false;
-        }
-        p += w;
-        n -= (size_t)w;
-        off += (uint64_t)w;
-    }
-    return true;
-}
-
-// One formatting round's buffers into a regular file at [at[0], end): the
-// file is extended to `end`, the range mapped shared and filled by up to 8
-// threads.  Formatting runs at ~32 GB/s on the MI355X boxes' 16 CPUs, but a
-// file takes write()s from one thread at a time (~8.5 GB/s, eight pwrite
-// threads gained nothing); page faults on a shared mapping do not queue on
-// that lock (profiles/r05t_save*.json).  false: nothing was written (the
-// caller writes the round with pwrite instead).
-bool map_round(int fd, const std::vector<std::string>& bufs, const std::vector<uint64_t>& at, uint64_t end) {
-    static const uint64_t page = (uint64_t)sysconf(_SC_PAGESIZE);
-    const uint64_t lo = at[0] & ~(page - 1);
-    if (end <= at[0]) return true;
-    if (ftruncate(fd, (off_t)end) != 0) return false;
-    void* m = mmap(nullptr, end - lo, PROT_WRITE, MAP_SHARED, fd, (off_t)lo);
-    if (m == MAP_FAILED) return false;
-    char* base = static_cast<char*>(m) - lo;
-    const int NT = (int)bufs.size(), NW = std::min(NT, 8);
-    auto fill = [&](int w) {
-        for (int t = w; t < NT; t += NW) memcpy(base + at[t], bufs[t].data(), bufs[t].size());
-    };
-    std::vector<std::thread> ws;
-    for (int w = 1; w < NW; ++w) ws.emplace_back(fill, w);
-    fill(0);
-    for (auto& x : ws) x.join();
-    munmap(m, end - lo);
-    return true;
-}
-
 template <class T>
 int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits, uint64_t total_kmers_in,
                    const uint32_t* total_order_row, int threads) {
     const uint64_t n = c.n, num_docs = c.D;
-    // the caller has written the file's leading fields: the sections go after them
-    int fd = ::open(path, O_RDWR | O_CLOEXEC);
-    bool mapped = fd >= 0;  // rounds through a shared mapping (regular files opened read-write)
-    if (fd < 0) fd = ::open(path, O_WRONLY | O_CLOEXEC);
-    if (fd < 0) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
-    struct stat st;
-    mapped = mapped && fstat(fd, &st) == 0 && S_ISREG(st.st_mode);
-    const off_t end = lseek(fd, 0, SEEK_END);
-    uint64_t off = end > 0 ? (uint64_t)end : 0;
-    auto put = [&](const char* s, size_t len) {
-        const bool r = pwrite_full(fd, s, len, off);
-        off += len;
-        return r;
-    };
-    auto puts_ = [&](const char* s) { return put(s, strlen(s)); };
+    FILE* f = fopen(path, "ab");
+    if (!f) return xs::set_error(XS_ERR_IO, (std::string("cannot append to ") + path).c_str());
     const int NT = std::max(1, std::min(threads > 0 ? threads : 16, 64));
     const uint64_t block = 1 << 14;  // reads per formatting round
     // two sets of per-thread buffers: round i is formatted while round i-1 is written
     std::vector<std::string> out[2] = {std::vector<std::string>((size_t)NT), std::vector<std::string>((size_t)NT)};
-    std::vector<uint64_t> at[2] = {std::vector<uint64_t>((size_t)NT), std::vector<uint64_t>((size_t)NT)};
     bool ok = true;
     const char* heads[3] = {"\"hits\": ", "\"scores\": ", "\"num_kmers\": "};
     for (int section = 0; section < 3 && ok; ++section) {
         // an empty section is "{}" as json.dumps writes it (a shard without reads)
         const bool empty = n == 0 && section != 1;
-        ok = puts_(heads[section]) && puts_(empty ? "{}" : "{\n");
+        ok = fputs(heads[section], f) >= 0 && fputs(empty ? "{}" : "{\n", f) >= 0;
         std::thread writer;
-        std::atomic<bool> wok{true};
+        bool wok = true;
         int cur = 0;
         for (uint64_t b0 = 0; b0 < n && ok; b0 += block, cur ^= 1) {
             const uint64_t b1 = std::min(n, b0 + block);
@@ -295,15 +232,9 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
             if (writer.joinable()) writer.join();
             ok = wok;
             if (!ok) break;
-            for (int t = 0; t < NT; ++t) {  // this round's place in the file
-                at[cur][t] = off;
-                off += out[cur][t].size();
-            }
-            writer = std::thread([&, cur, round_end = off] {
-                if (mapped && map_round(fd, out[cur], at[cur], round_end)) return;
-                mapped = false;  // this file takes no mapping: write()s from here on
+            writer = std::thread([&, cur] {
                 for (int t = 0; t < NT && wok; ++t)
-                    wok = pwrite_full(fd, out[cur][t].data(), out[cur][t].size(), at[cur][t]);
+                    wok = fwrite(out[cur][t].data(), 1, out[cur][t].size(), f) == out[cur][t].size();
             });
         }
         if (writer.joinable()) writer.join();
@@ -337,11 +268,12 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
                 }
                 o += "\n        }";
             }
-            ok = put(o.data(), o.size());
+            ok = fwrite(o.data(), 1, o.size(), f) == o.size();
         }
-        if (ok) ok = puts_(empty ? (section < 2 ? ",\n    " : ",\n") : (section < 2 ? "\n    },\n    " : "\n    },\n"));
+        if (ok)
+            ok = fputs(empty ? (section < 2 ? ",\n    " : ",\n") : (section < 2 ? "\n    },\n    " : "\n    },\n"), f) >= 0;
     }
-    if (::close(fd) != 0) ok = false;
+    if (fclose(f) != 0) ok = false;
     if (!ok) return xs::set_error(XS_ERR_IO, (std::string("write failed: ") + path).c_str());
     return XS_OK;
 }
