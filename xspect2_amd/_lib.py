@@ -7,6 +7,8 @@ object is missing or cannot be loaded, importing this module raises.
 from __future__ import annotations
 
 import ctypes
+import importlib.util
+import sys
 from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
@@ -160,6 +162,33 @@ SIGNATURES = {
 _LIB = None
 
 
+def _preload_hip_runtime() -> None:
+    """One HIP runtime per process, without importing torch.
+
+    torch's ROCm build carries its own libamdhip64 (SONAME libamdhip64.so.7)
+    and its libtorch_hip asks for it by file name, so a process that loaded
+    /opt/rocm's copy first (through this library's RUNPATH) would load a
+    second runtime when torch is imported, and device pointers would not pass
+    between them.  Loading torch's copy first (RTLD_GLOBAL) makes both this
+    library (by SONAME) and a later `import torch` (the same file) use it.
+    Importing torch itself for that cost a one-shot `xspect classify` process
+    1.2 s; the runtime alone is ~20 ms (tools/cli_probe.py,
+    profiles/r05u_cli*.json).  Without torch, /opt/rocm's runtime is used."""
+    if "torch" in sys.modules:
+        return  # torch has loaded its runtime already
+    try:
+        spec = importlib.util.find_spec("torch")  # locates, does not import
+    except (ImportError, ValueError):
+        return
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for root in spec.submodule_search_locations:
+        hip = Path(root) / "lib" / "libamdhip64.so"
+        if hip.exists():
+            ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+            return
+
+
 def load() -> ctypes.CDLL:
     """Load the in-tree shared library (raises if it is missing)."""
     global _LIB
@@ -170,12 +199,7 @@ def load() -> ctypes.CDLL:
         raise ImportError(
             f"{SO_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the probe path has no CPU fallback)")
-    # torch (if present) must own the HIP runtime first: libamdhip64.so.7 is
-    # then shared by soname instead of loading a second copy from /opt/rocm.
-    try:
-        import torch  # noqa: F401
-    except Exception:  # pragma: no cover - torch is optional for the ABI
-        pass
+    _preload_hip_runtime()
     lib = ctypes.CDLL(str(path))
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
