@@ -1,7 +1,8 @@
 """Start-up costs of a one-shot `xspect classify` process on this box (the
 reference's CLI runs one process per input): the package import, loading
-libxspect_hip.so, the first HIP call, a bank file opening onto the device and
-the first small query, each timed in a fresh child process (so nothing is
+libxspect_hip.so, the first HIP call, the first kernel launch (a tiny bank's
+repack: the library's code object goes to the GPU), a bank file opening onto
+the device and the first small query, each timed in a fresh child process (so nothing is
 warm but the page cache).  One JSON line.
 
     python tools/cli_probe.py
@@ -33,6 +34,11 @@ t["load_library_s"] = time.perf_counter() - t1
 t1 = time.perf_counter()
 n = _lib.device_count()
 t["first_hip_call_s"] = time.perf_counter() - t1
+t1 = time.perf_counter()
+tiny = Bank.create_cobs(21, 7, [1001], 100)
+tiny.upload(np.zeros(tiny.payload_bytes(), np.uint8))  # the first kernel launch (the repack)
+tiny.close()
+t["first_kernel_s"] = time.perf_counter() - t1
 path = sys.argv[1]
 if path != "-":
     t1 = time.perf_counter()
