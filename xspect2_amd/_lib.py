@@ -185,7 +185,10 @@ def _preload_hip_runtime() -> None:
     for root in spec.submodule_search_locations:
         hip = Path(root) / "lib" / "libamdhip64.so"
         if hip.exists():
-            ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+            try:
+                ctypes.CDLL(str(hip), mode=ctypes.RTLD_GLOBAL)
+            except OSError:  # an unusable torch install: this library's own runtime then
+                pass
             return
 
 
