@@ -56,8 +56,9 @@ class GpuSearch:
     def search_batch(self, seqs, step=1, out=None):
         """seqs: list[str] -> (hits uint32 [n, D], num_kmers uint64 [n]).
         out: a reused C-contiguous uint32 [n, D] array; a serving loop passes
-        one to skip the OS's first-touch faults of a fresh matrix, which cost
-        more than the query itself at 10^6 reads."""
+        one to skip what a fresh matrix costs the OS (faulting it in, and
+        unmapping it when dropped: more than the query at 10^6 reads, DESIGN.md
+        section 9c)."""
         data = [s.encode() for s in seqs]
         offs = np.zeros(len(data) + 1, np.uint64)
         offs[1:] = np.cumsum([len(b) for b in data])
