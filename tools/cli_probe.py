@@ -39,6 +39,12 @@ tiny = Bank.create_cobs(21, 7, [1001], 100)
 tiny.upload(np.zeros(tiny.payload_bytes(), np.uint8))  # the first kernel launch (the repack)
 tiny.close()
 t["first_kernel_s"] = time.perf_counter() - t1
+fq = sys.argv[2]
+from xspect2_amd.file_io import read_batches
+for name in ("first_device_reader_s", "second_device_reader_s"):  # the parse kernels' module, then warm
+    t1 = time.perf_counter()
+    nb = sum(bt.n for bt in read_batches(fq, 1 << 20, device=0))
+    t[name] = time.perf_counter() - t1
 path = sys.argv[1]
 if path != "-":
     t1 = time.perf_counter()
@@ -68,12 +74,15 @@ def main():
             "b.upload(np.random.default_rng(1).integers(0, 256, b.payload_bytes(), dtype=np.uint8))\n"
             "b.save(%r)\n" % (str(ROOT), str(path)))
     subprocess.run([sys.executable, "-c", make], check=True)
+    fq = Path("/tmp/xs_cli_probe.fq")
+    fq.write_bytes(b"".join(b"@r%d\n%s\n+\n%s\n" % (i, b"ACGT" * 37 + b"AC", b"I" * 150) for i in range(1000)))
     runs = []
     for _ in range(3):
-        r = subprocess.run([sys.executable, "-c", CHILD % str(ROOT), str(path)], check=True,
+        r = subprocess.run([sys.executable, "-c", CHILD % str(ROOT), str(path), str(fq)], check=True,
                            capture_output=True, text=True)
         runs.append(json.loads(r.stdout.strip().splitlines()[-1]))
     path.unlink()
+    fq.unlink()
     best = {k: min(r[k] for r in runs) for k in runs[0]}
     print(json.dumps({"runs": runs, "best": best, "bank_file_mb": 2_000_003 * 13 / 1e6}), flush=True)
 
