@@ -97,3 +97,31 @@ def test_u32_wire_very_long_reads(xs, oracle_mod):
     want = _all_outputs_equal_oracle(xs, gb, ob, reads)
     assert int(want.max()) > 65535
     gb.close()
+
+
+def test_pinned_buffers_are_given_back(xs):
+    """xs_host_alloc / xs_host_free over both kinds of pinned memory (2 MiB
+    and more: registered huge-page mappings; less: hipHostMalloc), 24
+    rounds of 256 MiB + 1 MiB: the process's resident memory does not grow
+    by more than a round's worth (a mapping kept after its free would add
+    256 MiB a round), and each buffer holds what was written to it."""
+    import gc
+
+    def rss_mb():
+        for line in open("/proc/self/status"):
+            if line.startswith("VmRSS:"):
+                return int(line.split()[1]) / 1024
+        return 0.0
+
+    base = None
+    for i in range(24):
+        big = xs.pinned_empty((256 << 20,), np.uint8)
+        small = xs.pinned_empty((1 << 20,), np.uint8)
+        big[:: 1 << 20] = i
+        small[:] = i
+        assert int(big[(255 << 20)]) == i and int(small[-1]) == i
+        del big, small
+        gc.collect()
+        if i == 3:
+            base = rss_mb()
+    assert rss_mb() - base < 400, (base, rss_mb())
