@@ -79,6 +79,8 @@ def test_input_validation_before_device(tmp_path):
         m.calculate_hits("A" * 21)
     with pytest.raises(NotImplementedError):
         m.predict([Record("a", "A" * 30)], validation=True)
+    with pytest.raises(NotImplementedError):  # present, as in the reference (:508), but out of scope
+        m.detecting_misclassification({}, [], min_reads=10)
 
 
 def test_splitter_known_answer_and_oracle(golden, oracle_mod):

@@ -293,6 +293,14 @@ class ProbabilisticFilterModel:
                                       "is outside the GPU probe path")
         return self.predict_columnar(sequence_input, exclude_ids, step, display_name).to_model_result()
 
+    def detecting_misclassification(self, hits: dict, seq_records: list, min_reads: int = 10) -> dict:
+        """Reference :508-601 maps the reads with minimap2 against genomes it
+        downloads from NCBI: network and an aligner, outside the k-mer × filter
+        path.  Present so a caller switching classes gets this
+        error rather than an AttributeError."""
+        raise NotImplementedError("detecting_misclassification (minimap2 against NCBI downloads) "
+                                  "is outside the GPU probe path")
+
     # ------------------------------------------------------------ k-mer counts
     def _count_kmers_len(self, length: int, step: int) -> int:
         return math.ceil((length - self.k + 1) / step)   # reference :462
