@@ -116,3 +116,7 @@ def test_filter_sequences_equals_restatement(tmp_path, kind, capsys):
     # ids that match nothing: the reference has opened (created) the file
     filter_sequences(inp, tmp_path / "empty.fasta", ["nope"])
     assert (tmp_path / "empty.fasta").read_bytes() == b""
+    # also where the reference keeps it (src/xspect/file_io.py:166)
+    from xspect2_amd import file_io
+    file_io.filter_sequences(inp, tmp_path / "out2.fasta", wanted)
+    assert (tmp_path / "out2.fasta").read_bytes() == out.read_bytes()

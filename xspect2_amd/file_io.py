@@ -409,3 +409,11 @@ def prepare_input_output_paths(input_path: Path):
         return output_path
 
     return inputs, get_output_path
+
+
+def filter_sequences(input_file: Path, output_file: Path, included_ids: list[str]) -> None:
+    """Where the reference keeps it (file_io.py:166-191): the records of
+    `input_file` whose ids are in `included_ids`, written as FASTA; the
+    implementation is xspect2_amd.filter_sequences.filter_sequences."""
+    from .filter_sequences import filter_sequences as _filter
+    return _filter(input_file, output_file, included_ids)
