@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--dir", default=None)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--quick", action="store_true", help="parse and e2e legs only")
+    ap.add_argument("--profile-classify", default=None,
+                    help="write a cProfile summary of a second predict_columnar(file) to this path")
     args = ap.parse_args()
 
     import torch
@@ -254,6 +256,19 @@ def main():
     cres = species.predict_columnar(fq)
     res["classify_predict_s"] = time.perf_counter() - t
     cres.input_source = fq.name
+    if args.profile_classify:  # where the host side of predict_columnar goes (warm)
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        t = time.perf_counter()
+        pr.enable()
+        species.predict_columnar(fq)
+        pr.disable()
+        res["classify_predict_again_s"] = time.perf_counter() - t
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats("cumulative").print_stats(30)
+        Path(args.profile_classify).write_text(buf.getvalue())
     t = time.perf_counter()
     cres.save(tmp / "classify.json")
     res["classify_save_s"] = time.perf_counter() - t
