@@ -38,6 +38,22 @@ def test_json_quote_and_duplicates_match_python(seed):
     assert p.has_duplicates() == (len(set(ids)) != len(ids))
 
 
+def test_duplicates_over_threads():
+    """xs_ids_has_duplicates at sizes that use its threads (hashing split over
+    up to 16 threads, 256 hash buckets searched in parallel): 300 k distinct
+    ids, then one repeat placed first/last, across the threads' ranges, an
+    empty id twice, and ids that are prefixes of each other."""
+    base = [f"read_{i}" for i in range(300_000)]
+    assert not PackedIds.of(base).has_duplicates()
+    assert not PackedIds.of(base + [f"read_{i}x" for i in range(1000)] + [""]).has_duplicates()
+    for a, b in ((0, 299_999), (10, 150_000), (70_000, 70_001), (299_998, 5)):
+        ids = list(base)
+        ids[b] = ids[a]
+        assert PackedIds.of(ids).has_duplicates(), (a, b)
+    assert PackedIds.of(base + ["", ""]).has_duplicates()
+    assert PackedIds.of([""] + base + [""]).has_duplicates()
+
+
 def test_non_ascii_ids_fall_back_to_python():
     ids = ["r1", "é", "ü∑", "r1x", "\U0001F600"]
     p = PackedIds.of(ids)

@@ -20,6 +20,7 @@
 #include "../../include/xspect_hip.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <numeric>
@@ -498,31 +499,76 @@ int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int
         if (!offs || !has_dup || (!buf && n && offs[n])) return xs::set_error(XS_ERR_ARG, "null argument");
         *has_dup = 0;
         if (n < 2) return XS_OK;
-        uint64_t cap = 16;
-        while (cap < 2 * n) cap <<= 1;
-        std::vector<uint64_t> slot(cap, ~0ull);  // id index + 1 of the occupant, ~0 = empty
-        std::vector<uint64_t> hv(cap);
-        for (uint64_t i = 0; i < n; ++i) {
-            const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
-            const uint64_t len = offs[i + 1] - offs[i];
-            uint64_t hsh = 1469598103934665603ull;
-            for (uint64_t j = 0; j < len; ++j) hsh = (hsh ^ s[j]) * 1099511628211ull;
-            hsh ^= hsh >> 29;
-            for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
-                if (slot[p] == ~0ull) {
-                    slot[p] = i;
-                    hv[p] = hsh;
-                    break;
-                }
-                if (hv[p] == hsh) {
-                    const uint64_t k = slot[p];
-                    if (offs[k + 1] - offs[k] == len && memcmp(buf + offs[k], s, len) == 0) {
-                        *has_dup = 1;
-                        return XS_OK;
+        // every read of a file is checked (MatrixResult; 12.5 M per rank at config 3): the ids are
+        // hashed by up to 16 threads, binned by hash into 256 buckets, and each bucket is searched
+        // for equal ids with a small table of its own (one thread per bucket at a time)
+        const int T = (int)std::min<uint64_t>(16, std::max<uint64_t>(1, n / 65536));
+        constexpr int kBucketBits = 8, kBuckets = 1 << kBucketBits;
+        std::vector<uint64_t> hv(n);
+        std::vector<uint64_t> cnt((size_t)T * kBuckets, 0);
+        const uint64_t per = (n + T - 1) / T;
+        auto par = [&](auto&& fn) {
+            std::vector<std::thread> th;
+            for (int t = 1; t < T; ++t) th.emplace_back(fn, t);
+            fn(0);
+            for (auto& x : th) x.join();
+        };
+        par([&](int t) {
+            const uint64_t a = per * t, e = std::min(n, a + per);
+            uint64_t* c = &cnt[(size_t)t * kBuckets];
+            for (uint64_t i = a; i < e; ++i) {
+                const unsigned char* s = reinterpret_cast<const unsigned char*>(buf + offs[i]);
+                uint64_t h = 1469598103934665603ull;
+                for (uint64_t j = 0, len = offs[i + 1] - offs[i]; j < len; ++j) h = (h ^ s[j]) * 1099511628211ull;
+                h ^= h >> 29;
+                h *= 0xBF58476D1CE4E5B9ull;
+                h ^= h >> 32;
+                hv[i] = h;
+                ++c[h >> (64 - kBucketBits)];
+            }
+        });
+        // bucket b holds [start[b], start[b + 1]) of `order`; thread t writes from its own cursor
+        std::vector<uint64_t> start(kBuckets + 1, 0), cur((size_t)T * kBuckets);
+        for (int b = 0; b < kBuckets; ++b) {
+            uint64_t o = start[b];
+            for (int t = 0; t < T; ++t) {
+                cur[(size_t)t * kBuckets + b] = o;
+                o += cnt[(size_t)t * kBuckets + b];
+            }
+            start[b + 1] = o;
+        }
+        std::vector<uint64_t> order(n);
+        par([&](int t) {
+            const uint64_t a = per * t, e = std::min(n, a + per);
+            uint64_t* c = &cur[(size_t)t * kBuckets];
+            for (uint64_t i = a; i < e; ++i) order[c[hv[i] >> (64 - kBucketBits)]++] = i;
+        });
+        std::atomic<int> found{0};
+        par([&](int t) {
+            std::vector<uint64_t> slot;  // index into order + 1; 0 = empty
+            for (int b = t; b < kBuckets && !found.load(std::memory_order_relaxed); b += T) {
+                const uint64_t b0 = start[b], m = start[b + 1] - b0;
+                if (m < 2) continue;
+                uint64_t cap = 16;
+                while (cap < 2 * m) cap <<= 1;
+                slot.assign(cap, 0);
+                for (uint64_t q = 0; q < m; ++q) {
+                    const uint64_t i = order[b0 + q], h = hv[i], len = offs[i + 1] - offs[i];
+                    for (uint64_t p = (h * 0x9E3779B97F4A7C15ull) >> 1 & (cap - 1);; p = (p + 1) & (cap - 1)) {
+                        if (!slot[p]) {
+                            slot[p] = q + 1;
+                            break;
+                        }
+                        const uint64_t k = order[b0 + slot[p] - 1];
+                        if (hv[k] == h && offs[k + 1] - offs[k] == len && memcmp(buf + offs[k], buf + offs[i], len) == 0) {
+                            found.store(1, std::memory_order_relaxed);
+                            return;
+                        }
                     }
                 }
             }
-        }
+        });
+        *has_dup = found.load();
         return XS_OK;
     });
 }
