@@ -236,8 +236,31 @@ int main() {
         for (uint64_t i = 0; i < n; ++i)
             if (out[i] != (ref.count(keys[i]) ? 1 : 0)) ++unexpected;
     }
+    // repeated ids (xs_ids_has_duplicates): threaded passes over 300 k ids of 0..12 bytes, distinct
+    // and with one repeat at random places, checked against std::set
+    for (int trial = 0; trial < 6; ++trial) {
+        const uint64_t n = 300000;
+        std::vector<std::string> ids;
+        std::set<std::string> seen;
+        while (ids.size() < n) {
+            std::string s = std::to_string(ids.size()) + rand_seq(rng() % 6, "ab:_");
+            if (seen.insert(s).second) ids.push_back(s);
+        }
+        if (trial % 2) ids[rng() % n] = ids[rng() % n];
+        std::string buf;
+        std::vector<uint64_t> off{0};
+        for (auto& s : ids) {
+            buf += s;
+            off.push_back(buf.size());
+        }
+        int dup = -1;
+        if (xs_ids_has_duplicates(buf.data(), off.data(), n, &dup)) ++unexpected;
+        const bool want = std::set<std::string>(ids.begin(), ids.end()).size() != n;
+        if (dup != (want ? 1 : 0)) ++unexpected;
+    }
     printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices, "
-           "20 id-key batches + a threaded one, 6 member masks; %d clean error returns, %d on well-formed input\n",
+           "20 id-key batches + a threaded one, 6 member masks, 6 threaded repeat checks; %d clean error returns, "
+           "%d on well-formed input\n",
            files, errors, unexpected);
     return unexpected ? 1 : 0;
 }
