@@ -406,3 +406,33 @@ def test_config1_classify_species_on_an_assembly(tmp_path, species_dir, genomes,
     assert got["scores"]["total"] == {d: round(tot[d] / int(nk.sum()), 2) for d in tot}
     assert max(tot, key=tot.get) == "GCF_000018445"  # genome 1's species
     assert got["input_source"] == "assembly.fna"
+
+
+def test_classify_species_directory_saves_behind(tmp_path, species_dir, genomes, monkeypatch, capsys):
+    """A directory of inputs through classify_species: each file's result is
+    saved on a worker thread while the next file is predicted
+    (classify._SaveBehind); the outputs <stem>_<i>.json equal one-file calls
+    byte for byte and the "Saved result as" lines come in file order."""
+    from xspect2_amd import classify
+    from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
+
+    root = tmp_path / "xspect-data"
+    monkeypatch.setenv("XSPECT_DATA", str(root))
+    model = ProbabilisticFilterModel(K, "Acinetobacter", None, None, "Species", root / "models")
+    model.fit(species_dir)
+    model.save()
+    model.close()
+    inp = tmp_path / "inputs"
+    inp.mkdir()
+    for i in range(3):
+        g = genomes[i].tobytes().decode()
+        write_fasta([Record(f"s{i}_a", g[: 9000 + 1000 * i]), Record(f"s{i}_b", g[12_000:])], inp / f"a{i}.fasta")
+    capsys.readouterr()
+    classify.classify_species("Acinetobacter", inp, tmp_path / "out" / "res.json")
+    lines = [ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("Saved result as")]
+    assert lines == [f"Saved result as res_{i + 1}.json" for i in range(3)]
+    files, _ = __import__("xspect2_amd.file_io", fromlist=["x"]).prepare_input_output_paths(inp)
+    for i, f in enumerate(files):
+        one = tmp_path / "one" / f"r{i}.json"
+        classify.classify_species("Acinetobacter", f, one)
+        assert (tmp_path / "out" / f"res_{i + 1}.json").read_bytes() == one.read_bytes()

@@ -312,3 +312,39 @@ def test_host_pool_never_hands_one_block_to_two_threads():
     for x in th:
         x.join()
     assert not bad and sum(b.size for b in p.blocks) <= 1 << 30
+
+
+def test_save_behind_keeps_order_prints_and_errors(tmp_path, capsys):
+    """classify_*'s saves of a directory's results run on one worker thread
+    behind the next prediction (classify._SaveBehind): every file is written,
+    "Saved result as ..." comes in file order once each save has finished,
+    and a failing save raises in the caller."""
+    import time
+    from xspect2_amd.classify import _SaveBehind
+
+    class Res:
+        def __init__(self, text, delay=0.0, fail=False):
+            self.text, self.delay, self.fail = text, delay, fail
+
+        def save(self, path):
+            time.sleep(self.delay)
+            if self.fail:
+                raise OSError("disk full")
+            path.write_text(self.text)
+
+    s = _SaveBehind()
+    for i in range(4):
+        s.submit(Res(f"r{i}", delay=0.05 if i % 2 == 0 else 0.0), tmp_path / f"out_{i + 1}.json")
+    s.finish()
+    assert [(tmp_path / f"out_{i + 1}.json").read_text() for i in range(4)] == ["r0", "r1", "r2", "r3"]
+    out = capsys.readouterr().out.splitlines()
+    assert out == [f"Saved result as out_{i + 1}.json" for i in range(4)]
+    s = _SaveBehind()
+    s.submit(Res("x", fail=True), tmp_path / "bad.json")
+    with pytest.raises(OSError, match="disk full"):
+        s.submit(Res("y"), tmp_path / "next.json")
+    s.finish()
+    s = _SaveBehind()
+    s.submit(Res("x", fail=True), tmp_path / "bad2.json")
+    with pytest.raises(OSError, match="disk full"):
+        s.finish()
