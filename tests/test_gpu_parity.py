@@ -284,6 +284,48 @@ def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
     gb.close()
 
 
+def _random_direct_configs(n=32, seed=20261018):
+    """Seeded random banks for the direct COBS probe families (fast, wide,
+    slots, general): classic with 1..2200 docs, or compact with page sizes
+    1..64 and 1..8 groups; k 5..32, h 1..9; a few thousand rows per group."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(5, 33))
+        h = int(rng.integers(1, 10))
+        if rng.random() < 0.5:
+            D = int(rng.choice([int(rng.integers(1, 129)), int(rng.integers(129, 2201))]))
+            out.append((D, k, h, None, 1))
+        else:
+            page = int(rng.choice([1, 2, 3, 8, 16, 32, 40, 48, 64]))
+            G = int(rng.integers(1, 9))
+            D = int(rng.integers((G - 1) * 8 * page + 1, G * 8 * page + 1))
+            out.append((D, k, h, page, G))
+    return out
+
+
+@pytest.mark.parametrize("D,k,h,page,G", _random_direct_configs())
+def test_direct_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, page, G):
+    """Seeded random classic and compact banks through the direct probes
+    (the partitioned path kept off): same hits, k-mer counts and totals as
+    the oracle at steps 1 and 4, for random, document-derived, non-ACGT,
+    short and multi-unit reads."""
+    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    rng = np.random.default_rng(D * 131 + k * 7 + h)
+    sig = [int(x) for x in rng.integers(700, 5000, G)]
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, page=page, seed=D + k, per_doc=1)
+    reads = _reads(rng, 150, k) + [s[: int(rng.integers(k, len(s) + 1))] for s in seqs[:40]]
+    reads += _reads(rng, 20, k, alphabet="ACGTNacgtnRY") + [b"", b"A" * max(k - 1, 0), seqs[0] * 3]
+    for step in (1, 4):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h, want_h), _explain(got_h, want_h, reads)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+    gb.close()
+
+
 @pytest.mark.parametrize("D,k,h,page", [(5, 21, 7, None), (100, 21, 7, None), (37, 31, 1, 2), (12, 32, 3, None)])
 def test_device_build_matches_oracle_build(xs, oracle_mod, D, k, h, page):
     rng = np.random.default_rng(7 * D + k)
