@@ -326,7 +326,19 @@ def test_direct_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, page,
     gb.close()
 
 
-@pytest.mark.parametrize("D,k,h,page", [(5, 21, 7, None), (100, 21, 7, None), (37, 31, 1, 2), (12, 32, 3, None)])
+def _random_build_configs(n=16, seed=20261019):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        k, h = int(rng.integers(5, 33)), int(rng.integers(1, 10))
+        page = None if rng.random() < 0.5 else int(rng.choice([1, 2, 8, 64]))
+        D = int(rng.integers(1, 300))
+        out.append((D, k, h, page))
+    return out
+
+
+@pytest.mark.parametrize("D,k,h,page", [(5, 21, 7, None), (100, 21, 7, None), (37, 31, 1, 2), (12, 32, 3, None)]
+                         + _random_build_configs())
 def test_device_build_matches_oracle_build(xs, oracle_mod, D, k, h, page):
     rng = np.random.default_rng(7 * D + k)
     seqs, ids = _docs(rng, D, k, per_doc=3)
