@@ -360,7 +360,12 @@ def _stack(parts: list, D: int) -> tuple[np.ndarray, np.ndarray]:
     if len(parts) == 1:
         return parts[0]
     dt = max((h.dtype for h, _ in parts), key=lambda t: t.itemsize)
-    return np.concatenate([h.astype(dt, copy=False) for h, _ in parts]), np.concatenate([n for _, n in parts])
+    # into a recycled host block (bank._HostPool): no fresh pages to fault in now or unmap when the
+    # result is dropped (the batches' own arrays go back to the pool once this returns)
+    from .bank import _HOST_POOL
+    out = _HOST_POOL.empty((sum(h.shape[0] for h, _ in parts), D), dt)
+    np.concatenate([h.astype(dt, copy=False) for h, _ in parts], out=out)
+    return out, np.concatenate([n for _, n in parts])
 
 
 def _batches(lens: list[int]) -> Iterable[tuple[int, int]]:
