@@ -196,6 +196,7 @@ struct xs_bank {
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
     PinnedBuf small_h;              // small host calls: the whole request and its results (query_small)
     PinnedBuf cut_ofs;              // device-read batches: read offsets at the chunk cuts
+    PinnedBuf offs_h;               // host batches: the read offsets rebased to 0, for their H2D copy
     DevBuf small_d;
     hipEvent_t hstage_ev[2] = {nullptr, nullptr};
     hipStream_t copy_stream = nullptr, d2h_stream = nullptr;
@@ -903,6 +904,18 @@ int host_threads() {
     return (int)std::max(1u, std::min(8u, hw ? hw : 1u));
 }
 
+// fn(t, a, e) over the ranges of [0, n) of up to `threads` threads (one below 2^18 items:
+// a host batch's per-read passes run before its first copy, in the call's critical path)
+template <class F>
+void par_ranges(uint64_t n, int threads, F fn) {
+    const int T = n < (1u << 18) ? 1 : threads;
+    const uint64_t per = (n + T - 1) / T;
+    std::vector<std::thread> th;
+    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(fn, t, per * t, std::min(n, per * (t + 1)));
+    fn(0, 0, std::min(n, per));
+    for (auto& x : th) x.join();
+}
+
 // ---- hit rows back to a host array, behind the probe ------------------------
 // A host call's hit rows go to the caller's array on a worker thread while the
 // bank stream probes the next chunks (the main thread only launches): each
@@ -1107,9 +1120,24 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         }
     }
     const uint64_t base = dev ? 0 : offsets[0];
-    if (!dev)
-        for (uint64_t r = 0; r < n; ++r)
-            if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    if (!dev) {
+        // one pass, on several threads: the offsets checked and rebased to 0 into pinned memory
+        // (their H2D copy then needs no staging)
+        if (int rc = b->offs_h.ensure((n + 1) * 8)) return rc;
+        uint64_t* rb = static_cast<uint64_t*>(b->offs_h.p);
+        bool bad[8] = {};
+        par_ranges(n, host_threads(), [&](int t, uint64_t a, uint64_t e) {
+            bool ok = true;
+            for (uint64_t r = a; r < e; ++r) {
+                ok &= offsets[r + 1] >= offsets[r];
+                rb[r] = offsets[r] - base;
+            }
+            bad[t] = !ok;
+        });
+        rb[n] = offsets[n] - base;
+        for (bool x : bad)
+            if (x) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
+    }
     const uint64_t bytes = dev ? dev->seq_bytes : offsets[n] - base;
     const uint64_t cols = b->kind == XS_BANK_RBLOOM ? 1 : b->D;
     const uint64_t pcols = cols + 1;
@@ -1176,9 +1204,8 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
     }
     const uint8_t* d_seqs = dev ? dev->seqs : b->seqs.as<uint8_t>();
     const uint64_t* d_offs = dev ? dev->offs : b->offs.as<uint64_t>();
-    std::vector<uint64_t> rebased(dev ? 0 : n + 1);
     // whatever way the call ends (an error return included), no H2D copy may still be
-    // reading `rebased` or the caller's reads once it has: the copy stream drains on exit
+    // reading the caller's reads or the rebased offsets once it has: the copy stream drains on exit
     struct DrainOnExit {
         hipStream_t s = nullptr;
         ~DrainOnExit() {
@@ -1186,9 +1213,8 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
         }
     } drain;
     if (!dev) {
-        for (uint64_t r = 0; r <= n; ++r) rebased[r] = offsets[r] - base;
         drain.s = b->copy_stream;
-        HIPCHK(hipMemcpyAsync(b->offs.p, rebased.data(), (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
+        HIPCHK(hipMemcpyAsync(b->offs.p, b->offs_h.p, (n + 1) * 8, hipMemcpyHostToDevice, b->copy_stream));
     }
     const int threads = host_threads();
     // the hit rows go back behind the probe (HitSink: its own thread, stream and pinned ring)
@@ -1241,7 +1267,7 @@ int query_host(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n
             tot_host[c] = v;
         }
     }
-    if (!dev) HIPCHK(hipStreamSynchronize(b->copy_stream));  // `rebased` leaves scope
+    if (!dev) HIPCHK(hipStreamSynchronize(b->copy_stream));  // offs_h is rewritten by the next call
     if (narrowing) {  // a count wider than the wire (device reads: the caller's max_len understated)
         uint32_t over = 0;
         HIPCHK(hipMemcpyAsync(&over, b->ovf.p, sizeof(over), hipMemcpyDeviceToHost, b->stream));
@@ -1771,13 +1797,26 @@ static int query_impl(xs_bank* b, const char* seqs, const uint64_t* offsets, uin
     uint64_t max_nk = 0;
     if (hits_out) {
         const uint64_t cap = hit_bytes == 1 ? 0xFFu : hit_bytes == 2 ? 0xFFFFu : 0xFFFFFFFFu;
-        for (uint64_t r = 0; r < n; ++r) {
-            const uint64_t len = offsets[r + 1] >= offsets[r] ? offsets[r + 1] - offsets[r] : 0;
-            const uint64_t nk = len >= b->k ? (len - b->k) / step + 1 : 0;
-            if (nk > cap)
+        uint64_t mx[8] = {}, over[8];
+        for (auto& o : over) o = ~0ull;
+        const uint32_t k = b->k;
+        par_ranges(n, host_threads(), [&](int t, uint64_t a, uint64_t e) {
+            uint64_t m = 0;
+            for (uint64_t r = a; r < e; ++r) {
+                const uint64_t len = offsets[r + 1] >= offsets[r] ? offsets[r + 1] - offsets[r] : 0;
+                const uint64_t nk = len >= k ? (len - k) / step + 1 : 0;
+                if (nk > cap && over[t] == ~0ull) over[t] = r;
+                m = std::max(m, nk);
+            }
+            mx[t] = m;
+        });
+        for (int t = 0; t < 8; ++t) {
+            if (over[t] != ~0ull) {
+                const uint64_t r = over[t], len = offsets[r + 1] - offsets[r];
                 return fail(XS_ERR_ARG, "read %llu has %llu sampled k-mers: counts may not fit %d byte(s)",
-                            (unsigned long long)r, (unsigned long long)nk, hit_bytes);
-            max_nk = std::max(max_nk, nk);
+                            (unsigned long long)r, (unsigned long long)((len - k) / step + 1), hit_bytes);
+            }
+            max_nk = std::max(max_nk, mx[t]);
         }
     }
     std::lock_guard<std::mutex> lk(b->mu);
