@@ -125,3 +125,35 @@ def test_pinned_buffers_are_given_back(xs):
         if i == 3:
             base = rss_mb()
     assert rss_mb() - base < 400, (base, rss_mb())
+
+
+def test_large_host_batch_argument_errors(xs, oracle_mod):
+    """The per-read passes of a host batch run on several threads from 2^18
+    reads on: a decreasing offset anywhere is refused, and a read too long
+    for a narrow output is reported by its index (the first such read)."""
+    from xspect2_amd import _lib
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [40_000], seed=31)
+    n = 300_000
+    seq = (b"ACGT" * 15) * n  # 300 k reads of 60 bp
+    offs = np.arange(n + 1, dtype=np.uint64) * 60
+    bad = offs.copy()
+    bad[250_001] = bad[250_000] - 1  # in the last threads' ranges
+    hits = np.empty((n, 100), np.uint32)
+    nk = np.empty(n, np.uint64)
+    lib = _lib.load()
+    rc = lib.xs_query(gb.handle, seq, bad.ctypes.data, n, 1, hits.ctypes.data, nk.ctypes.data)
+    assert rc == _lib.XS_ERR_ARG and b"non-decreasing" in lib.xs_last_error()
+    # reads 200000 and 280000 have 280 k-mers: too many for uint8 counts; the first is named
+    lens = np.full(n, 60, dtype=np.uint64)
+    lens[200_000] = lens[280_000] = 300
+    offs2 = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=offs2[1:])
+    seq2 = (b"ACGT" * 75) * 2 + seq[: int(offs2[-1]) - 600]
+    out8 = np.empty((n, 100), np.uint8)
+    rc = lib.xs_query_hits(gb.handle, seq2, offs2.ctypes.data, n, 1, out8.ctypes.data, 1, nk.ctypes.data)
+    assert rc == _lib.XS_ERR_ARG and b"read 200000 has 280 sampled k-mers" in lib.xs_last_error()
+    # and a valid large batch still equals the oracle
+    got, got_nk = gb.query([seq[:60]] * 10 + [seqs[0][:150]])
+    want, want_nk = ob.query([seq[:60]] * 10 + [seqs[0][:150]])
+    assert np.array_equal(got, want) and np.array_equal(got_nk, want_nk)
+    gb.close()
