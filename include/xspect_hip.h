@@ -267,11 +267,41 @@ int xs_bank_probe_rows(xs_bank* bank, uint64_t* rows);
  * filters of >= 16 MiB: k-mer bit indices binned by 2 MiB filter partition,
  * each partition tested from one XCD's L2).  The partitioned path is taken
  * while the handle's previous query found at least 24 % of its k-mers in the
- * filter (member-rich input, where it is faster); XSPECT2_AMD_BLOOM_PART=0
- * disables it.  Both give identical results. */
+ * filter (member-rich input, where it is faster); xs_bank_set_probe_options
+ * can disable it.  Both give identical results. */
 #define XS_PATH_GATHER 0
 #define XS_PATH_PARTITIONED 1
 int xs_bank_probe_path(const xs_bank* bank, int* path);
+
+/* Probe path selection of one handle.  The defaults (what xs_bank_open and
+ * xs_bank_create_* set: 1, 1, 24576, 1) are the paths a production query takes;
+ * the other values exist so tests can run every path on the same bank, and no
+ * environment variable changes them.  Every path gives identical results.  No
+ * reference counterpart (cobs_index / rbloom have one probe each,
+ * pyproject.toml:16-17).  Applies to the handle's next query. */
+typedef struct xs_probe_options_t {
+    int32_t cobs_part;      /* COBS classic banks of <= 128 docs: 0 = direct probe only; 1 = the partitioned
+                               probe for banks of >= 32 MiB and calls of >= 2^23 k-mers; 2 = partitioned for
+                               every such bank and call; 3 = as 2 with partitions down to 1024 rows; 4 = as 2
+                               with partitions of 1024 rows */
+    int32_t bloom_part;     /* rbloom: 0 = gather probe only; 1 = partitioned for filters of >= 16 MiB on
+                               member-rich input; 2 = such filters whatever the input; 3 = every filter, with
+                               partitions down to 1024 bits */
+    uint32_t workspace_mib; /* cap of the partitioned COBS probe's transient workspace (a larger call runs in
+                               ranges that reuse it) */
+    int32_t small_calls;    /* 1: calls of <= 4096 reads and <= 1 MiB go to the device in one round trip;
+                               0: every call takes the regular chunked pipeline */
+} xs_probe_options_t;
+int xs_bank_set_probe_options(xs_bank* bank, const xs_probe_options_t* options);
+int xs_bank_get_probe_options(const xs_bank* bank, xs_probe_options_t* options);
+
+/* Device bytes of the handle's transient workspace (staging, reads, hit
+ * matrices, the partitioned probes' entries and rows; not the bank image):
+ * held now, and the most held at once since the handle was created.  For
+ * memory planning beside other work on the GPU (288 GB per MI355X); a doc
+ * slice (xs_bank_open_docs) stages one ~32 MiB piece of whole rows at a time,
+ * never the whole bank. */
+int xs_bank_workspace_bytes(const xs_bank* bank, uint64_t* held, uint64_t* peak);
 
 void xs_bank_close(xs_bank* bank);
 

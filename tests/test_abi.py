@@ -59,3 +59,21 @@ def test_product_does_not_import_oracle():
         src = c.read_text()
         assert not re.search(r'#include\s+[<"][^>"]*oracle', src), c
         assert "xo_" not in re.sub(r"//.*", "", src), c
+
+
+def test_no_environment_reads_on_the_query_path():
+    """Path selection is a per-handle option (xs_bank_set_probe_options), not
+    an environment variable read per call: the probe
+    kernels' planners and the query code read no environment; what is left
+    are the reader's two operational settings, each read once per process
+    (function-local statics in xs_fastx.cpp)."""
+    csrc = ROOT / "xspect2_amd" / "csrc"
+    for f in sorted(csrc.glob("xs_probe_*.hip")) + [csrc / "xs_api.cpp", csrc / "xs_kernels.hip",
+                                                     csrc / "xs_internal.h", csrc / "xs_json.cpp"]:
+        assert "getenv" not in f.read_text(), f.name
+    fx = (csrc / "xs_fastx.cpp").read_text()
+    reads = re.findall(r'getenv\("([A-Z0-9_]+)"\)', fx)
+    assert sorted(reads) == ["XSPECT2_AMD_FASTX_TRACE", "XSPECT2_AMD_FX_FIRST_MB", "XSPECT2_AMD_FX_RING"], reads
+    for var in reads:  # each inside a static initialiser: read once
+        i = fx.index(f'getenv("{var}")')
+        assert "static" in fx[fx.rfind("\n", 0, fx.rfind("\n", 0, i)) - 200:i], var

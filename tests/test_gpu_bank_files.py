@@ -52,6 +52,10 @@ def test_classic_file_over_many_pieces(bank_mod, tmp_path):
         try:
             want = np.ascontiguousarray(rows[:, lo // 8: lo // 8 + (hi - lo + 7) // 8])
             assert np.array_equal(sl.download(), want.reshape(-1)), (lo, hi)
+            # a slice stages one ~32 MiB piece of whole rows at a time, never the whole
+            # 117 MB of rows (config 5's split is for banks one GPU cannot hold)
+            held, peak = sl.workspace_bytes()
+            assert held == 0 and 0 < peak <= 33 << 20 < S * 13, (lo, hi, peak)
         finally:
             sl.close()
 
@@ -71,3 +75,39 @@ def test_rbloom_file_over_many_pieces(bank_mod, tmp_path):
     from xspect2_amd._lib import XS_BANK_RBLOOM
     b = bank_mod.Bank.create_bloom(21, 100_000_007, 7)
     _roundtrip(bank_mod, b, tmp_path, XS_BANK_RBLOOM, "big.bloom")
+
+
+def test_failed_save_leaves_the_existing_file(bank_mod, tmp_path):
+    """xs_bank_save writes beside the destination and renames the file over it
+    once whole: a save that fails (here: the temporary name is
+    taken by a directory) returns an error and leaves the model already at
+    the path byte for byte, with no partial file; a save that succeeds
+    replaces it and leaves nothing else behind."""
+    import os
+
+    from xspect2_amd import _lib
+    from xspect2_amd._lib import XS_BANK_COBS_CLASSIC
+    D, S = 100, 300_007
+    b = bank_mod.Bank.create_cobs(21, 7, [S], D, [f"d{i}" for i in range(D)])
+    rng = np.random.default_rng(5)
+    old = rng.integers(0, 256, b.payload_bytes(), dtype=np.uint8)
+    b.upload(old)
+    path = tmp_path / "m.cobs_classic"
+    b.save(path)
+    before = path.read_bytes()
+    new = rng.integers(0, 256, b.payload_bytes(), dtype=np.uint8)
+    b.upload(new)
+    blocker = tmp_path / f"m.cobs_classic.xs-part-{os.getpid()}"
+    blocker.mkdir()
+    rc = _lib.load().xs_bank_save(b.handle, str(path).encode())
+    assert rc == _lib.XS_ERR_IO, rc
+    assert path.read_bytes() == before
+    blocker.rmdir()
+    b.save(path)
+    assert sorted(p.name for p in tmp_path.iterdir()) == ["m.cobs_classic"]
+    got = bank_mod.Bank.open(path, XS_BANK_COBS_CLASSIC, device=0)
+    try:
+        assert np.array_equal(got.download(), new)
+    finally:
+        got.close()
+        b.close()

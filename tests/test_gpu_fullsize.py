@@ -75,7 +75,7 @@ def _query(bank, torch, dev, r, r_offs, cols, step=1):
             tot.cpu().numpy().view(np.uint64), bank.probe_path())
 
 
-def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
+def test_config2_species_full_size(data, dev_inputs, oracle_mod):
     from xspect2_amd import _lib
     from xspect2_amd.bank import Bank, cobs_signature_size
     genomes, reads = data
@@ -88,9 +88,9 @@ def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
     torch.cuda.synchronize(dev)
     assert bank.info.device_bytes > 256 << 20  # larger than the Infinity Cache
 
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    bank.set_probe_options(cobs_part=0)
     h0, n0, t0, p0 = _query(bank, torch, dev, r, r_offs, D)
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "1")
+    bank.set_probe_options(cobs_part=1)
     h1, n1, t1, p1 = _query(bank, torch, dev, r, r_offs, D)
     assert p0 == _lib.XS_PATH_GATHER and p1 == _lib.XS_PATH_PARTITIONED
     assert np.array_equal(h0, h1), int((h0 != h1).sum())
@@ -114,9 +114,9 @@ def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
 
     # sparse sampling (step 3: 44 k-mers per read, probabilistic_filter_model.py:462) at full
     # size: both paths equal, the counts and totals consistent, the oracle sample equal
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
+    bank.set_probe_options(cobs_part=0)
     s0, m0, u0, _ = _query(bank, torch, dev, r, r_offs, D, step=3)
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
+    bank.set_probe_options(cobs_part=2)
     s1, m1, u1, q1 = _query(bank, torch, dev, r, r_offs, D, step=3)
     assert q1 == _lib.XS_PATH_PARTITIONED and np.array_equal(s0, s1) and np.array_equal(m0, m1)
     assert (m1 == (NK + 2) // 3).all() and np.array_equal(u1[:D], s1.sum(axis=0, dtype=np.uint64))
@@ -125,7 +125,7 @@ def test_config2_species_full_size(data, dev_inputs, oracle_mod, monkeypatch):
     bank.close()
 
 
-def test_genus_rbloom_full_size(data, dev_inputs, oracle_mod, monkeypatch):
+def test_genus_rbloom_full_size(data, dev_inputs, oracle_mod):
     from xspect2_amd import _lib
     from xspect2_amd.bank import Bank, bloom_parameters
     genomes, reads = data
@@ -135,9 +135,9 @@ def test_genus_rbloom_full_size(data, dev_inputs, oracle_mod, monkeypatch):
     bank.build_device(g, genomes.size, g_offs, D, None, stream=torch.cuda.current_stream(dev).cuda_stream)
     torch.cuda.synchronize(dev)
 
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "0")
+    bank.set_probe_options(bloom_part=0)
     h0, n0, t0, p0 = _query(bank, torch, dev, r, r_offs, 1)
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
+    bank.set_probe_options(bloom_part=2)
     h1, n1, t1, p1 = _query(bank, torch, dev, r, r_offs, 1)
     assert p0 == _lib.XS_PATH_GATHER and p1 == _lib.XS_PATH_PARTITIONED
     assert np.array_equal(h0, h1), int((h0 != h1).sum())
@@ -223,7 +223,7 @@ def test_config4_mlst_full_size(oracle_mod):
         bank.close()
 
 
-def test_config3_per_gpu_shard(data, dev_inputs, oracle_mod, monkeypatch):
+def test_config3_per_gpu_shard(data, dev_inputs, oracle_mod):
     """BASELINE config 3's per-GPU shard: 12.5 M x 150 bp reads (one eighth of
     100 M; seed 42 + rank, here rank 0 -> seed 43) against the replicated
     config-2 bank, in one device call.  The partitioned probe runs it in
@@ -247,7 +247,7 @@ def test_config3_per_gpu_shard(data, dev_inputs, oracle_mod, monkeypatch):
     bank.build_device(g, genomes.size, g_offs, D, torch.arange(D, dtype=torch.int32, device=dev), stream=s)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+        bank.set_probe_options(cobs_part=int(mode))
         hits = torch.empty((n, D), dtype=torch.int32, device=dev)
         nk = torch.empty(n, dtype=torch.int64, device=dev)
         tot = torch.zeros(D + 1, dtype=torch.int64, device=dev)

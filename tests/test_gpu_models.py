@@ -123,9 +123,9 @@ def test_species_fit_predict_save_load(tmp_path, species_dir, genomes, oracle_mo
         loaded.predict([Record("short", "ACGT")])
 
 
-def test_species_model_same_on_both_probe_paths(tmp_path, species_dir, genomes, monkeypatch):
+def test_species_model_same_on_both_probe_paths(tmp_path, species_dir, genomes):
     """predict(), predict_columnar() and the saved JSON are byte-identical whether
-    the species bank is probed directly (XSPECT2_AMD_COBS_PART=0) or through
+    the species bank is probed directly (probe option cobs_part=0) or through
     the partitioned pipeline (=3, forced on this small bank)."""
     from xspect2_amd.probabilistic_filter_model import ProbabilisticFilterModel
 
@@ -139,7 +139,7 @@ def test_species_model_same_on_both_probe_paths(tmp_path, species_dir, genomes, 
     write_fasta(recs, fa)
     outs = {}
     for mode in ("0", "3"):
-        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
+        model.index.set_probe_options(cobs_part=int(mode))
         res = model.predict(recs, step=2)
         col = model.predict_columnar(fa)
         path = tmp_path / f"out_{mode}.json"

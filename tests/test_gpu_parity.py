@@ -74,25 +74,21 @@ CLASSIC_CASES = [
 
 
 @pytest.mark.parametrize("D,k,h,sig", CLASSIC_CASES)
-def test_classic_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig):
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
-    _classic_case(xs, oracle_mod, D, k, h, sig)
+def test_classic_probe_matches_oracle(xs, oracle_mod, D, k, h, sig):
+    _classic_case(xs, oracle_mod, D, k, h, sig, opts={"cobs_part": 0})
 
 
 @pytest.mark.parametrize("D,k,h,sig", [c for c in CLASSIC_CASES if c[0] <= 128] + [(128, 21, 7, [70_001]),
                                                                                   (64, 31, 8, [300_007])])
 @pytest.mark.parametrize("mode,ws_mb", [("3", None), ("3", "1"), ("3", "2"), ("4", None), ("4", "2")])
-def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, D, k, h, sig, mode, ws_mb):
+def test_classic_partitioned_probe_matches_oracle(xs, oracle_mod, D, k, h, sig, mode, ws_mb):
     """The partitioned COBS probe (k-mer rows binned by bank partition, per-XCD
     L2-resident lookup, per-block AND + count) with partitions down to 1024
     rows (mode 3) or of exactly 1024 rows (mode 4: banks over 512 Ki rows get
     more than 512 partitions, whose runs are not padded), and workspaces of
     1-2 MiB (the bucket blocks then run in ranges of a few blocks that reuse
     it), on the classic cases of <= 128 docs: same hits, counts and totals."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
-    if ws_mb:
-        monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0)
+    _classic_case(xs, oracle_mod, D, k, h, sig, want_path=1 if h <= 8 else 0, opts=_opts(mode, ws_mb))
 
 
 def _random_partitioned_configs(n=48, seed=20261017):
@@ -110,39 +106,44 @@ def _random_partitioned_configs(n=48, seed=20261017):
 
 
 @pytest.mark.parametrize("D,k,h,sig,mode,ws_mb", _random_partitioned_configs())
-def test_partitioned_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, sig, mode, ws_mb):
+def test_partitioned_probe_random_configs(xs, oracle_mod, D, k, h, sig, mode, ws_mb):
     """Seeded random configurations of the partitioned COBS probe (docs 1-128,
     k 5-32, h 1-8, 1 k-200 k rows in partitions down to 1024 rows or of 1024
     rows, small workspaces that force block ranges, padded and unpadded runs):
     same hits, k-mer counts and totals as the oracle at steps 1, 2 and 7."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
-    if ws_mb:
-        monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", ws_mb)
-    _classic_case(xs, oracle_mod, D, k, h, [sig], want_path=1)
+    _classic_case(xs, oracle_mod, D, k, h, [sig], want_path=1, opts=_opts(mode, ws_mb))
 
 
 @pytest.mark.parametrize("mode,D", [("4", 100), ("4", 117), ("4", 128), ("3", 64), ("3", 128)])
-def test_partitioned_padding_threshold(xs, oracle_mod, monkeypatch, mode, D):
+def test_partitioned_padding_threshold(xs, oracle_mod, mode, D):
     """A 1 M-row bank cut into 1024-row partitions (mode 4: 977 of them, more
     than kCobsPadParts = 512, so the runs are not padded) and into 64
     partitions (mode 3: padded with all-ones pad rows), with the k-mer id in
     the row's top bits (D <= 117) and in the entries (D = 128): same hits,
     counts and totals as the oracle."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
-    _classic_case(xs, oracle_mod, D, 21, 7, [1_000_003], want_path=1)
+    _classic_case(xs, oracle_mod, D, 21, 7, [1_000_003], want_path=1, opts=_opts(mode))
 
 
-def test_partitioned_largest_partitions(xs, oracle_mod, monkeypatch):
+def test_partitioned_largest_partitions(xs, oracle_mod):
     """A bank of 2^27 + 15 rows (2 GiB on the device): 1025 partitions of 2^17
     rows would exceed kPartMax = 1024, so the plan doubles them to 2^18 rows
     (513 partitions: more than kCobsPadParts, unpadded runs); same hits as
     the oracle."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
-    _classic_case(xs, oracle_mod, 100, 21, 7, [(1 << 27) + 15], want_path=1)
+    _classic_case(xs, oracle_mod, 100, 21, 7, [(1 << 27) + 15], want_path=1, opts={"cobs_part": 2})
 
 
-def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
+def _opts(mode, ws_mb=None):
+    """Probe options of a parametrised case: cobs_part mode, optional workspace cap in MiB."""
+    o = {"cobs_part": int(mode)}
+    if ws_mb:
+        o["workspace_mib"] = int(ws_mb)
+    return o
+
+
+def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None, opts=None):
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D * 31 + k)
+    if opts:
+        gb.set_probe_options(**opts)
     rng = np.random.default_rng(D + k + h)
     reads = _reads(rng, 300, k)
     reads += [s[: int(rng.integers(k, len(s) + 1))] for s in seqs[:40]]      # true positives
@@ -164,15 +165,15 @@ def _classic_case(xs, oracle_mod, D, k, h, sig, want_path=None):
 
 @pytest.mark.parametrize("case", ["all_short", "one_read", "one_long_read", "empty_only", "tiny_reads",
                                   "empty_between"])
-def test_partitioned_degenerate_batches(xs, oracle_mod, monkeypatch, case):
+def test_partitioned_degenerate_batches(xs, oracle_mod, case):
     """Forced partitioned COBS probe on batches with no k-mers at all, a single
     read, a single read spanning many bucket blocks, only empty reads, reads
     of 1-3 k-mers (a bucket block spans more reads than it stages in LDS) and
     reads with runs of empty and short reads between them (reads sharing a
     first k-mer in the block's k-mer -> read map): hits, counts and totals
     equal the oracle's (zeros where no k-mer)."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=12)
+    gb.set_probe_options(cobs_part=3)
     rng = np.random.default_rng(5)
     genome = b"".join(seqs)
 
@@ -202,7 +203,7 @@ def test_partitioned_degenerate_batches(xs, oracle_mod, monkeypatch, case):
     gb.close()
 
 
-def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
+def test_partitioned_default_on_bank_over_mall(xs, oracle_mod):
     """Default mode on a classic bank larger than the Infinity Cache (17 M
     rows x 16 B = 272 MB on the device): the query takes the partitioned path
     by itself; host and device APIs, totals, best doc, steps 1 and 3, reads of
@@ -211,7 +212,6 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
     torch = pytest.importorskip("torch")
     from xspect2_amd import _lib
     from xspect2_amd.packing import pack_sequences
-    monkeypatch.delenv("XSPECT2_AMD_COBS_PART", raising=False)
     D, k, h, sig = 100, 21, 7, 17_000_011
     rng = np.random.default_rng(2024)
     nb = sig * 13
@@ -231,10 +231,10 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
         want[step] = (want_h, want_n)
         # host batches go in 8/32 MiB chunks, some under the default's k-mer
         # threshold (step 3 always): force the path so every chunk takes it
-        monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")
+        gb.set_probe_options(cobs_part=2)
         got_h, got_n = gb.query(reads, step=step)
         assert gb.probe_path() == _lib.XS_PATH_PARTITIONED
-        monkeypatch.delenv("XSPECT2_AMD_COBS_PART")
+        gb.set_probe_options(cobs_part=1)
         assert np.array_equal(got_n, want_n)
         assert np.array_equal(got_h, want_h), int((got_h != want_h).sum())
         tot, nk = gb.query_totals(reads, step=step)
@@ -242,10 +242,10 @@ def test_partitioned_default_on_bank_over_mall(xs, oracle_mod, monkeypatch):
         best, bh, bnk, btot = gb.query_best(reads, step=step, want_totals=True)
         assert np.array_equal(bh, want_h.max(axis=1)) and np.array_equal(bnk, want_n)
     assert 0 < int(want_h.sum())
-    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "64")
+    gb.set_probe_options(workspace_mib=64)
     got_h, got_n = gb.query(reads, step=3)
     assert np.array_equal(got_h, want_h) and np.array_equal(got_n, want_n)
-    monkeypatch.delenv("XSPECT2_AMD_CP_WS_MB")
+    gb.set_probe_options(workspace_mib=24 << 10)
     # device API on a torch stream
     pr = pack_sequences(reads)
     dev = torch.device("cuda", 0)
@@ -305,15 +305,15 @@ def _random_direct_configs(n=32, seed=20261018):
 
 
 @pytest.mark.parametrize("D,k,h,page,G", _random_direct_configs())
-def test_direct_probe_random_configs(xs, oracle_mod, monkeypatch, D, k, h, page, G):
+def test_direct_probe_random_configs(xs, oracle_mod, D, k, h, page, G):
     """Seeded random classic and compact banks through the direct probes
     (the partitioned path kept off): same hits, k-mer counts and totals as
     the oracle at steps 1 and 4, for random, document-derived, non-ACGT,
     short and multi-unit reads."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "0")
     rng = np.random.default_rng(D * 131 + k * 7 + h)
     sig = [int(x) for x in rng.integers(700, 5000, G)]
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, page=page, seed=D + k, per_doc=1)
+    gb.set_probe_options(cobs_part=0)
     reads = _reads(rng, 150, k) + [s[: int(rng.integers(k, len(s) + 1))] for s in seqs[:40]]
     reads += _reads(rng, 20, k, alphabet="ACGTNacgtnRY") + [b"", b"A" * max(k - 1, 0), seqs[0] * 3]
     for step in (1, 4):
@@ -371,9 +371,8 @@ def test_bank_file_roundtrip(xs, oracle_mod, tmp_path):
 
 @pytest.mark.parametrize("mode", ["0", "3"])
 @pytest.mark.parametrize("k", [21, 31, 5, 16, 32])
-def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode):
+def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, k, mode):
     """mode 0: direct probe; mode 3: partitioned probe with small partitions."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
     n_items = sum(len(s) for s in genome) - k + 1
@@ -381,6 +380,7 @@ def test_bloom_probe_and_build_match_oracle(xs, oracle_mod, monkeypatch, k, mode
     bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
     bf.build(genome)
     gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.set_probe_options(bloom_part=int(mode))
     gb.build(genome)
     assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
     reads = _reads(rng, 300, k, alphabet="ACGTacgtNRY") + [g[:500] for g in genome] + [genome[0]]
@@ -401,16 +401,16 @@ def _random_bloom_configs(n=24, seed=1017):
 
 
 @pytest.mark.parametrize("k,nbytes,K,seed", _random_bloom_configs())
-def test_bloom_partitioned_random_configs(xs, oracle_mod, monkeypatch, k, nbytes, K, seed):
+def test_bloom_partitioned_random_configs(xs, oracle_mod, k, nbytes, K, seed):
     """Seeded random rbloom filters (k 5-32, 1 kB-2 MB, K 1-8 bit indices)
     through the partitioned probe with small partitions; mixed-case / IUPAC
     reads: same hits, counts and totals as the oracle at steps 1 and 3."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
     rng = np.random.default_rng(seed)
     genome = _reads(rng, 8, k, alphabet="ACGTacgtN", min_len=k, max_len=5000)
     bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
     bf.build(genome)
     gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.set_probe_options(bloom_part=3)
     gb.build(genome)
     assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
     reads = _reads(rng, 400, k, alphabet="ACGTacgtNRY") + [g[:300] for g in genome] + [genome[0] * 2]
@@ -427,13 +427,12 @@ def test_bloom_partitioned_random_configs(xs, oracle_mod, monkeypatch, k, nbytes
 
 @pytest.mark.parametrize("mode", ["0", "3"])
 @pytest.mark.parametrize("k", [21, 31])
-def test_bloom_single_odd_byte_at_every_window_position(xs, oracle_mod, monkeypatch, k, mode):
+def test_bloom_single_odd_byte_at_every_window_position(xs, oracle_mod, k, mode):
     """Uppercase ACGT reads with one N, lower-case or IUPAC byte: the read is
     2k-1 long with the odd byte in the middle, so its k windows hold that byte
     at every window position 0..k-1.  Windows with an N take the permute
     complement, the others the per-byte Biopython table; half the reads are in
     the filter, so hits are non-trivial.  Both probe paths."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(k + 5)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     odd = b"NnacgtRYKMSWBDHVXU-*."
@@ -447,6 +446,7 @@ def test_bloom_single_odd_byte_at_every_window_position(xs, oracle_mod, monkeypa
     bf = oracle_mod.BloomFilter(np.zeros(50_021, dtype=np.uint8), 7, k)
     bf.build(members)
     gb = xs.Bank.create_bloom(k, 50_021, 7)
+    gb.set_probe_options(bloom_part=int(mode))
     gb.build(members)
     assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
     want_h, want_n = bf.query(reads)
@@ -459,20 +459,20 @@ def test_bloom_single_odd_byte_at_every_window_position(xs, oracle_mod, monkeypa
 @pytest.mark.parametrize("mode,k,K,nbytes", [("3", 21, 7, 200_003), ("3", 31, 5, 77_777), ("3", 16, 8, 1 << 20),
                                              ("1", 21, 7, 40 << 20), ("1", 21, 7, (1 << 31) + 4099),
                                              ("3", 21, 10, 100_003)])  # K > 8: gather path
-def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mode, k, K, nbytes):
+def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, mode, k, K, nbytes):
     """The partitioned rbloom probe (k-mer bit indices binned by filter
     partition, per-partition lookup, per-read count) against the oracle:
     hundreds of bucket blocks, ragged and multi-unit reads, empty and short
     reads, non-ACGT bytes, steps 1 and 3.  mode 1 with 40 MiB takes the
     default path (20 partitions of 2 MiB); the 2 GiB + 4 KiB filter needs
     4 MiB partitions (more than 1024 of 2 MiB) and a partial last one."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", mode)
     rng = np.random.default_rng(nbytes % 1000 + k)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = [acgt[rng.integers(0, 4, 60_000)].tobytes() for _ in range(3)]
     bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
     bf.build(genome)
     gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.set_probe_options(bloom_part=int(mode))
     gb.upload(bf.bits)
     reads = []
     for _ in range(2500):
@@ -498,14 +498,13 @@ def test_bloom_partitioned_probe_matches_oracle(xs, oracle_mod, monkeypatch, mod
     gb.close()
 
 
-def test_bloom_partitioned_threads_and_torch_stream(xs, oracle_mod, monkeypatch):
+def test_bloom_partitioned_threads_and_torch_stream(xs, oracle_mod):
     """Partitioned probe from 4 host threads on one handle (serialised by its
     mutex) and on a second handle at once, then through the device API on a
     torch stream: every answer equals the oracle's."""
     import threading
 
     import torch
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
     rng = np.random.default_rng(44)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = [acgt[rng.integers(0, 4, 80_000)].tobytes()]
@@ -514,6 +513,7 @@ def test_bloom_partitioned_threads_and_torch_stream(xs, oracle_mod, monkeypatch)
     bf.build(genome)
     banks = [xs.Bank.create_bloom(21, nbytes, 7) for _ in range(2)]
     for b in banks:
+        b.set_probe_options(bloom_part=2)
         b.upload(bf.bits)
     sets = []
     for t in range(6):
@@ -561,17 +561,17 @@ def test_bloom_partitioned_threads_and_torch_stream(xs, oracle_mod, monkeypatch)
 
 
 @pytest.mark.parametrize("step", [1, 2])
-def test_bloom_partitioned_many_short_reads(xs, oracle_mod, monkeypatch, step):
+def test_bloom_partitioned_many_short_reads(xs, oracle_mod, step):
     """Bucket blocks spanning more reads than they stage in LDS (reads of
     k..k+3 bytes: 1-4 k-mers each, so a 1024-k-mer block holds hundreds of
     reads) take the global read search; mixed with empty and sub-k reads."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
     rng = np.random.default_rng(31 + step)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = [acgt[rng.integers(0, 4, 20_000)].tobytes()]
     bf = oracle_mod.BloomFilter(np.zeros(300_007, dtype=np.uint8), 7, 21)
     bf.build(genome)
     gb = xs.Bank.create_bloom(21, 300_007, 7)
+    gb.set_probe_options(bloom_part=3)
     gb.upload(bf.bits)
     reads = []
     for _ in range(6000):
@@ -587,17 +587,17 @@ def test_bloom_partitioned_many_short_reads(xs, oracle_mod, monkeypatch, step):
 
 
 @pytest.mark.parametrize("step", [1, 3])
-def test_bloom_partitioned_empty_reads_between(xs, oracle_mod, monkeypatch, step):
+def test_bloom_partitioned_empty_reads_between(xs, oracle_mod, step):
     """Reads of 60-300 bytes with runs of empty and sub-k reads between them:
     the bucket block stages its reads in LDS and several share a first k-mer
     in its k-mer -> read map (the later, non-empty one holds it)."""
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "3")
     rng = np.random.default_rng(77 + step)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = acgt[rng.integers(0, 4, 50_000)].tobytes()
     bf = oracle_mod.BloomFilter(np.zeros(300_007, dtype=np.uint8), 7, 21)
     bf.build([genome])
     gb = xs.Bank.create_bloom(21, 300_007, 7)
+    gb.set_probe_options(bloom_part=3)
     gb.upload(bf.bits)
     reads = []
     for _ in range(800):
@@ -612,13 +612,12 @@ def test_bloom_partitioned_empty_reads_between(xs, oracle_mod, monkeypatch, step
     gb.close()
 
 
-def test_bloom_path_follows_member_fraction(xs, oracle_mod, monkeypatch):
+def test_bloom_path_follows_member_fraction(xs, oracle_mod):
     """Default mode on a 40 MiB filter: the first query takes the partitioned
     path; after a member-poor query (random reads) the next takes the gather
     path, and after a member-rich one the partitioned path again.  Every
     answer equals the oracle's."""
     from xspect2_amd import _lib
-    monkeypatch.delenv("XSPECT2_AMD_BLOOM_PART", raising=False)
     rng = np.random.default_rng(9)
     acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
     genome = [acgt[rng.integers(0, 4, 50_000)].tobytes()]
@@ -681,7 +680,7 @@ def test_device_api_with_torch_stream(xs, oracle_mod):
 
 
 @pytest.mark.parametrize("kind", ["cobs", "bloom"])
-def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
+def test_device_queries_on_mixed_streams(xs, oracle_mod, kind):
     """Queries on one handle from two torch streams and the handle's own host
     API, back to back with no synchronisation in between and growing batches
     (the shared workspace is reallocated mid-sequence): the library orders
@@ -689,12 +688,11 @@ def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
     the oracle's."""
     torch = pytest.importorskip("torch")
     from xspect2_amd.packing import pack_sequences
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "2")
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "2")  # partitioned COBS on the small bank,
-    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "4")   # in ranges that reuse a 4 MiB workspace
     rng = np.random.default_rng(77)
     if kind == "cobs":
         ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)
+        # partitioned COBS on the small bank, in ranges that reuse a 4 MiB workspace
+        gb.set_probe_options(cobs_part=2, workspace_mib=4)
         src = seqs
         cols = 100
     else:
@@ -703,6 +701,7 @@ def test_device_queries_on_mixed_streams(xs, oracle_mod, monkeypatch, kind):
         ob = oracle_mod.BloomFilter(np.zeros(20 << 20, dtype=np.uint8), 7, 21)
         ob.build(src)
         gb = xs.Bank.create_bloom(21, 20 << 20, 7)
+        gb.set_probe_options(bloom_part=2)
         gb.upload(ob.bits)
         cols = 1
     dev = torch.device("cuda", 0)
@@ -945,7 +944,7 @@ def test_host_batches_staged_in_chunks(xs, oracle_mod):
 
 
 @pytest.mark.parametrize("mode", ["0", "3"])
-def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, monkeypatch, mode):
+def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, mode):
     """xs_query_hits: the hit matrix narrowed on the device to uint8 / uint16
     ("auto" picks the narrowest that holds the batch's largest k-mer count)
     equals xs_query's uint32 matrix, on both probe paths, into a fresh or a
@@ -953,8 +952,8 @@ def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, monkeypatch, mode):
     too narrow for the reads is refused."""
     from xspect2_amd import _lib
     from xspect2_amd.bank import pinned_empty
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=4)
+    gb.set_probe_options(cobs_part=int(mode))
     rng = np.random.default_rng(4)
     genome = b"".join(seqs)
     reads = [genome[o:o + 150] for o in rng.integers(0, len(genome) - 150, 60_000)] + [b"", b"ACGT"]
@@ -977,7 +976,7 @@ def test_narrow_host_hits_and_pinned_out(xs, oracle_mod, monkeypatch, mode):
 
 
 @pytest.mark.parametrize("mode", ["0", "3"])
-def test_device_reads_narrowing_checks_real_counts(xs, oracle_mod, monkeypatch, mode):
+def test_device_reads_narrowing_checks_real_counts(xs, oracle_mod, mode):
     """xs_query_hits_device on device-resident reads (a device reader batch's
     form): several chunks, each planned from its own bytes, equal the oracle
     in u8 / u16, totals-only included; a caller's max_len below the longest
@@ -986,8 +985,8 @@ def test_device_reads_narrowing_checks_real_counts(xs, oracle_mod, monkeypatch, 
     import ctypes
     import torch
     from xspect2_amd import _lib
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", mode)
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=6)
+    gb.set_probe_options(cobs_part=int(mode))
     rng = np.random.default_rng(6)
     genome = b"".join(seqs)
     reads = [genome[o:o + 150] for o in rng.integers(0, len(genome) - 400, 300_000)] + [genome[:400]]
@@ -1020,12 +1019,11 @@ def test_device_reads_narrowing_checks_real_counts(xs, oracle_mod, monkeypatch, 
     gb.close()
 
 
-def test_pass_stats_of_the_partitioned_probe(xs, oracle_mod, monkeypatch):
+def test_pass_stats_of_the_partitioned_probe(xs, oracle_mod):
     """xs_bank_pass_stats: with profiling on, the partitioned probe's passes
     are timed on the launch stream; their sum is within the probe's own time."""
-    monkeypatch.setenv("XSPECT2_AMD_COBS_PART", "3")
-    monkeypatch.setenv("XSPECT2_AMD_CP_WS_MB", "2")  # several workspace ranges
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [30_011], seed=5)
+    gb.set_probe_options(cobs_part=3, workspace_mib=2)  # several workspace ranges
     reads = [s[:150] for s in seqs] * 200
     gb.set_profiling(True)
     gb.probe_stats()

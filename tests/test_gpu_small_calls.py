@@ -4,7 +4,7 @@ H2D copy, the direct probe kernel, one D2H copy, one sync) instead of
 query_host's unit pipeline and staging ring (GPU).
 
 Every answer must be the oracle's and the regular path's
-(XSPECT2_AMD_SMALL=0): hits in every width, k-mer counts, totals, the
+(the handle's small_calls option off): hits in every width, k-mer counts, totals, the
 per-read best doc; for classic banks of every probe-kernel family, compact
 (MLST) banks and rbloom filters, with empty reads, reads shorter than k,
 multi-unit reads (> 256 k-mers, counted atomically), non-ACGT bytes and
@@ -47,14 +47,14 @@ def _requests(rng, seqs, k):
             "long_only": [long_read]}
 
 
-def _check(xs, monkeypatch, gb, oracle_query, reqs, steps=(1, 3)):
+def _check(xs, gb, oracle_query, reqs, steps=(1, 3)):
     cols = gb.num_docs if gb.kind != 2 else 1
     for name, reads in reqs.items():
         for step in steps:
             want_h, want_n = oracle_query(reads, step)
             want_h = np.asarray(want_h, dtype=np.uint32).reshape(len(reads), cols)
-            for small in ("1", "0"):
-                monkeypatch.setenv("XSPECT2_AMD_SMALL", small)
+            for small in (1, 0):
+                gb.set_probe_options(small_calls=small)
                 got_h, got_n = gb.query(reads, step=step)
                 assert np.array_equal(got_n, want_n) and np.array_equal(got_h, want_h), (name, step, small)
                 assert gb.probe_path() == 0
@@ -72,14 +72,14 @@ def _check(xs, monkeypatch, gb, oracle_query, reqs, steps=(1, 3)):
 
 @pytest.mark.parametrize("D,k,h,sig", [(100, 21, 7, [40_000]), (8, 5, 2, [301]), (200, 21, 7, [12_007]),
                                        (1000, 21, 7, [3_001]), (2100, 21, 7, [4_001]), (129, 31, 1, [20_011])])
-def test_small_calls_classic(xs, oracle_mod, monkeypatch, D, k, h, sig):
+def test_small_calls_classic(xs, oracle_mod, D, k, h, sig):
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, seed=D + 3 * k)
     rng = np.random.default_rng(D * 7 + k)
-    _check(xs, monkeypatch, gb, lambda r, s: ob.query(r, step=s), _requests(rng, seqs, k))
+    _check(xs, gb, lambda r, s: ob.query(r, step=s), _requests(rng, seqs, k))
     gb.close()
 
 
-def test_small_calls_compact(xs, oracle_mod, monkeypatch):
+def test_small_calls_compact(xs, oracle_mod):
     """A compact (MLST-like) bank: 1100 docs in groups of 8 x 64 docs."""
     D, k, page = 1100, 31, 64
     per = 8 * page
@@ -87,25 +87,25 @@ def test_small_calls_compact(xs, oracle_mod, monkeypatch):
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, 1, sig, page=page, seed=9, per_doc=1)
     assert len(sig) == -(-D // per)
     rng = np.random.default_rng(21)
-    _check(xs, monkeypatch, gb, lambda r, s: ob.query(r, step=s), _requests(rng, seqs, k), steps=(1,))
+    _check(xs, gb, lambda r, s: ob.query(r, step=s), _requests(rng, seqs, k), steps=(1,))
     gb.close()
 
 
 @pytest.mark.parametrize("k", [21, 31])
-def test_small_calls_bloom(xs, oracle_mod, monkeypatch, k):
-    monkeypatch.setenv("XSPECT2_AMD_BLOOM_PART", "0")
+def test_small_calls_bloom(xs, oracle_mod, k):
     rng = np.random.default_rng(k + 100)
     genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=3000)
     nbytes, K = oracle_mod.BloomFilter.params(sum(len(s) for s in genome) - k + 1, 0.01)
     bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
     bf.build(genome)
     gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.set_probe_options(bloom_part=0)
     gb.upload(bf.bits)
-    _check(xs, monkeypatch, gb, lambda r, s: bf.query(r, step=s), _requests(rng, genome, k))
+    _check(xs, gb, lambda r, s: bf.query(r, step=s), _requests(rng, genome, k))
     gb.close()
 
 
-def test_over_the_limits_take_the_regular_path(xs, oracle_mod, monkeypatch):
+def test_over_the_limits_take_the_regular_path(xs, oracle_mod):
     """5000 reads (over 4096) and one 2 MiB read (over 1 MiB of sequence):
     the regular path, same answers."""
     ob, gb, seqs, _ = _pair(xs, oracle_mod, 100, 21, 7, [40_000], seed=5)

@@ -62,6 +62,16 @@ class BankInfo(ctypes.Structure):
     ]
 
 
+class ProbeOptions(ctypes.Structure):
+    """xs_probe_options_t: path selection of one bank handle (defaults = production)."""
+    _fields_ = [
+        ("cobs_part", ctypes.c_int32),
+        ("bloom_part", ctypes.c_int32),
+        ("workspace_mib", ctypes.c_uint32),
+        ("small_calls", ctypes.c_int32),
+    ]
+
+
 class FastxBatch(ctypes.Structure):
     _fields_ = [
         ("n", ctypes.c_uint64),
@@ -142,6 +152,9 @@ SIGNATURES = {
     "xs_bank_probe_rows": (_int, [_vp, ctypes.POINTER(_u64)]),
     "xs_bank_pass_stats": (_int, [_vp, _vp, _vp]),
     "xs_bank_probe_path": (_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    "xs_bank_set_probe_options": (_int, [_vp, ctypes.POINTER(ProbeOptions)]),
+    "xs_bank_get_probe_options": (_int, [_vp, ctypes.POINTER(ProbeOptions)]),
+    "xs_bank_workspace_bytes": (_int, [_vp, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     "xs_bank_close": (None, [_vp]),
     "xs_write_result_sections": (_int, [ctypes.c_char_p, _u64, _u64, _vp, _int, _vp, ctypes.c_char_p, _vp,
                                         ctypes.c_char_p, _vp, _vp, _vp, _u64, _vp, _int]),

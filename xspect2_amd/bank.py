@@ -99,20 +99,30 @@ class _HostPool:
     blocks kept here; a block goes back into service once no array refers to
     it any more (every numpy view of a block holds the block itself as its
     base, so the block's reference count says whether one is alive), and a
-    repeated query of the same size writes into pages faulted once.  At most
-    ``cap`` bytes are kept; larger requests get fresh arrays."""
+    repeated query of the same size writes into pages faulted once.  A block's
+    count is compared with the count it had when it was appended, measured
+    the same way, so the test does not depend on how the interpreter counts
+    getrefcount's own argument.  Consumers must hold the arrays (or views of
+    them), not only their buffer address.  At most ``cap`` bytes are kept
+    (2 GiB: config 2's 400 MB uint32 matrix and a few batches' rows); larger
+    requests get fresh arrays, and release_host_memory() gives the free blocks
+    back."""
 
-    def __init__(self, cap: int = 4 << 30, min_bytes: int = 8 << 20):
+    def __init__(self, cap: int = 2 << 30, min_bytes: int = 8 << 20):
         import sys
         import threading
         self._refs = sys.getrefcount
         self._lock = threading.Lock()  # queries from several threads (the reference's web workers)
         self.blocks: list[np.ndarray] = []
+        self._base: list[int] = []  # each block's reference count with no array of it alive
         self.cap, self.min_bytes = cap, min_bytes
 
     def _free(self, i: int) -> bool:
-        # references to block i: the list's and getrefcount's argument, and none from an array
-        return self._refs(self.blocks[i]) <= 2
+        return self._refs(self.blocks[i]) <= self._base[i]
+
+    def _pop(self, i: int) -> int:
+        self._base.pop(i)
+        return self.blocks.pop(i).size
 
     def empty(self, shape, dtype) -> np.ndarray:
         dtype = np.dtype(dtype)
@@ -130,12 +140,13 @@ class _HostPool:
         i = 0
         while kept + n > self.cap and i < len(self.blocks):  # drop free blocks, oldest first
             if self._free(i):
-                kept -= self.blocks.pop(i).size
+                kept -= self._pop(i)
             else:
                 i += 1
         if kept + n > self.cap:
             return np.empty(shape, dtype)
         self.blocks.append(np.empty(n, np.uint8))
+        self._base.append(self._refs(self.blocks[-1]))  # measured as _free measures it, no view yet
         return self.blocks[-1][:n].view(dtype).reshape(shape)
 
 
@@ -145,7 +156,7 @@ class _HostPool:
             freed, i = 0, 0
             while i < len(self.blocks):
                 if self._free(i):
-                    freed += self.blocks.pop(i).size
+                    freed += self._pop(i)
                 else:
                     i += 1
             return freed
@@ -453,6 +464,33 @@ class Bank:
         v = ctypes.c_int(0)
         check(load().xs_bank_probe_path(self.handle, ctypes.byref(v)))
         return int(v.value)
+
+    def workspace_bytes(self) -> tuple[int, int]:
+        """(held, peak) device bytes of this handle's transient workspace
+        (xs_bank_workspace_bytes; the bank image not included)."""
+        held, peak = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        check(load().xs_bank_workspace_bytes(self.handle, ctypes.byref(held), ctypes.byref(peak)))
+        return int(held.value), int(peak.value)
+
+    def probe_options(self) -> dict:
+        """This handle's path selection (xs_bank_get_probe_options)."""
+        o = _lib.ProbeOptions()
+        check(load().xs_bank_get_probe_options(self.handle, ctypes.byref(o)))
+        return {name: int(getattr(o, name)) for name, _ in o._fields_}
+
+    def set_probe_options(self, **changes) -> dict:
+        """Change this handle's path selection (xs_bank_set_probe_options):
+        cobs_part 0-4, bloom_part 0-3, workspace_mib, small_calls 0/1;
+        unnamed fields keep their values.  The defaults are the
+        production paths; every path gives the same results (the tests run
+        them all on one bank).  Returns the previous options."""
+        old = self.probe_options()
+        unknown = set(changes) - set(old)
+        if unknown:
+            raise TypeError(f"unknown probe options {sorted(unknown)}")
+        o = _lib.ProbeOptions(**{**old, **{k: int(v) for k, v in changes.items()}})
+        check(load().xs_bank_set_probe_options(self.handle, ctypes.byref(o)))
+        return old
 
     # ------------------------------------------------------------ lifetime
     def close(self) -> None:

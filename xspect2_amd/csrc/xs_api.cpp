@@ -70,9 +70,16 @@ const char kClassicMagic[] = "CLASSIC_INDEX";
 const char kCompactMagic[] = "COMPACT_INDEX";
 constexpr uint64_t kPad = 64;  // spare bytes after staged host reads
 
+// Device bytes a handle's workspace holds now and has held at most at once
+// (xs_bank_workspace_bytes).
+struct WsAcct {
+    uint64_t held = 0, peak = 0;
+};
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    WsAcct* acct = nullptr;  // the owning handle's workspace tally, if any
     // Workspace buffers of a bank handle: every enqueue that touches them ends
     // with a record of the handle's ws_ev (ws_leave), so waiting for that event
     // is enough before freeing the old buffer on growth.  Buffers without a
@@ -90,6 +97,7 @@ struct DevBuf {
                 (void)hipDeviceSynchronize();
             }
             (void)hipFree(p);
+            if (acct) acct->held -= cap;
         }
         p = nullptr;
         cap = 0;
@@ -98,6 +106,7 @@ struct DevBuf {
         if (e != hipSuccess)
             return fail(XS_ERR_HIP, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
         cap = want;
+        if (acct) acct->peak = std::max(acct->peak, acct->held += want);
         return XS_OK;
     }
     template <class T>
@@ -105,6 +114,7 @@ struct DevBuf {
     // give the memory back now (the caller has synchronised every stream that used it)
     void release() {
         if (p) (void)hipFree(p);
+        if (acct) acct->held -= cap;
         p = nullptr;
         cap = 0;
     }
@@ -136,14 +146,11 @@ void par_memcpy(void* dst, const void* src, size_t n, int threads) {
         return;
     }
     const size_t per = (n + threads - 1) / threads;
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads; ++t) {
-        const size_t a = per * t;
-        if (a >= n) break;
-        th.emplace_back([=] { memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, std::min(per, n - a)); });
-    }
-    memcpy(dst, src, std::min(per, n));
-    for (auto& x : th) x.join();
+    const int T = (int)((n + per - 1) / per);
+    xs::parallel_for(T, [=](int t) {
+        const size_t a = per * (size_t)t;
+        memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, std::min(per, n - a));
+    });
 }
 
 // Ask for transparent huge pages over the page-aligned part of a pageable
@@ -174,6 +181,7 @@ struct xs_bank {
     uint64_t pitch = 0;  // COBS: padded bytes per row
     uint64_t dev_bytes = 0;
     uint64_t nbytes = 0;  // rbloom filter bytes
+    WsAcct ws_acct;       // the workspace buffers below (not the image)
     DevBuf image;
     DevBuf groups;
     hipStream_t stream = nullptr;
@@ -191,6 +199,7 @@ struct xs_bank {
     bool bloom_pending = false;
     double member_frac = 1.0;
     int last_path = XS_PATH_GATHER;
+    ProbeOptions opt;               // path selection (xs_bank_set_probe_options)
     PinnedBuf stage[3];             // D2H staging ring for large host outputs (d2h_pageable: 2, HitSink: 3)
     hipEvent_t stage_ev[3] = {nullptr, nullptr, nullptr};
     PinnedBuf hstage[2];            // H2D staging ring for host read batches
@@ -220,7 +229,9 @@ struct xs_bank {
                           &pk_miss, &pk_aux, &bloom_tot}) {
             d->guard_ev = &ws_ev;
             d->guard_used = &ws_used;
+            d->acct = &ws_acct;
         }
+        small_d.acct = &ws_acct;
     }
 
     uint64_t sig_total() const {
@@ -381,6 +392,22 @@ int download_payload(xs_bank* b, void* host, uint64_t nbytes) {
 constexpr uint64_t kLoadPiece = 32u << 20;
 constexpr int kLoadSlots = 3;
 
+// run(a, e, &ok) over the ranges of [0, n) of up to `threads` (<= 8) threads, at least
+// 4 MiB each; false if any range failed
+template <class F>
+bool par_io(uint64_t n, int threads, F run) {
+    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>({(uint64_t)threads, 8, n / (4u << 20)}));
+    const uint64_t per = (n + T - 1) / T;
+    bool ok[8] = {true, true, true, true, true, true, true, true};
+    xs::parallel_for(T, [&](int t) {
+        const uint64_t a = per * (uint64_t)t;
+        if (a < n) run(a, std::min(n, a + per), &ok[t]);
+    });
+    for (bool o : ok)
+        if (!o) return false;
+    return true;
+}
+
 // [off, off + n) of fd into dst, split over up to `threads` threads; false on a
 // read error or a short file
 bool pread_all(int fd, uint8_t* dst, uint64_t n, uint64_t off, int threads) {
@@ -396,20 +423,14 @@ bool pread_all(int fd, uint8_t* dst, uint64_t n, uint64_t off, int threads) {
         }
         *ok = true;
     };
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n / (4u << 20)));
-    const uint64_t per = (n + T - 1) / T;
-    std::vector<std::thread> th;
-    bool ok[8] = {true, true, true, true, true, true, true, true};
-    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)), &ok[t]);
-    run(0, std::min(n, per), &ok[0]);
-    for (auto& x : th) x.join();
-    for (bool o : ok)
-        if (!o) return false;
-    return true;
+    return par_io(n, threads, run);
 }
 
-// nbytes of `path` from byte `pos` to the device at dst, on b->stream (synchronised on return)
-int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, uint8_t* dst) {
+// nbytes of `path` from byte `pos`, in pieces of `piece` bytes (the last one shorter) read by
+// up to 8 threads into a ring of pinned slots; emit(off, m, slot) enqueues piece [off, off + m)'s
+// transfer out of its slot on b->stream, which is synchronised on return
+template <class Emit>
+int stream_file(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, uint64_t piece, Emit emit) {
     const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
     if (fd < 0) return fail(XS_ERR_IO, "cannot open %s", path);
     struct Closer {
@@ -428,7 +449,7 @@ int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t n
                 if (ev[i]) (void)hipEventDestroy(ev[i]);
         }
     } drain{b->stream, ev};
-    const uint64_t piece = std::min<uint64_t>(kLoadPiece, std::max<uint64_t>(nbytes, 1));
+    piece = std::min<uint64_t>(piece, std::max<uint64_t>(nbytes, 1));
     for (int i = 0; i < kLoadSlots; ++i) {
         if (int rc = ring[i].ensure(piece)) return rc;
         HIPCHK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
@@ -441,11 +462,18 @@ int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t n
         const uint64_t m = std::min(piece, nbytes - off);
         if (!pread_all(fd, static_cast<uint8_t*>(ring[s].p), m, pos + off, threads))
             return fail(XS_ERR_IO, "%s: short read", path);
-        HIPCHK(hipMemcpyAsync(dst + off, ring[s].p, m, hipMemcpyHostToDevice, b->stream));
+        HIPCHK(emit(off, m, static_cast<const uint8_t*>(ring[s].p)));
         HIPCHK(hipEventRecord(ev[s], b->stream));
     }
     HIPCHK(hipStreamSynchronize(b->stream));
     return XS_OK;
+}
+
+// nbytes of `path` from byte `pos` to the device at dst, on b->stream (synchronised on return)
+int stream_file_to_device(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, uint8_t* dst) {
+    return stream_file(b, path, pos, nbytes, kLoadPiece, [&](uint64_t off, uint64_t m, const uint8_t* src) {
+        return hipMemcpyAsync(dst + off, src, m, hipMemcpyHostToDevice, b->stream);
+    });
 }
 
 // [off, off + n) of fd from src, split over up to `threads` threads; false on a write error
@@ -462,16 +490,7 @@ bool pwrite_all(int fd, const uint8_t* src, uint64_t n, uint64_t off, int thread
         }
         *ok = true;
     };
-    const int T = (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)threads, n / (4u << 20)));
-    const uint64_t per = (n + T - 1) / T;
-    std::vector<std::thread> th;
-    bool ok[8] = {true, true, true, true, true, true, true, true};
-    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)), &ok[t]);
-    run(0, std::min(n, per), &ok[0]);
-    for (auto& x : th) x.join();
-    for (bool o : ok)
-        if (!o) return false;
-    return true;
+    return par_io(n, threads, run);
 }
 
 // nbytes of the device buffer src to `path` from byte `pos` (the header before it is
@@ -480,9 +499,11 @@ bool pwrite_all(int fd, const uint8_t* src, uint64_t n, uint64_t off, int thread
 int stream_device_to_file(xs_bank* b, const char* path, uint64_t pos, uint64_t nbytes, const uint8_t* src) {
     const int fd = ::open(path, O_WRONLY | O_CLOEXEC);
     if (fd < 0) return fail(XS_ERR_IO, "cannot open %s for writing", path);
-    struct Closer {
+    struct Closer {  // an error path's close; the success path closes (and checks) below
         int fd;
-        ~Closer() { ::close(fd); }
+        ~Closer() {
+            if (fd >= 0) ::close(fd);
+        }
     } closer{fd};
     PinnedBuf ring[kLoadSlots];
     hipEvent_t ev[kLoadSlots] = {};
@@ -517,6 +538,8 @@ int stream_device_to_file(xs_bank* b, const char* path, uint64_t pos, uint64_t n
             return fail(XS_ERR_IO, "write to %s failed", path);
         if (i + kLoadSlots < pieces) HIPCHK(queue(i + kLoadSlots));
     }
+    closer.fd = -1;
+    if (::close(fd) != 0) return fail(XS_ERR_IO, "write to %s failed: %s", path, strerror(errno));
     return XS_OK;
 }
 
@@ -733,7 +756,7 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
     CobsPartPlan cplan;
     bool cobs_part = false;
     if (!bloom) {
-        cobs_part = cobs_part_plan(b->cobs_view(), b->k, in.n, in.plan_bytes(), step, &cplan) &&
+        cobs_part = cobs_part_plan(b->cobs_view(), b->k, in.n, in.plan_bytes(), step, b->opt, &cplan) &&
                     !(b->pk_nkc.ensure(cplan.nkc_bytes) || b->pk_kofs.ensure(cplan.nkc_bytes) ||
                       b->pk_scan.ensure(cplan.scan_bytes) || b->pk_entries.ensure(cplan.entry_bytes) ||
                       b->pk_tbl.ensure(cplan.tbl_bytes) || b->pk_aux.ensure(cplan.aux_bytes));
@@ -781,7 +804,8 @@ int run_query(xs_bank* b, const Inputs& in, uint32_t step, uint32_t* d_hits, uin
         }
         return true;
     };
-    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.plan_bytes(), step, b->member_frac, &plan) && part_ws()) {
+    if (bloom && bloom_part_plan(b->bloom_view(), in.n, in.plan_bytes(), step, b->member_frac, b->opt, &plan) &&
+        part_ws()) {
         path = XS_PATH_PARTITIONED;
         const BloomPartWs ws{b->pk_nkc.as<uint64_t>(), b->pk_kofs.as<uint64_t>(), b->pk_scan.p, b->pk_scan.cap,
                              b->pk_entries.as<uint64_t>(), b->pk_tbl.as<uint16_t>(), b->pk_miss.as<uint32_t>(),
@@ -910,10 +934,11 @@ template <class F>
 void par_ranges(uint64_t n, int threads, F fn) {
     const int T = n < (1u << 18) ? 1 : threads;
     const uint64_t per = (n + T - 1) / T;
-    std::vector<std::thread> th;
-    for (int t = 1; t < T && per * t < n; ++t) th.emplace_back(fn, t, per * t, std::min(n, per * (t + 1)));
-    fn(0, 0, std::min(n, per));
-    for (auto& x : th) x.join();
+    if (T == 1) return fn(0, 0, n);
+    xs::parallel_for(T, [&](int t) {
+        const uint64_t a = per * (uint64_t)t;
+        if (a < n) fn(t, a, std::min(n, a + per));
+    });
 }
 
 // ---- hit rows back to a host array, behind the probe ------------------------
@@ -940,10 +965,10 @@ void widen_rows(D* dst, const S* src, size_t n, int threads) {
         return;
     }
     const size_t per = (n + threads - 1) / threads;
-    std::vector<std::thread> th;
-    for (int t = 1; t < threads && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
-    run(0, std::min(per, n));
-    for (auto& x : th) x.join();
+    xs::parallel_for(threads, [&](int t) {
+        const size_t a = per * (size_t)t;
+        if (a < n) run(a, std::min(n, a + per));
+    });
 }
 
 class HitSink {
@@ -1023,7 +1048,22 @@ class HitSink {
             err_ = what;
         }
     }
+    // the worker thread's body: a C++ exception in it (a failed allocation, a copy-out
+    // task) becomes the call's error instead of ending the process
     void run() {
+        try {
+            copy_loop();
+        } catch (const std::bad_alloc&) {
+            fail_with(XS_ERR_NOMEM, "host memory allocation failed in the hit copier");
+        } catch (const std::exception& e) {
+            fail_with(XS_ERR_INTERNAL, e.what());
+        } catch (...) {
+            fail_with(XS_ERR_INTERNAL, "unknown C++ exception in the hit copier");
+        }
+        // whatever happened above: no DMA may still be writing a staging slot when the call returns
+        if (hipStreamSynchronize(b_->d2h_stream) != hipSuccess) fail_with(XS_ERR_HIP, "hit D2H failed");
+    }
+    void copy_loop() {
         if (hipSetDevice(b_->device) != hipSuccess) return fail_with(XS_ERR_HIP, "hipSetDevice failed in the hit copier");
         std::deque<Piece> inflight;
         int next_slot = 0;
@@ -1066,8 +1106,6 @@ class HitSink {
             if (int rc = copy_out(inflight.front())) fail_with(rc, "hit copy-out failed");
             inflight.pop_front();
         }
-        // after a failure too: no DMA may still be writing a staging slot when the call returns
-        if (hipStreamSynchronize(b_->d2h_stream) != hipSuccess) fail_with(XS_ERR_HIP, "hit D2H failed");
     }
 
     xs_bank* b_;
@@ -1294,18 +1332,12 @@ constexpr uint64_t kSmallUnitsPerBlock = 4;  // 4 waves taking 1 unit per grab (
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
-// XSPECT2_AMD_SMALL=0 sends every call through query_host (A/B, tests).
-bool small_enabled() {
-    const char* e = getenv("XSPECT2_AMD_SMALL");
-    return !e || atoi(e) != 0;
-}
-
 // *done = false: the call does not qualify (nothing was enqueued).  Hit rows
 // go to hits_host as hit_bytes-wide counts (the caller checked the width).
 int query_small(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t n, uint32_t step,
                 void* hits_host, int hit_bytes, uint64_t* nk_host, uint64_t* tot_host, bool* done) {
     *done = false;
-    if (b->profiling || n == 0 || n > kSmallReads || !small_enabled()) return XS_OK;
+    if (b->profiling || n == 0 || n > kSmallReads || !b->opt.small_calls) return XS_OK;
     const uint64_t base = offsets[0];
     for (uint64_t r = 0; r < n; ++r)
         if (offsets[r + 1] < offsets[r]) return fail(XS_ERR_ARG, "offsets must be non-decreasing");
@@ -1337,10 +1369,10 @@ int query_small(xs_bank* b, const char* seqs, const uint64_t* offsets, uint64_t 
         }
         (void)hipGetLastError();  // hipErrorNotReady is not an error here
         BloomPartPlan plan;
-        if (bloom_part_plan(b->bloom_view(), n, bytes, step, b->member_frac, &plan)) return XS_OK;
+        if (bloom_part_plan(b->bloom_view(), n, bytes, step, b->member_frac, b->opt, &plan)) return XS_OK;
     } else {
         CobsPartPlan plan;
-        if (cobs_part_plan(b->cobs_view(), b->k, n, bytes, step, &plan)) return XS_OK;
+        if (cobs_part_plan(b->cobs_view(), b->k, n, bytes, step, b->opt, &plan)) return XS_OK;
     }
     const int blocks = (int)std::min<uint64_t>((uint64_t)probe_grid(b), std::max<uint64_t>(1, (U + kSmallUnitsPerBlock - 1) / kSmallUnitsPerBlock));
     // device / pinned layout: [queue | offsets | unit_ofs | unit_read | seqs] [partials | hits]
@@ -1423,10 +1455,133 @@ int xs::set_error(int code, const char* msg) {
     return code;
 }
 
+// ---- persistent host workers (xs::parallel_for) ----------------------------
+// The library's data-parallel host passes (hit rows copied out and widened,
+// offsets rebased, files read and written in pieces, ids hashed, JSON
+// formatted) used to start and join fresh std::threads every call -- up to ~90
+// per 400 MB result and thousands per JSON save -- and an exception while
+// starting one left joinable threads behind (std::terminate).  Now they hand
+// their tasks to workers started once and kept for the process.
 namespace {
+
+class WorkerPool {
+  public:
+    void run(int n, const std::function<void(int)>& fn) {
+        if (n <= 1) {
+            if (n == 1) fn(0);
+            return;
+        }
+        Job job;
+        job.fn = &fn;
+        job.n = n;
+        job.left = n - 1;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            grow(n - 1);
+            jobs_.push_back(&job);
+        }
+        cv_.notify_all();
+        std::exception_ptr mine;
+        try {
+            fn(0);
+        } catch (...) {
+            mine = std::current_exception();
+        }
+        std::unique_lock<std::mutex> g(mu_);
+        while (job.next < job.n) {  // the caller takes its own job's unclaimed tasks (no worker free, or none started)
+            const int t = job.next++;
+            if (job.next == job.n) jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
+            g.unlock();
+            std::exception_ptr e;
+            try {
+                fn(t);
+            } catch (...) {
+                e = std::current_exception();
+            }
+            g.lock();
+            finish(&job, e);
+        }
+        job.done.wait(g, [&] { return job.left == 0; });
+        g.unlock();
+        if (mine) std::rethrow_exception(mine);
+        if (job.err) std::rethrow_exception(job.err);
+    }
+
+  private:
+    struct Job {
+        const std::function<void(int)>* fn = nullptr;
+        int n = 0, next = 1, left = 0;  // tasks 1..n-1 go to workers; left = those not finished
+        std::exception_ptr err;
+        std::condition_variable done;
+    };
+    static constexpr int kMaxWorkers = 31;
+
+    // under mu_: the next task of the oldest job that has one
+    bool claim(Job** j, int* t) {
+        while (!jobs_.empty()) {
+            Job* f = jobs_.front();
+            if (f->next < f->n) {
+                *j = f;
+                *t = f->next++;
+                if (f->next == f->n) jobs_.pop_front();
+                return true;
+            }
+            jobs_.pop_front();
+        }
+        return false;
+    }
+    // under mu_
+    void finish(Job* j, std::exception_ptr e) {
+        if (e && !j->err) j->err = e;
+        if (--j->left == 0) j->done.notify_all();
+    }
+    // under mu_: at least `want` workers (as many as the system lets us start, at most kMaxWorkers)
+    void grow(int want) {
+        want = std::min(want, kMaxWorkers);
+        while (workers_ < want) {
+            try {
+                std::thread([this] { loop(); }).detach();
+            } catch (...) {
+                return;  // fewer workers: the callers run the remaining tasks themselves
+            }
+            ++workers_;
+        }
+    }
+    void loop() {
+        std::unique_lock<std::mutex> g(mu_);
+        for (;;) {
+            Job* j = nullptr;
+            int t = 0;
+            while (!claim(&j, &t)) cv_.wait(g);
+            g.unlock();
+            std::exception_ptr e;
+            try {
+                (*j->fn)(t);
+            } catch (...) {
+                e = std::current_exception();
+            }
+            g.lock();
+            finish(j, e);
+        }
+    }
+
+    std::mutex mu_;
+    std::condition_variable cv_;
+    std::deque<Job*> jobs_;
+    int workers_ = 0;
+};
+
+// never destroyed: its detached workers outlive static destruction at exit
+WorkerPool& pool() {
+    static WorkerPool* p = new WorkerPool;
+    return *p;
+}
+
 std::mutex g_pin_mu;
 std::unordered_map<void*, size_t> g_pins;  // registered mappings: start -> length
 }  // namespace
+
+void xs::parallel_for(int n, const std::function<void(int)>& fn) { pool().run(n, fn); }
 
 int xs::pinned_alloc(size_t bytes, void** out) {
     *out = nullptr;
@@ -1445,11 +1600,9 @@ int xs::pinned_alloc(size_t bytes, void** out) {
             // registration below would otherwise fault them one by one)
             const int threads = (int)std::min<size_t>(8, std::max<size_t>(1, n / (size_t(16) << 20)));
             const size_t per = (n / kHuge + threads - 1) / threads * kHuge;
-            std::vector<std::thread> th;
-            for (int t = 1; t < threads && per * t < n; ++t)
-                th.emplace_back([=] { memset(p + per * t, 0, std::min(per, n - per * t)); });
-            memset(p, 0, std::min(per, n));
-            for (auto& x : th) x.join();
+            xs::parallel_for(threads, [=](int t) {
+                if (per * t < n) memset(p + per * t, 0, std::min(per, n - per * t));
+            });
             if (hipHostRegister(p, n, hipHostRegisterDefault) == hipSuccess) {
                 std::lock_guard<std::mutex> g(g_pin_mu);
                 g_pins[p] = n;
@@ -1587,15 +1740,25 @@ int xs_bank_open_docs(const char* path, int device, uint64_t doc_lo, uint64_t do
         b->names.assign(full->names.begin() + (ptrdiff_t)doc_lo, full->names.begin() + (ptrdiff_t)doc_hi);
         if (int rc = validate_geometry(b)) return rc;
         if (int rc = alloc_image(b)) return rc;
-        // whole rows to the device, then the rows' byte columns [doc_lo / 8, + page) into the image
+        // whole rows to the device a piece at a time (about kLoadPiece bytes of whole rows), each
+        // piece's byte columns [doc_lo / 8, + page) repacked into the image at its first row: the
+        // device holds the slice and one piece of whole rows, never the whole bank (config 5's
+        // column split exists for banks one GPU cannot hold)
         const uint64_t c0 = doc_lo / 8, P = b->page;
+        const uint64_t piece = std::max<uint64_t>(1, kLoadPiece / R) * R;
         HIPCHK(hipSetDevice(b->device));
         if (int rc = ws_enter(b, b->stream)) return rc;
-        if (int rc = b->tmp.ensure(S * R)) return rc;
-        if (int rc = stream_file_to_device(b, path, pos, S * R, b->tmp.as<uint8_t>())) return rc;
-        HIPCHK(launch_repack(b->tmp.as<uint8_t>() + c0, R, b->image.as<uint8_t>(), b->pitch, S, P, b->stream));
-        HIPCHK(hipStreamSynchronize(b->stream));
-        b->tmp.release();  // the whole rows (all docs) are not kept beside the slice
+        if (int rc = b->tmp.ensure(std::min<uint64_t>(piece, S * R))) return rc;
+        uint8_t* stage = b->tmp.as<uint8_t>();
+        // one staging buffer: the stream orders each piece's copy after the previous piece's repack
+        if (int rc = stream_file(b, path, pos, S * R, piece, [&](uint64_t off, uint64_t m, const uint8_t* src) {
+                hipError_t e = hipMemcpyAsync(stage, src, m, hipMemcpyHostToDevice, b->stream);
+                if (e != hipSuccess) return e;
+                return launch_repack(stage + c0, R, b->image.as<uint8_t>() + off / R * b->pitch, b->pitch, m / R, P,
+                                     b->stream);
+            }))
+            return rc;
+        b->tmp.release();  // the staging piece is not kept beside the slice
         *out = keep.release();
         return XS_OK;
     });
@@ -1711,7 +1874,14 @@ int xs_bank_save(xs_bank* b, const char* path) {
         std::lock_guard<std::mutex> lk(b->mu);
         HIPCHK(hipSetDevice(b->device));
         HIPCHK(hipDeviceSynchronize());
-        return b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, path) : write_cobs_file(b, path);
+        // the file is written beside its destination and renamed over it once whole: a failed
+        // save leaves no short or holed file at `path`, and an existing model there intact
+        const std::string tmp = std::string(path) + ".xs-part-" + std::to_string((long)getpid());
+        const int rc = b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, tmp.c_str()) : write_cobs_file(b, tmp.c_str());
+        if (rc == XS_OK && ::rename(tmp.c_str(), path) == 0) return XS_OK;
+        const int err = errno;
+        (void)::unlink(tmp.c_str());
+        return rc != XS_OK ? rc : fail(XS_ERR_IO, "cannot rename %s to %s: %s", tmp.c_str(), path, strerror(err));
     });
 }
 
@@ -2166,6 +2336,44 @@ int xs_bank_probe_path(const xs_bank* b, int* path) {
         if (!b || !path) return fail(XS_ERR_ARG, "null argument");
         std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);  // after any query in flight on the handle
         *path = b->last_path;
+        return XS_OK;
+    });
+}
+
+int xs_bank_set_probe_options(xs_bank* b, const xs_probe_options_t* o) {
+    return xs::guard([&]() -> int {
+        if (!b || !o) return fail(XS_ERR_ARG, "null argument");
+        if (o->cobs_part < 0 || o->cobs_part > 4) return fail(XS_ERR_ARG, "cobs_part must be 0..4");
+        if (o->bloom_part < 0 || o->bloom_part > 3) return fail(XS_ERR_ARG, "bloom_part must be 0..3");
+        if (o->workspace_mib < 1) return fail(XS_ERR_ARG, "workspace_mib must be >= 1");
+        if (o->small_calls != 0 && o->small_calls != 1) return fail(XS_ERR_ARG, "small_calls must be 0 or 1");
+        std::lock_guard<std::mutex> lk(b->mu);  // after any query in flight on the handle
+        b->opt.cobs_part = o->cobs_part;
+        b->opt.bloom_part = o->bloom_part;
+        b->opt.workspace_mib = o->workspace_mib;
+        b->opt.small_calls = o->small_calls;
+        return XS_OK;
+    });
+}
+
+int xs_bank_workspace_bytes(const xs_bank* b, uint64_t* held, uint64_t* peak) {
+    return xs::guard([&]() -> int {
+        if (!b || !held || !peak) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);
+        *held = b->ws_acct.held;
+        *peak = b->ws_acct.peak;
+        return XS_OK;
+    });
+}
+
+int xs_bank_get_probe_options(const xs_bank* b, xs_probe_options_t* o) {
+    return xs::guard([&]() -> int {
+        if (!b || !o) return fail(XS_ERR_ARG, "null argument");
+        std::lock_guard<std::mutex> lk(const_cast<xs_bank*>(b)->mu);
+        o->cobs_part = b->opt.cobs_part;
+        o->bloom_part = b->opt.bloom_part;
+        o->workspace_mib = b->opt.workspace_mib;
+        o->small_calls = b->opt.small_calls;
         return XS_OK;
     });
 }

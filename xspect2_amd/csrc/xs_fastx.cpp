@@ -719,10 +719,7 @@ int parse_window(xs_fastx* r, const char* lo, const char* hi, int* nparts) {
             pt.stop = cut[i + 1];
         }
     };
-    std::vector<std::thread> th;
-    for (int i = 1; i < T; ++i) th.emplace_back(work, i);
-    work(0);
-    for (auto& x : th) x.join();
+    xs::parallel_for(T, work);
     r->parts[T - 1].stop = hi;
     *nparts = T;
     for (int i = 0; i < T; ++i)
@@ -770,12 +767,7 @@ int pack_parts(xs_fastx* r, Batch& bt, int nparts) {
             dd += pt.desc_lens[j];
         }
     };
-    {
-        std::vector<std::thread> th;
-        for (int i = 1; i < nparts; ++i) th.emplace_back(pack, i);
-        if (nparts) pack(0);
-        for (auto& x : th) x.join();
-    }
+    xs::parallel_for(nparts, pack);
     offs[n] = sbytes;
     ioffs[n] = ibytes;
     doffs[n] = dbytes;
@@ -883,8 +875,17 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
             cv.notify_all();
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+    xs::ThreadGroup th;  // pread workers beside this thread, which queues each piece's DMA
+    try {
+        for (int t = 0; t < T; ++t) th.start(work, t);
+    } catch (...) {  // the workers already started stop at `failed` before the group joins them
+        {
+            std::lock_guard<std::mutex> g(mu);
+            failed = true;
+        }
+        cv.notify_all();
+        throw;
+    }
     int rc = XS_OK;
     for (size_t p = 0; p < pieces; ++p) {  // queue each piece's DMA as soon as it is in
         {
@@ -907,7 +908,7 @@ int load_text(xs_fastx* r, size_t lo, size_t hi, int ts) {
         cv.notify_all();
         if (rc) break;
     }
-    for (auto& x : th) x.join();
+    th.join();
     if (rc) return rc;
     if (failed) return xs::set_error(XS_ERR_IO, "read failed while loading the window's text");
     FXCHK(hipMemsetAsync(text.as<char>() + span, 0, padded + 16 - span, d.copy));
@@ -1454,10 +1455,7 @@ int xs_write_fasta(const char* path, int append, const char* seqs, const uint64_
                     }
                 }
             };
-            std::vector<std::thread> th;
-            for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-            work(0);
-            for (auto& x : th) x.join();
+            xs::parallel_for(T, work);
             for (int t = 0; t < T && ok; ++t) ok = fwrite(out[t].data(), 1, out[t].size(), f) == out[t].size();
         }
         if (fclose(f) != 0) ok = false;

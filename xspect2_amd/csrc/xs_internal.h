@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 
 #include <exception>
+#include <functional>
 #include <new>
+#include <thread>
 #include <type_traits>
+#include <utility>
 #include <vector>
 #include <stdint.h>
 
@@ -115,6 +118,24 @@ inline void pass_mark(PassRecorder* r, int tag, hipStream_t s) {
     if (r) (void)r->mark(tag, s);
 }
 
+// Probe path selection of one bank handle (xs_bank_set_probe_options; the
+// defaults are what every production query takes).  Read by the planners at
+// each query, under the handle's mutex; no environment variable changes them.
+constexpr uint32_t kCobsPartWsMiB = 24 << 10;  // default cap of a range's entries + rows
+struct ProbeOptions {
+    // partitioned COBS probe: 0 = direct probe only; 1 = automatic (classic banks of
+    // <= 128 docs of at least kCobsPartMinBankMiB, calls of at least kCobsPartMinKmers
+    // k-mers); 2 = every such bank and call; 3 = as 2 with partitions down to 1024
+    // rows; 4 = as 2 with partitions of 1024 rows (more than kCobsPadParts: unpadded runs)
+    int cobs_part = 1;
+    // partitioned rbloom probe: 0 = gather probe only; 1 = automatic (filters of
+    // >= 16 MiB on member-rich input); 2 = such filters whatever the input; 3 =
+    // every filter, with partitions down to 1024 bits
+    int bloom_part = 1;
+    uint32_t workspace_mib = kCobsPartWsMiB;  // cap of the partitioned COBS probe's workspace
+    int small_calls = 1;                      // 0: small host calls take the regular pipeline
+};
+
 // Partitioned rbloom probe (xs_probe_bloompart.hip): k-mers per bucket block,
 // most hash functions it takes, most filter partitions.
 constexpr int kPartKmers = 1024;
@@ -140,16 +161,15 @@ struct BloomPartWs {
 // False when the direct probe should run (small filter, K > kPartKMax, a
 // batch too large for the transient workspace, member-poor input -- the
 // previous query's member fraction below kPartMinMembers -- or
-// XSPECT2_AMD_BLOOM_PART=0).
+// opt.bloom_part = 0).
 constexpr double kPartMinMembers = 0.24;  // measured crossover, profiles/r01_bloom_crossover.txt
 bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32_t step, double member_frac,
-                     BloomPartPlan* plan);
+                     const ProbeOptions& opt, BloomPartPlan* plan);
 hipError_t launch_probe_bloom_part(const ReadView& rv, const BloomView& bv, const BloomPartPlan& plan,
                                    const BloomPartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
                                    hipStream_t s, PassRecorder* rec = nullptr);
 // Partitioned COBS probe (xs_probe_cobspart.hip) for classic banks of <= 128
 // docs (16-B rows) larger than the Infinity Cache.
-constexpr uint32_t kCobsPartWsMiB = 24 << 10;  // default cap of a range's entries + rows
 constexpr uint64_t kCobsPartMinKmers = 1ull << 23;  // default mode: smaller batches take the direct probe
 constexpr uint64_t kCobsPartMinBankMiB = 32;         // default mode: smaller banks take the direct probe
 struct CobsPartPlan {
@@ -178,9 +198,9 @@ struct PartWs {
 };
 // False when the direct probe should run (bank not classic 16-B rows, under
 // kCobsPartMinBankMiB, h > 8, fewer than kCobsPartMinKmers k-mers in the call, or
-// XSPECT2_AMD_COBS_PART=0).
+// opt.cobs_part = 0).
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
-                    CobsPartPlan* plan);
+                    const ProbeOptions& opt, CobsPartPlan* plan);
 hipError_t launch_probe_cobs_part(const ReadView& rv, const CobsView& bv, const CobsPartPlan& plan,
                                   const PartWs& ws, uint32_t* hits, uint64_t* partials, int blocks,
                                   hipStream_t s, PassRecorder* rec = nullptr);
@@ -268,6 +288,35 @@ int set_error(int code, const char* msg);
 // the mapped kind, unspecified for the hipHostMalloc kind.
 int pinned_alloc(size_t bytes, void** out);
 void pinned_free(void* p);
+
+// fn(t) for every t in [0, n): t = 0 on the calling thread, the others on the
+// library's persistent host workers (started once, reused by every call: no
+// thread is created per copy or pass).  Returns when all n have finished; an
+// exception thrown by any fn(t) is rethrown here, on the calling thread, after
+// the others have finished.  Calls from several threads at once share the
+// workers; the caller itself runs tasks while it waits, so a call always
+// completes even if no worker could be started.
+void parallel_for(int n, const std::function<void(int)>& fn);
+
+// Threads started for one call that must run beside it (a reader's loader, a
+// writer behind the formatting), joined on every exit path: when a start
+// fails, the threads already running finish before the exception leaves.
+struct ThreadGroup {
+    std::vector<std::thread> th;
+    template <class... A>
+    void start(A&&... a) {
+        th.emplace_back(std::forward<A>(a)...);
+    }
+    void join() {
+        for (auto& x : th)
+            if (x.joinable()) x.join();
+        th.clear();
+    }
+    ThreadGroup() = default;
+    ThreadGroup(const ThreadGroup&) = delete;
+    ThreadGroup& operator=(const ThreadGroup&) = delete;
+    ~ThreadGroup() { join(); }
+};
 
 // Every C-ABI entry point runs its body under guard(): a C++ exception (a
 // host vector that cannot be allocated, a worker thread that cannot start)

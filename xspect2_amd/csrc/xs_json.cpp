@@ -23,6 +23,7 @@
 #include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <numeric>
 #include <string>
 #include <thread>
@@ -215,30 +216,26 @@ int write_sections(const char* path, const Ctx<T>& c, const uint64_t* total_hits
         // an empty section is "{}" as json.dumps writes it (a shard without reads)
         const bool empty = n == 0 && section != 1;
         ok = fputs(heads[section], f) >= 0 && fputs(empty ? "{}" : "{\n", f) >= 0;
-        std::thread writer;
+        xs::ThreadGroup writer;  // the previous round's buffers go out while this round is formatted
         bool wok = true;
         int cur = 0;
         for (uint64_t b0 = 0; b0 < n && ok; b0 += block, cur ^= 1) {
             const uint64_t b1 = std::min(n, b0 + block);
             const uint64_t per = (b1 - b0 + NT - 1) / NT;
-            std::vector<std::thread> th;
-            auto work = [&, b0, b1, per, cur](int t) {
+            xs::parallel_for(NT, [&, b0, b1, per, cur](int t) {
                 out[cur][t].clear();
                 const uint64_t lo = b0 + per * t, hi = std::min(b1, lo + per);
                 if (lo < hi) format_block(c, section, lo, hi, out[cur][t]);
-            };
-            for (int t = 1; t < NT; ++t) th.emplace_back(work, t);
-            work(0);
-            for (auto& x : th) x.join();
-            if (writer.joinable()) writer.join();
+            });
+            writer.join();
             ok = wok;
             if (!ok) break;
-            writer = std::thread([&, cur] {
+            writer.start([&, cur] {
                 for (int t = 0; t < NT && wok; ++t)
                     wok = fwrite(out[cur][t].data(), 1, out[cur][t].size(), f) == out[cur][t].size();
             });
         }
-        if (writer.joinable()) writer.join();
+        writer.join();
         ok = ok && wok;
         if (!ok) break;
         if (section == 1) {
@@ -430,10 +427,10 @@ int xs_ids_hash128(const char* buf, const uint64_t* offs, uint64_t n, uint64_t* 
         };
         const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
         const uint64_t per = (n + T - 1) / T;
-        std::vector<std::thread> th;
-        for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
-        run(0, std::min(n, per));
-        for (auto& x : th) x.join();
+        xs::parallel_for((int)T, [&](int t) {
+            const uint64_t a = per * (uint64_t)t;
+            if (a < n) run(a, std::min(n, a + per));
+        });
         return XS_OK;
     });
 }
@@ -484,10 +481,10 @@ int xs_u64_member_mask(const uint64_t* keys, uint64_t n, const uint64_t* set, ui
         };
         const uint64_t T = std::min<uint64_t>(16, std::max<uint64_t>(1, n / (1u << 16)));
         const uint64_t per = (n + T - 1) / T;
-        std::vector<std::thread> th;
-        for (uint64_t t = 1; t < T && per * t < n; ++t) th.emplace_back(run, per * t, std::min(n, per * (t + 1)));
-        run(0, std::min(n, per));
-        for (auto& x : th) x.join();
+        xs::parallel_for((int)T, [&](int t) {
+            const uint64_t a = per * (uint64_t)t;
+            if (a < n) run(a, std::min(n, a + per));
+        });
         return XS_OK;
     });
 }
@@ -507,12 +504,7 @@ int xs_ids_has_duplicates(const char* buf, const uint64_t* offs, uint64_t n, int
         std::vector<uint64_t> hv(n);
         std::vector<uint64_t> cnt((size_t)T * kBuckets, 0);
         const uint64_t per = (n + T - 1) / T;
-        auto par = [&](auto&& fn) {
-            std::vector<std::thread> th;
-            for (int t = 1; t < T; ++t) th.emplace_back(fn, t);
-            fn(0);
-            for (auto& x : th) x.join();
-        };
+        auto par = [&](const std::function<void(int)>& fn) { xs::parallel_for(T, fn); };
         par([&](int t) {
             const uint64_t a = per * t, e = std::min(n, a + per);
             uint64_t* c = &cnt[(size_t)t * kBuckets];

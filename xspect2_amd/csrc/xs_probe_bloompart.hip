@@ -348,16 +348,6 @@ __global__ void __launch_bounds__(256) bloom_count_kernel(ReadView rv, const uin
 
 }  // namespace
 
-// XSPECT2_AMD_BLOOM_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for filters of >= 16 MiB on member-rich input; 2 =
-// partitioned for such filters whatever the input; 3 = partitioned for every
-// filter, with partitions down to 1024 bits (tests reach many partitions on
-// small filters).  Read per call.
-static int part_env() {
-    const char* e = getenv("XSPECT2_AMD_BLOOM_PART");
-    return e ? atoi(e) : 1;
-}
-
 // Partition shift for a filter of `mbits` bits: 2^24-bit (2 MiB) partitions
 // (2 MiB: 8.92 ms per config-2 step; 1 MiB 9.31, 512 KiB 10.86, 4 MiB 10.00),
 // halved down to 2^20 bits while that leaves fewer than 64 partitions (8 per
@@ -370,9 +360,14 @@ static uint32_t part_shift(uint64_t mbits, uint32_t pref, uint32_t floor) {
     return s;
 }
 
+// opt.bloom_part (ProbeOptions): 0 = direct probe only; 1 (default) =
+// partitioned probe for filters of >= 16 MiB on member-rich input; 2 =
+// partitioned for such filters whatever the input; 3 = partitioned for every
+// filter, with partitions down to 1024 bits (tests reach many partitions on
+// small filters).
 bool bloom_part_plan(const BloomView& bv, uint64_t n, uint64_t seq_bytes, uint32_t step, double member_frac,
-                     BloomPartPlan* plan) {
-    const int mode = part_env();
+                     const ProbeOptions& opt, BloomPartPlan* plan) {
+    const int mode = opt.bloom_part;
     if (mode <= 0 || bv.K == 0 || bv.K > (uint32_t)kPartKMax) return false;
     // member-poor input: the direct probe's early exit (2 bits first) wins
     if (mode == 1 && member_frac < kPartMinMembers) return false;

@@ -516,24 +516,19 @@ __global__ void part_zero_rows_kernel(const uint64_t* __restrict__ kofs, uint64_
 
 }  // namespace
 
-// XSPECT2_AMD_COBS_PART: 0 = direct probe only; 1 (default) = partitioned
-// probe for classic banks of <= 128 docs of at least kCobsPartMinBankMiB and
-// batches of at least kCobsPartMinKmers k-mers; 2 = partitioned for such banks
-// of any size; 3 = as 2 with partitions down to 1024 rows (tests reach many
-// partitions on small banks); 4 = as 2 with 1024-row partitions (tests reach
-// more than kCobsPadParts partitions: unpadded runs).  Read per call.
-static int cobs_part_env() {
-    const char* e = getenv("XSPECT2_AMD_COBS_PART");
-    return e ? atoi(e) : 1;
-}
-
 // Bucket blocks of 2048 k-mers: 12.71-12.85 ms per config-2 step against 13.81
 // at 1024 and 14.4 at 4096 when measured.
 constexpr uint32_t kCobsCK = 2048;
 
+// opt.cobs_part (ProbeOptions): 0 = direct probe only; 1 (default) = partitioned
+// probe for classic banks of <= 128 docs of at least kCobsPartMinBankMiB and
+// batches of at least kCobsPartMinKmers k-mers; 2 = partitioned for such banks
+// of any size; 3 = as 2 with partitions down to 1024 rows (tests reach many
+// partitions on small banks); 4 = as 2 with 1024-row partitions (tests reach
+// more than kCobsPadParts partitions: unpadded runs).
 bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_bytes, uint32_t step,
-                    CobsPartPlan* plan) {
-    const int mode = cobs_part_env();
+                    const ProbeOptions& opt, CobsPartPlan* plan) {
+    const int mode = opt.cobs_part;
     if (mode <= 0) return false;
     if (bv.G != 1 || bv.pitch != 16 || bv.D > 128 || bv.h == 0 || bv.h > (uint32_t)kMaxH || k > kMaxK) return false;
     const uint64_t sig = bv.sig0;
@@ -560,15 +555,14 @@ bool cobs_part_plan(const CobsView& bv, uint32_t k, uint64_t n, uint64_t seq_byt
     const uint64_t nblk = (kbound + ck - 1) / ck;
     const uint64_t P = parts(shift);
     // The bucket blocks run in ranges that reuse one workspace of at most
-    // XSPECT2_AMD_CP_WS_MB MiB of entries + rows (default kCobsPartWsMiB), so
+    // opt.workspace_mib MiB of entries + rows (default kCobsPartWsMiB), so
     // any batch size fits.  Runs are padded to 4 entries (64-B row pieces: 4.37
     // -> 3.51 ms for the lookup's write stream alone, tools/runwrite.hip) while
     // the pad slots fit the bucket block's LDS (P <= kCobsPadParts).
     const uint32_t pad = P <= kCobsPadParts ? 4 : 1;
     const uint64_t stride = ((uint64_t)ck * bv.h + (pad - 1) * P + 7) / 8 * 8;
     const uint64_t per_block = stride * (sizeof(uint32_t) + sizeof(uint4));
-    const char* ws_env = getenv("XSPECT2_AMD_CP_WS_MB");
-    const uint64_t cap = (uint64_t)std::max(1, ws_env ? atoi(ws_env) : (int)kCobsPartWsMiB) << 20;
+    const uint64_t cap = (uint64_t)std::max<uint32_t>(1, opt.workspace_mib) << 20;
     // a range holds fewer than 2^32 entries (the lookup's u32 positions)
     const uint64_t rblk = std::max<uint64_t>(1, std::min<uint64_t>({nblk, cap / per_block, ((1ull << 32) - 1) / stride}));
     plan->ck = ck;

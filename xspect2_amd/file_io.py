@@ -13,6 +13,7 @@ from __future__ import annotations
 import os
 
 import ctypes
+import functools
 from dataclasses import dataclass
 from pathlib import Path
 from typing import Iterator
@@ -33,14 +34,17 @@ def file_reader_device(index) -> int | None:
     """The device a model's file inputs are read on (the reader's device mode,
     text straight to HBM, records found there), or None for the host reader:
     device mode when the index is a GPU bank (bank.Bank), unless
-    XSPECT2_AMD_READER=host."""
-    import os
-
+    XSPECT2_AMD_READER=host (an operational setting, read once per process)."""
     from .bank import Bank
 
-    if os.environ.get("XSPECT2_AMD_READER", "device").strip().lower() == "host":
+    if _host_reader_forced():
         return None
     return index.device if isinstance(index, Bank) else None
+
+
+@functools.lru_cache(maxsize=None)
+def _host_reader_forced() -> bool:
+    return os.environ.get("XSPECT2_AMD_READER", "device").strip().lower() == "host"
 
 
 @dataclass

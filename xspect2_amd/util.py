@@ -24,10 +24,19 @@ def slugify(text: str) -> str:
     return text.strip("-")
 
 
+_DEVICE: int | None = None
+
+
 def default_device() -> int:
-    """GPU ordinal for banks: XSPECT2_AMD_DEVICE, else LOCAL_RANK, else 0."""
-    for var in ("XSPECT2_AMD_DEVICE", "LOCAL_RANK"):
-        v = os.environ.get(var)
-        if v is not None and v.strip():
-            return int(v)
-    return 0
+    """GPU ordinal for banks: XSPECT2_AMD_DEVICE, else LOCAL_RANK, else 0
+    (an operational setting: read at the first call, then kept)."""
+    global _DEVICE
+    if _DEVICE is None:
+        dev = 0
+        for var in ("XSPECT2_AMD_DEVICE", "LOCAL_RANK"):
+            v = os.environ.get(var)
+            if v is not None and v.strip():
+                dev = int(v)
+                break
+        _DEVICE = dev
+    return _DEVICE
