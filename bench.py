@@ -45,7 +45,7 @@ filter word (h or K per k-mer).  The direct kernels: one 128-byte L2 line fill p
 k-mer and doc group; rbloom: K dwords per k-mer; MLST: the 64-byte rows
 themselves, its banks being Infinity-Cache resident).  Both + the read bytes,
 hit matrix and per-read metadata; peak = 8.0 TB/s; traffic = PMC bytes per
-probe from profiles/r05_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
+probe from profiles/r06_traffic.json.  cpu_baseline: the C oracle (oracle/liboracle.so,
 OpenMP) on a bounded sample of the same reads and bank (rank 0, N=1 only);
 its hits are also compared with the GPU's; plus the reference's per-read loop
 shape on one core.  host_path: the same step from host buffers (PCIe).
@@ -119,7 +119,7 @@ def parse():
                     help="skip the end-to-end legs (the bench's reads as a FASTQ file -> totals / hit matrix)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
-    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r05_traffic.json"))
+    ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r06_traffic.json"))
     ap.add_argument("--rccl-world1", action="store_true",
                     help="rehearsal: a one-rank RCCL process group running every collective of the N>1 path "
                          "(the all-reduce of totals or the column exchange, the per-rank gathers and checks) "
@@ -552,7 +552,7 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:  # the whole partitioned pipeline per query (tools/gpu/gpu_r05_final.sh -> profiles/r05_traffic.json)
+    if wl.partitioned:  # the whole partitioned pipeline per query (profiles/r06_traffic.json: species from r05_pmc_cobspart.json, genus from r06_pmc_bloompart.json)
         traffic = None
         try:
             key = "species_partitioned" if wl.partitioned == "cobs" else "genus_partitioned"
@@ -567,7 +567,7 @@ def main():
         # the dominant pass against its own ceiling: L2 requests per launch (PMC,
         # scaled to this call's k-mers) over the lookup's live HIP-event time
         pmc_file, prefix = (("r05_pmc_cobspart.json", "xs::cobs_lookup_kernel") if wl.partitioned == "cobs" else
-                            ("r04_pmc_bloompart.json", "xs::bloom_lookup_kernel"))
+                            ("r06_pmc_bloompart.json", "xs::bloom_lookup_kernel"))
         try:
             pmc = json.loads((ROOT / "profiles" / pmc_file).read_text())["kernels"]
             key = next(k for k in pmc if k.startswith(prefix))

@@ -50,12 +50,12 @@ def test_classic_file_over_many_pieces(bank_mod, tmp_path):
     for lo, hi in ((0, 8), (8, 64), (96, 100), (0, 100)):
         sl = bank_mod.Bank.open(path, XS_BANK_COBS_CLASSIC, device=0, docs=(lo, hi))
         try:
+            # the open staged one ~32 MiB piece of whole rows at a time, never the whole 117 MB
+            # of rows (config 5's split is for banks one GPU cannot hold), and kept none
+            held, peak = sl.workspace_bytes()
+            assert held == 0 and 0 < peak <= 33 << 20 < S * 13, (lo, hi, held, peak)
             want = np.ascontiguousarray(rows[:, lo // 8: lo // 8 + (hi - lo + 7) // 8])
             assert np.array_equal(sl.download(), want.reshape(-1)), (lo, hi)
-            # a slice stages one ~32 MiB piece of whole rows at a time, never the whole
-            # 117 MB of rows (config 5's split is for banks one GPU cannot hold)
-            held, peak = sl.workspace_bytes()
-            assert held == 0 and 0 < peak <= 33 << 20 < S * 13, (lo, hi, peak)
         finally:
             sl.close()
 

@@ -48,16 +48,18 @@ def test_defaults_roundtrip_and_bad_values(bank_mod):
 
 
 def test_environment_does_not_select_paths(bank_mod, monkeypatch):
-    """A 48 MB classic bank and a call of 70 k reads (> 2^23 k-mers): the
-    default options take the partitioned probe even with round 5's variables
-    set to their 'off' values in the environment; the handle's option takes
-    the direct probe; the two answers are equal, and the small-call option
-    likewise changes the path of a 10-read call, not its answer."""
+    """A 48 MB classic bank and one device call of 70 k reads (> 2^23
+    k-mers): the default options take the partitioned probe even with round
+    5's variables set to their 'off' values in the environment; the handle's
+    option takes the direct probe; the two answers are equal, and the
+    small-call option likewise changes the path of a 10-read call, not its
+    answer."""
+    torch = pytest.importorskip("torch")
     from xspect2_amd import _lib
     for var, val in (("XSPECT2_AMD_COBS_PART", "0"), ("XSPECT2_AMD_BLOOM_PART", "0"),
                      ("XSPECT2_AMD_CP_WS_MB", "1"), ("XSPECT2_AMD_SMALL", "0")):
         monkeypatch.setenv(var, val)
-    D, S = 100, 3_000_017
+    D, S, n, L = 100, 3_000_017, 70_000, 150
     rng = np.random.default_rng(11)
     rows = np.frombuffer(rng.bytes(S * 13), np.uint8) | np.frombuffer(rng.bytes(S * 13), np.uint8)
     rows = rows.reshape(S, 13).copy()
@@ -65,18 +67,28 @@ def test_environment_does_not_select_paths(bank_mod, monkeypatch):
     b = bank_mod.Bank.create_cobs(21, 7, [S], D)
     try:
         b.upload(rows.reshape(-1))
-        acgt = np.frombuffer(b"ACGT", np.uint8)
-        reads = [acgt[rng.integers(0, 4, 150)].tobytes() for _ in range(70_000)]
-        part_h, part_n = b.query(reads)
-        assert b.probe_path() == _lib.XS_PATH_PARTITIONED
+        reads = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n * L)]
+        dev = torch.device("cuda", 0)
+        d_seq = torch.from_numpy(reads.copy()).to(dev)
+        d_off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+        s = torch.cuda.current_stream(dev).cuda_stream
+
+        def probe():
+            hits = torch.empty((n, D), dtype=torch.int32, device=dev)
+            tot = torch.zeros(D + 1, dtype=torch.int64, device=dev)
+            b.query_device(d_seq, n * L, d_off, n, 1, hits, None, tot, stream=s)
+            torch.cuda.synchronize(dev)
+            return hits.cpu().numpy(), tot.cpu().numpy(), b.probe_path()
+
+        part_h, part_t, path = probe()
+        assert path == _lib.XS_PATH_PARTITIONED
         b.set_probe_options(cobs_part=0)
-        direct_h, direct_n = b.query(reads)
-        assert b.probe_path() == _lib.XS_PATH_GATHER
-        assert np.array_equal(part_h, direct_h) and np.array_equal(part_n, direct_n)
-        assert int(part_h.sum()) > 0
-        few = reads[:10]
+        direct_h, direct_t, path = probe()
+        assert path == _lib.XS_PATH_GATHER
+        assert np.array_equal(part_h, direct_h) and np.array_equal(part_t, direct_t) and int(part_t[:D].sum()) > 0
+        few = [reads[i * L:(i + 1) * L].tobytes() for i in range(10)]
         want = b.query(few)[0]
         b.set_probe_options(small_calls=0)
-        assert np.array_equal(b.query(few)[0], want) and np.array_equal(want, direct_h[:10])
+        assert np.array_equal(b.query(few)[0], want) and np.array_equal(want, direct_h[:10].view(np.uint32))
     finally:
         b.close()
