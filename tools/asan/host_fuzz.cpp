@@ -5,16 +5,20 @@
 // Biopython / json.dumps is tested in tests/test_fastx.py and
 // tests/test_json_writer.py; this driver looks for memory errors only.
 //   make -C tools/asan run
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <random>
 #include <set>
+#include <stdexcept>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/xspect_hip.h"
+#include "../../xspect2_amd/csrc/xs_internal.h"
 
 namespace xs {
 int set_error(int code, const char* msg) {  // the library's version lives in xs_api.cpp (GPU side)
@@ -236,6 +240,38 @@ int main() {
         for (uint64_t i = 0; i < n; ++i)
             if (out[i] != (ref.count(keys[i]) ? 1 : 0)) ++unexpected;
     }
+    // the persistent host workers (xs::parallel_for): 6 caller threads at once, each running jobs of
+    // 1..20 tasks, some nested (a task starting its own job) and some throwing: every task runs
+    // exactly once, a throwing task's exception reaches its caller after the others have finished
+    {
+        std::vector<std::thread> callers;
+        std::atomic<int> bad{0};
+        for (int c = 0; c < 6; ++c)
+            callers.emplace_back([c, &bad] {
+                std::mt19937_64 r(c);
+                for (int job = 0; job < 300; ++job) {
+                    const int n = 1 + (int)(r() % 20);
+                    std::vector<std::atomic<int>> ran(n);
+                    for (auto& x : ran) x = 0;
+                    const int thrower = job % 7 == 0 ? (int)(r() % n) : -1;
+                    bool caught = false;
+                    try {
+                        xs::parallel_for(n, [&](int t) {
+                            ran[t]++;
+                            if (job % 5 == 0) xs::parallel_for(3, [](int) {});  // nested
+                            if (t == thrower) throw std::runtime_error("task failed");
+                        });
+                    } catch (const std::runtime_error&) {
+                        caught = true;
+                    }
+                    if (caught != (thrower >= 0)) ++bad;
+                    for (auto& x : ran)
+                        if (x != 1) ++bad;
+                }
+            });
+        for (auto& t : callers) t.join();
+        unexpected += bad.load();
+    }
     // repeated ids (xs_ids_has_duplicates): threaded passes over 300 k ids of 0..12 bytes, distinct
     // and with one repeat at random places, checked against std::set
     for (int trial = 0; trial < 6; ++trial) {
@@ -259,8 +295,8 @@ int main() {
         if (dup != (want ? 1 : 0)) ++unexpected;
     }
     printf("host sanitizer run: %d input files x 15 reader configurations + 12 byte-range parts, 20 JSON matrices, "
-           "20 id-key batches + a threaded one, 6 member masks, 6 threaded repeat checks; %d clean error returns, "
-           "%d on well-formed input\n",
+           "20 id-key batches + a threaded one, 6 member masks, 6 threaded repeat checks, 1800 worker-pool jobs from 6 threads (nested, throwing); %d clean error returns, "
+           "%d unexpected results\n",
            files, errors, unexpected);
     return unexpected ? 1 : 0;
 }
