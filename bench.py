@@ -552,7 +552,7 @@ def main():
         except Exception:
             traffic = None
 
-    if wl.partitioned:  # the whole partitioned pipeline per query (profiles/r06_traffic.json: species from r05_pmc_cobspart.json, genus from r06_pmc_bloompart.json)
+    if wl.partitioned:  # the whole partitioned pipeline per query (profiles/r06_traffic.json, from r06_pmc_cobspart.json and r06_pmc_bloompart.json)
         traffic = None
         try:
             key = "species_partitioned" if wl.partitioned == "cobs" else "genus_partitioned"
@@ -566,7 +566,7 @@ def main():
     if wl.partitioned and "lookup" in pass_ms:
         # the dominant pass against its own ceiling: L2 requests per launch (PMC,
         # scaled to this call's k-mers) over the lookup's live HIP-event time
-        pmc_file, prefix = (("r05_pmc_cobspart.json", "xs::cobs_lookup_kernel") if wl.partitioned == "cobs" else
+        pmc_file, prefix = (("r06_pmc_cobspart.json", "xs::cobs_lookup_kernel") if wl.partitioned == "cobs" else
                             ("r06_pmc_bloompart.json", "xs::bloom_lookup_kernel"))
         try:
             pmc = json.loads((ROOT / "profiles" / pmc_file).read_text())["kernels"]
