@@ -185,3 +185,39 @@ def test_index_finds_the_first_equal_id():
     with pytest.raises(ValueError):
         p.index("classified")
     assert PackedIds.of(ids).index("é") == 6
+
+
+def test_host_workers_from_threads_and_after_fork():
+    """The library's persistent host workers (xs_pool.cpp) behind the threaded
+    id passes: 8 Python threads hashing 1 M-id batches at once through the
+    C ABI (ctypes releases the GIL) all get the one-thread answer; a forked
+    child, which has none of the parent's workers, gets it too."""
+    import os
+    import threading
+
+    from xspect2_amd.packing import PackedIds
+    ids = PackedIds.of([f"read_{i}" for i in range(1_000_000)])
+    want = ids.hash128()  # threaded: 1 M ids / 2^16 per thread
+    got, errs = [None] * 8, []
+
+    def work(i):
+        try:
+            got[i] = ids.hash128()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs and all(np.array_equal(g, want) for g in got)
+    pid = os.fork()
+    if pid == 0:  # child: any failure is its exit code
+        ok = False
+        try:
+            ok = bool(np.array_equal(ids.hash128(), want) and ids.has_duplicates() is False)
+        finally:
+            os._exit(0 if ok else 1)
+    _, status = os.waitpid(pid, 0)
+    assert os.WIFEXITED(status) and os.WEXITSTATUS(status) == 0, status

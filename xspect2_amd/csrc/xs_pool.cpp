@@ -7,7 +7,10 @@
 // per 400 MB result and thousands per JSON save -- and an exception while
 // starting one left joinable threads behind (std::terminate).  Now they hand
 // their tasks to workers started once and kept for the process.
+#include <pthread.h>
+
 #include <algorithm>
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <exception>
@@ -126,10 +129,19 @@ class WorkerPool {
     int workers_ = 0;
 };
 
-// never destroyed: its detached workers outlive static destruction at exit
+// Never destroyed: its detached workers outlive static destruction at exit.  A
+// forked child (Python multiprocessing with the fork start method) has none of
+// the parent's workers and maybe a mutex a vanished worker held: it starts
+// from a fresh pool (the old one is left behind, unused).
+std::atomic<WorkerPool*> g_pool{nullptr};
+std::once_flag g_pool_once;
+
 WorkerPool& pool() {
-    static WorkerPool* p = new WorkerPool;
-    return *p;
+    std::call_once(g_pool_once, [] {
+        g_pool.store(new WorkerPool);
+        (void)pthread_atfork(nullptr, nullptr, [] { g_pool.store(new WorkerPool); });
+    });
+    return *g_pool.load();
 }
 }  // namespace
 
