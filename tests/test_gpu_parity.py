@@ -1079,3 +1079,84 @@ def test_mlst_query_matches_oracle(xs, oracle_mod, n_short, n_long, threshold):
         want_fs[o, new] = row[new]
     assert np.array_equal(sc, want_sc) and np.array_equal(first, want_first) and np.array_equal(fs, want_fs)
     gb.close()
+
+
+def _random_bloom_gather_configs(n=24, seed=20261020):
+    rng = np.random.default_rng(seed)
+    return [(int(rng.integers(5, 33)), int(rng.integers(64, 3_000_001)), int(rng.integers(1, 17)),
+             int(rng.integers(0, 1_000_000))) for _ in range(n)]
+
+
+@pytest.mark.parametrize("k,nbytes,K,seed", _random_bloom_gather_configs())
+def test_bloom_gather_random_configs(xs, oracle_mod, k, nbytes, K, seed):
+    """Seeded random rbloom filters through the gather probe (the path
+    member-poor input and small filters take: 2 bits first, the rest only for
+    k-mers that pass them): k 5-32, 64 B - 3 MB, K 1-16 bit indices, member
+    and random reads with lower case, N and IUPAC bytes, steps 1 and 4; the
+    device build, hits, counts and totals equal the oracle's."""
+    rng = np.random.default_rng(seed)
+    genome = _reads(rng, 6, k, alphabet="ACGTacgtN", min_len=k, max_len=4000)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+    bf.build(genome)
+    gb = xs.Bank.create_bloom(k, nbytes, K)
+    gb.set_probe_options(bloom_part=0)
+    gb.build(genome)
+    assert np.array_equal(gb.download(), bf.bits), "device-built filter differs"
+    reads = _reads(rng, 300, k, alphabet="ACGTacgtNRYKM") + [g[:int(rng.integers(k, len(g) + 1))] for g in genome]
+    reads += [b"", b"A" * max(k - 1, 0), genome[0] * 2]
+    for step in (1, 4):
+        want_h, want_n = bf.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert gb.probe_path() == 0
+        assert np.array_equal(got_n, want_n) and np.array_equal(got_h[:, 0], want_h)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert int(tot[0]) == int(want_h.sum()) and nk == int(want_n.sum())
+    gb.close()
+
+
+def _random_mlst_configs(n=16, seed=20261021):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        page = int(rng.choice([1, 2, 4, 8, 16, 32, 64]))
+        G = int(rng.integers(1, 5))
+        D = int(rng.integers((G - 1) * 8 * page + 1, G * 8 * page + 1))
+        out.append((D, page, G, int(rng.integers(15, 33)), int(rng.integers(1, 4)), int(rng.choice([1, 2, 3])),
+                    int(rng.choice([0, 1, 20, 50])), int(rng.integers(0, 1 << 30))))
+    return out
+
+
+@pytest.mark.parametrize("D,page,G,k,h,step,threshold,seed", _random_mlst_configs())
+def test_mlst_query_random_configs(xs, oracle_mod, D, page, G, k, h, step, threshold, seed):
+    """Seeded random compact banks through xs_mlst_query (one MLST locus per
+    call, probabilistic_filter_mlst_model.py:192-303): 1-4 groups of pages
+    1-64, k 15-32, h 1-3, steps 1-3, thresholds 0 / 1 / 20 / 50; the direct
+    rows of short sequences, and per long sequence's chunks the sums of the
+    scores over the threshold, the first passing chunk and its score, equal
+    the reference's loop restated over the oracle's chunk rows."""
+    rng = np.random.default_rng(seed)
+    sig = [int(x) for x in rng.integers(700, 4000, G)]
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, h, sig, page=page, seed=seed % 1000, per_doc=1)
+    short = [s[:int(rng.integers(k + 1, len(s) + 1))] for s in seqs[:int(rng.integers(0, 30))]]
+    chunks, owner = [], []
+    n_long = int(rng.integers(0, 8))
+    for j in range(n_long):
+        for _ in range(int(rng.integers(1, 9))):
+            chunks.append(seqs[int(rng.integers(0, D))][:int(rng.integers(k + 1, 900))])
+            owner.append(j)
+    n_owners = n_long + 1
+    h_, sc, first, fs = gb.mlst_query(short, chunks, owner, n_owners, step, threshold)
+    want_h = ob.query(short, step=step)[0] if short else np.zeros((0, D), np.uint32)
+    assert np.array_equal(h_, want_h)
+    rows = ob.query(chunks, step=step)[0] if chunks else np.zeros((0, D), np.uint32)
+    want_sc = np.zeros((n_owners, D), np.uint64)
+    want_first = np.full((n_owners, D), 0xFFFFFFFF, np.uint32)
+    want_fs = np.zeros((n_owners, D), np.uint32)
+    for c, (o, row) in enumerate(zip(owner, rows)):
+        m = row > threshold
+        want_sc[o, m] += row[m]
+        new = m & (want_first[o] == 0xFFFFFFFF)
+        want_first[o, new] = c
+        want_fs[o, new] = row[new]
+    assert np.array_equal(sc, want_sc) and np.array_equal(first, want_first) and np.array_equal(fs, want_fs)
+    gb.close()
