@@ -1753,12 +1753,18 @@ int xs_bank_save(xs_bank* b, const char* path) {
         HIPCHK(hipDeviceSynchronize());
         // the file is written beside its destination and renamed over it once whole: a failed
         // save leaves no short or holed file at `path`, and an existing model there intact
-        const std::string tmp = std::string(path) + ".xs-part-" + std::to_string((long)getpid());
-        const int rc = b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, tmp.c_str()) : write_cobs_file(b, tmp.c_str());
-        if (rc == XS_OK && ::rename(tmp.c_str(), path) == 0) return XS_OK;
-        const int err = errno;
-        (void)::unlink(tmp.c_str());
-        return rc != XS_OK ? rc : fail(XS_ERR_IO, "cannot rename %s to %s: %s", tmp.c_str(), path, strerror(err));
+        struct Partial {  // removed on every way out (an exception included) but the rename
+            std::string path;
+            bool renamed = false;
+            ~Partial() {
+                if (!renamed) (void)::unlink(path.c_str());
+            }
+        } tmp{std::string(path) + ".xs-part-" + std::to_string((long)getpid())};
+        const char* t = tmp.path.c_str();
+        if (int rc = b->kind == XS_BANK_RBLOOM ? write_bloom_file(b, t) : write_cobs_file(b, t)) return rc;
+        if (::rename(t, path) != 0) return fail(XS_ERR_IO, "cannot rename %s to %s: %s", t, path, strerror(errno));
+        tmp.renamed = true;
+        return XS_OK;
     });
 }
 
