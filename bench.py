@@ -119,6 +119,9 @@ def parse():
                     help="skip the end-to-end legs (the bench's reads as a FASTQ file -> totals / hit matrix)")
     ap.add_argument("--totals-only", action="store_true",
                     help="diagnostic: probe without writing the per-read hit matrix (totals only)")
+    ap.add_argument("--probe-path", default="auto", choices=["auto", "direct", "partitioned"],
+                    help="diagnostic: the banks' probe path (xs_bank_set_probe_options; auto = the production "
+                         "choice, direct = the gather kernels, partitioned = the partitioned probes forced)")
     ap.add_argument("--traffic-json", default=str(ROOT / "profiles" / "r06_traffic.json"))
     ap.add_argument("--rccl-world1", action="store_true",
                     help="rehearsal: a one-rank RCCL process group running every collective of the N>1 path "
@@ -277,6 +280,11 @@ class Workload:
             reads, loci_info = self._mlst(args, dev, s)
             self.config.update(loci=len(self.banks), **loci_info)
             self.kernel = "probe_cobs_wide<31,1,C=4,P=2,G=3> (compact, 3 groups x 4 chunk lanes)"
+        if args.probe_path != "auto":  # diagnostic runs of one path (the default line never sets it)
+            mode = {"direct": 0, "partitioned": 2}[args.probe_path]
+            for b in self.banks:
+                b.set_probe_options(cobs_part=mode, bloom_part=mode)
+            self.config.update(probe_path=args.probe_path)
         self.reads = reads
         self.n = reads.shape[0]
         self.seq_bytes = reads.size
