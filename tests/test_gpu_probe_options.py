@@ -92,3 +92,50 @@ def test_environment_does_not_select_paths(bank_mod, monkeypatch):
         assert np.array_equal(b.query(few)[0], want) and np.array_equal(want, direct_h[:10].view(np.uint32))
     finally:
         b.close()
+
+
+def test_options_change_while_other_threads_query(bank_mod, oracle_mod):
+    """One thread flips the handle's probe options (direct / partitioned COBS,
+    small calls on / off, 1-4 MiB workspaces) while three others query the
+    same handle: every answer equals the oracle's (options apply between
+    queries, under the handle's mutex; round 5's setenv could race the
+    library's getenv on worker threads)."""
+    import threading
+
+    from test_gpu_parity import _pair, _reads
+    ob, gb, seqs, _ = _pair(bank_mod, oracle_mod, 100, 21, 7, [30_011], seed=21)
+    rng = np.random.default_rng(21)
+    genome = b"".join(seqs)
+    sets = []
+    for n in (5, 300, 3000, 9000):
+        reads = [genome[o:o + 150] for o in rng.integers(0, len(genome) - 150, n)] + _reads(rng, 20, 21)
+        sets.append((reads, ob.query(reads)))
+    stop, errors = threading.Event(), []
+
+    def flip():
+        i = 0
+        while not stop.is_set():
+            gb.set_probe_options(cobs_part=(0, 2, 3)[i % 3], small_calls=i % 2, workspace_mib=1 + i % 4)
+            i += 1
+
+    def work(t):
+        try:
+            for rep in range(6):
+                reads, (want_h, want_n) = sets[(t + rep) % len(sets)]
+                got_h, got_n = gb.query(reads)
+                if not (np.array_equal(got_h, want_h) and np.array_equal(got_n, want_n)):
+                    errors.append(f"thread {t} rep {rep}: mismatch")
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    flipper = threading.Thread(target=flip)
+    workers = [threading.Thread(target=work, args=(t,)) for t in range(3)]
+    flipper.start()
+    for w in workers:
+        w.start()
+    for w in workers:
+        w.join()
+    stop.set()
+    flipper.join()
+    gb.close()
+    assert not errors, errors
