@@ -72,6 +72,10 @@ def lib():
             ctypes.c_uint32, ctypes.c_int, _u8p, _u64p, ctypes.c_uint64,
             ctypes.c_uint32, _u32p, _u64p, ctypes.c_int,
         ]
+        L.xo_cobs_query_batched.restype = ctypes.c_int
+        L.xo_cobs_query_batched.argtypes = L.xo_cobs_query.argtypes
+        L.xo_xxh64_terms_check.restype = ctypes.c_uint64
+        L.xo_xxh64_terms_check.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64]
         L.xo_cobs_build.restype = ctypes.c_int
         L.xo_cobs_build.argtypes = [
             _u8p, _u64p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
@@ -209,6 +213,20 @@ class CobsBank:
     def query(self, seqs, step=1, threads=0):
         buf, offs = pack(seqs)
         return self.query_packed(buf, offs, step, threads)
+
+    def query_packed_batched(self, buf, offs, step=1, threads=0):
+        """query_packed through xo_cobs_query_batched: the same answer,
+        computed as a tuned CPU port would (bench.py's cpu_baseline)."""
+        n = len(offs) - 1
+        hits = np.zeros((n, self.D), dtype=np.uint32)
+        nk = np.zeros(n, dtype=np.uint64)
+        rc = lib().xo_cobs_query_batched(
+            _p(self.rows, _u8p), _p(self.sig, _u64p), len(self.sig), self.P, self.D, self.h,
+            self.k, _p(buf, _u8p), _p(offs, _u64p), n, step, _p(hits, _u32p), _p(nk, _u64p),
+            int(threads))
+        if rc != 0:
+            raise ValueError(f"xo_cobs_query_batched failed ({rc})")
+        return hits, nk
 
     # -- pure python (python-xxhash) restatement, small inputs only --------
     def query_py(self, seqs, step=1):

@@ -338,6 +338,189 @@ int xo_cobs_query(const uint8_t* rows, const uint64_t* sig, uint64_t G, uint64_t
     return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* The same query, batched for the CPU baseline (bench.py cpu_baseline): */
+/* identical hits and counts (tests/test_oracle.py checks them against   */
+/* xo_cobs_query bit for bit), computed the way a tuned CPU port would:  */
+/*  - XXH64 of a k < 32 byte key: the seed enters only through the start */
+/*    value, so each 8/4/1-byte term is computed once per k-mer and the  */
+/*    h seeds run the short chain (xo_xxh64 is the pinned reference);    */
+/*  - the row addresses of every sampled k-mer of a read are computed    */
+/*    first and the rows prefetched kLook k-mers ahead (memory-level     */
+/*    parallelism instead of one dependent miss after another);          */
+/*  - counts are added 4 docs at a time: one table lookup per mask       */
+/*    nibble into 16-bit lanes, flushed to the uint32 output every 65535 */
+/*    k-mers.                                                            */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t t8[4];  /* xxh64_round(0, chunk) of each 8-byte chunk */
+    uint64_t t4;     /* 4-byte chunk * P1 */
+    uint64_t t1[4];  /* trailing bytes * P5 */
+    int n8, has4, n1;
+    uint64_t len;
+} xo_xxh64_terms;
+
+static inline void xxh64_terms(const uint8_t* p, uint64_t len, xo_xxh64_terms* t) {
+    const uint8_t* end = p + len;
+    t->len = len;
+    t->n8 = 0;
+    while (p + 8 <= end) { t->t8[t->n8++] = xxh64_round(0, rd64(p)); p += 8; }
+    t->has4 = p + 4 <= end;
+    if (t->has4) { t->t4 = (uint64_t)rd32(p) * P64_1; p += 4; }
+    t->n1 = 0;
+    while (p < end) t->t1[t->n1++] = (uint64_t)(*p++) * P64_5;
+}
+
+static inline uint64_t xxh64_seeded(const xo_xxh64_terms* t, uint64_t seed) {
+    uint64_t h = seed + P64_5 + t->len;
+    for (int i = 0; i < t->n8; ++i) { h ^= t->t8[i]; h = rotl64(h, 27) * P64_1 + P64_4; }
+    if (t->has4) { h ^= t->t4; h = rotl64(h, 23) * P64_2 + P64_3; }
+    for (int i = 0; i < t->n1; ++i) { h ^= t->t1[i]; h = rotl64(h, 11) * P64_1; }
+    return xxh64_avalanche(h);
+}
+
+/* xo_xxh64 through the batched form: the tests compare the two for every
+ * length 0..31 and many seeds (the batched query relies on it) */
+uint64_t xo_xxh64_terms_check(const void* data, uint64_t len, uint64_t seed) {
+    if (len >= 32) return xo_xxh64(data, len, seed);
+    xo_xxh64_terms t;
+    xxh64_terms((const uint8_t*)data, len, &t);
+    return xxh64_seeded(&t, seed);
+}
+
+static uint64_t nibble_lanes[16];  /* bit i of a nibble -> 16-bit lane i */
+
+/* a % d without a division: q = mulhi(a, floor((2^64-1)/d)) undershoots the
+ * quotient by at most 2, so at most two corrections follow */
+static inline uint64_t mod_barrett(uint64_t a, uint64_t d, uint64_t magic) {
+    const uint64_t q = (uint64_t)(((__uint128_t)a * magic) >> 64);
+    uint64_t r = a - q * d;
+    while (r >= d) r -= d;
+    return r;
+}
+
+/* dst[0..P) &= src[0..P) in 8-byte words (the last word overlapping when P
+ * is not a multiple of 8; AND is idempotent, so the overlap is harmless) */
+static inline void and_row(uint8_t* dst, const uint8_t* src, uint64_t P) {
+    if (P < 8) {
+        for (uint64_t x = 0; x < P; ++x) dst[x] &= src[x];
+        return;
+    }
+    uint64_t x = 0, a, b;
+    for (; x + 8 <= P; x += 8) {
+        memcpy(&a, dst + x, 8);
+        memcpy(&b, src + x, 8);
+        a &= b;
+        memcpy(dst + x, &a, 8);
+    }
+    if (x < P) {
+        memcpy(&a, dst + P - 8, 8);
+        memcpy(&b, src + P - 8, 8);
+        a &= b;
+        memcpy(dst + P - 8, &a, 8);
+    }
+}
+
+int xo_cobs_query_batched(const uint8_t* rows, const uint64_t* sig, uint64_t G, uint64_t P, uint64_t D,
+                          uint32_t h, int k, const uint8_t* seqs, const uint64_t* offsets, uint64_t n,
+                          uint32_t step, uint32_t* hits, uint64_t* nk, int nthreads) {
+    if (k < 1 || k > 255 || h < 1 || h > 64 || step < 1) return -1;
+    if (k >= 32) return xo_cobs_query(rows, sig, G, P, D, h, k, seqs, offsets, n, step, hits, nk, nthreads);
+    init_tables();
+    for (int x = 0; x < 16; ++x) {
+        uint64_t v = 0;
+        for (int i = 0; i < 4; ++i)
+            if (x >> i & 1) v |= 1ull << (16 * i);
+        nibble_lanes[x] = v;
+    }
+    uint64_t* base = (uint64_t*)malloc((G + 1) * sizeof(uint64_t));
+    uint64_t* magic = (uint64_t*)malloc(G * sizeof(uint64_t));
+    base[0] = 0;
+    for (uint64_t g = 0; g < G; ++g) {
+        base[g + 1] = base[g] + sig[g] * P;
+        magic[g] = sig[g] ? ~0ull / sig[g] : 0;
+    }
+#ifndef XO_LOOK
+#define XO_LOOK 12
+#endif
+    enum { kLook = XO_LOOK, kFlush = 65535 };
+    const uint64_t lanes = 2 * G * P;  /* 4 docs per uint64 of counters */
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        uint8_t canon[256];
+        uint8_t* mask = (uint8_t*)malloc(G * P);
+        uint64_t* cnt = (uint64_t*)calloc(lanes, sizeof(uint64_t));
+        uint64_t cap = 0;
+        const uint8_t** rp = NULL;  /* [k-mer][group][hash] row pointers of one read */
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 64)
+#endif
+        for (int64_t r = 0; r < (int64_t)n; ++r) {
+            const uint8_t* s = seqs + offsets[r];
+            const uint64_t len = offsets[r + 1] - offsets[r];
+            const uint64_t m = xo_num_kmers(len, k, step);
+            uint32_t* out = hits + (uint64_t)r * D;
+            memset(out, 0, D * sizeof(uint32_t));
+            nk[r] = m;
+            const uint64_t per = G * h;
+            if (m * per > cap) {
+                cap = m * per;
+                rp = (const uint8_t**)realloc(rp, cap * sizeof(*rp));
+            }
+            for (uint64_t i = 0; i < m; ++i) {
+                xo_canonical_cobs(s + i * step, k, canon);
+                xo_xxh64_terms t;
+                xxh64_terms(canon, (uint64_t)k, &t);
+                for (uint32_t j = 0; j < h; ++j) {
+                    const uint64_t hv = xxh64_seeded(&t, j);
+                    for (uint64_t g = 0; g < G; ++g)
+                        rp[i * per + g * h + j] = rows + base[g] + mod_barrett(hv, sig[g], magic[g]) * P;
+                }
+            }
+            for (uint64_t i = 0; i < m && i < kLook; ++i)
+                for (uint64_t q = 0; q < per; ++q) __builtin_prefetch(rp[i * per + q]);
+            uint64_t since = 0;
+            for (uint64_t i = 0; i < m; ++i) {
+                if (i + kLook < m)
+                    for (uint64_t q = 0; q < per; ++q) __builtin_prefetch(rp[(i + kLook) * per + q]);
+                const uint8_t* const* kr = rp + i * per;
+                for (uint64_t g = 0; g < G; ++g) {
+                    uint8_t* mg = mask + g * P;
+                    memcpy(mg, kr[g * h], P);
+                    for (uint32_t j = 1; j < h; ++j) and_row(mg, kr[g * h + j], P);
+                }
+                for (uint64_t x = 0; x < G * P; ++x) {
+                    const uint8_t v = mask[x];
+                    if (!v) continue;
+                    cnt[2 * x] += nibble_lanes[v & 15];
+                    cnt[2 * x + 1] += nibble_lanes[v >> 4];
+                }
+                if (++since == kFlush || i + 1 == m) {  /* 16-bit lanes: flush before they can wrap */
+                    for (uint64_t q = 0; q < lanes; ++q) {
+                        const uint64_t c = cnt[q];
+                        if (!c) continue;
+                        for (int l = 0; l < 4; ++l) {
+                            const uint64_t d = 4 * q + (uint64_t)l;  /* group-major doc order = doc index */
+                            if (d < D) out[d] += (uint32_t)(c >> (16 * l) & 0xFFFF);
+                        }
+                        cnt[q] = 0;
+                    }
+                    since = 0;
+                }
+            }
+        }
+        free(rp);
+        free(cnt);
+        free(mask);
+    }
+    free(magic);
+    free(base);
+    return 0;
+}
+
 /* Construction: every position (step 1) of every record of doc rec_doc[r]
  * sets bit (doc - group start) of its h rows in the doc's group. */
 int xo_cobs_build(uint8_t* rows, const uint64_t* sig, uint64_t G, uint64_t P, uint64_t D,

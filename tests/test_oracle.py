@@ -138,3 +138,40 @@ def test_bloom_params_restated(oracle_mod):
     nbytes, K = oracle_mod.BloomFilter.params(1000, 0.01)
     assert K == 7
     assert nbytes == (int(-1000 * math.log(0.01) / math.log(2) ** 2) + 7) // 8
+
+
+def test_xxh64_seed_terms_equal_the_pinned_hash(oracle_mod):
+    """The batched oracle's XXH64 (per-k-mer terms computed once, the seed
+    chain per hash) equals xo_xxh64 (pinned to python-xxhash) for every
+    length 0..40 and 70 seeds."""
+    rng = np.random.default_rng(5)
+    L = oracle_mod.lib()
+    for n in range(41):
+        data = bytes(rng.integers(0, 256, n, dtype=np.uint8))
+        for seed in list(range(64)) + [2**32 - 1, 2**32, 2**63, 2**64 - 1, 12345678901, 7]:
+            assert L.xo_xxh64_terms_check(data, n, seed) == L.xo_xxh64(data, n, seed), (n, seed)
+
+
+@pytest.mark.parametrize("D,k,h,page", [(100, 21, 7, None), (3, 21, 7, None), (9, 5, 2, None), (130, 17, 4, None),
+                                        (1100, 31, 1, 64), (90, 21, 3, 4), (20, 31, 1, 1), (37, 32, 2, None)])
+def test_batched_cobs_query_equals_the_oracle(oracle_mod, D, k, h, page):
+    """xo_cobs_query_batched (bench.py's CPU baseline: prefetched rows, seed
+    terms computed once, 4 docs per add) gives the scalar oracle's hits and
+    counts bit for bit: classic and compact banks, padding docs past D,
+    non-ACGT and short reads, steps 1/2/5, threads 1 and 4, and one read of
+    more k-mers than a 16-bit counter lane holds (the flush path)."""
+    bank, docs = _small_bank(oracle_mod, D, k, h, compact_page=page, seed=D + k)
+    rng = np.random.default_rng(D * 3 + k)
+    queries = [s[: int(rng.integers(k, len(s) + 1))] for s, _ in docs[:60]]
+    queries += ["".join(rng.choice(list("ACGTNacgtRY"), int(rng.integers(0, 300)))) for _ in range(40)]
+    queries += ["ACG", "", docs[0][0] * 3]
+    long_read = "".join(docs[i % len(docs)][0] for i in range(400))[:70_000 + k]
+    queries.append(long_read)  # 70 k sampled k-mers at step 1: past 65535
+    buf, offs = oracle_mod.pack(queries)
+    for step in (1, 2, 5):
+        want_h, want_n = bank.query_packed(buf, offs, step=step)
+        for threads in (1, 4):
+            got_h, got_n = bank.query_packed_batched(buf, offs, step=step, threads=threads)
+            assert np.array_equal(got_n, want_n)
+            assert np.array_equal(got_h, want_h), (step, threads, int((got_h != want_h).sum()))
+    assert int(want_h[-1].max()) > 0
