@@ -805,9 +805,9 @@ def cpu_baseline(wl, args):
     def run(m):
         pr = pack_fixed(wl.reads[:m])
         t = time.perf_counter()
-        # COBS banks: the batched restatement (a tuned port: rows prefetched across a read's k-mers,
-        # seed-independent XXH64 terms once per k-mer, Barrett remainders, 4 docs per add), the same
-        # hits as the scalar oracle bit for bit (tests/test_oracle.py); rbloom filters: the scalar one
+        # the batched restatements (a tuned port: COBS rows / rbloom bit bytes prefetched across a
+        # read's k-mers, Barrett remainders; COBS: seed-independent XXH64 terms once per k-mer, 4 docs
+        # per add), the same hits as the scalar oracle bit for bit (tests/test_oracle.py)
         outs = [getattr(ob, "query_packed_batched", ob.query_packed)(pr.buf, pr.offsets, step=args.step,
                                                                      threads=threads) for ob in obanks]
         return time.perf_counter() - t, outs
@@ -831,7 +831,9 @@ def cpu_baseline(wl, args):
         mism += int(np.count_nonzero(gpu != hits.reshape(gpu.shape)))
         probes += int(nk.sum()) * gpu.shape[1] * passes
     port = ("batched: prefetched rows, hoisted hash terms, 4 docs per add; equal to the scalar oracle"
-            if hasattr(obanks[0], "query_packed_batched") else "the scalar oracle")
+            if type(obanks[0]).__name__ == "CobsBank" else
+            "batched: a read's bit indices first (Barrett remainders), bytes prefetched ahead; "
+            "equal to the scalar oracle")
     return {
         "value": probes / dt, "unit": "probes/s", "cores": threads, "kind": "port", "host_cpus": cpus,
         "sample": f"{passes} pass(es) over {m2} of the benchmark reads x {len(obanks)} bank(s) "

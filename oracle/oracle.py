@@ -91,6 +91,8 @@ def lib():
             _u8p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int, _u8p, _u64p,
             ctypes.c_uint64, ctypes.c_uint32, _u32p, _u64p, ctypes.c_int,
         ]
+        L.xo_bloom_query_batched.restype = ctypes.c_int
+        L.xo_bloom_query_batched.argtypes = L.xo_bloom_query.argtypes
         L.xo_num_threads.restype = ctypes.c_int
         _LIB = L
     return _LIB
@@ -285,6 +287,19 @@ class BloomFilter:
                                   _p(nk, _u64p), int(threads))
         if rc != 0:
             raise ValueError(f"xo_bloom_query failed ({rc})")
+        return hits, nk
+
+    def query_packed_batched(self, buf, offs, step=1, threads=0):
+        """query_packed through xo_bloom_query_batched: the same answer,
+        computed as a tuned CPU port would (bench.py's cpu_baseline)."""
+        n = len(offs) - 1
+        hits = np.zeros(n, dtype=np.uint32)
+        nk = np.zeros(n, dtype=np.uint64)
+        rc = lib().xo_bloom_query_batched(_p(self.bits, _u8p), self.bits.size, self.K, self.k,
+                                          _p(buf, _u8p), _p(offs, _u64p), n, step, _p(hits, _u32p),
+                                          _p(nk, _u64p), int(threads))
+        if rc != 0:
+            raise ValueError(f"xo_bloom_query_batched failed ({rc})")
         return hits, nk
 
     def query(self, seqs, step=1, threads=0):

@@ -617,6 +617,68 @@ int xo_bloom_query(const uint8_t* bits, uint64_t nbytes, uint64_t nhash, int k, 
     return 0;
 }
 
+/* The same query batched for the CPU baseline (bit-identical, tests/test_oracle.py):
+ * every sampled k-mer's K bit indices first (Barrett remainders instead of
+ * divisions), their bytes prefetched kLook k-mers ahead, then the test with
+ * rbloom's stop at the first zero bit. */
+int xo_bloom_query_batched(const uint8_t* bits, uint64_t nbytes, uint64_t nhash, int k, const uint8_t* seqs,
+                           const uint64_t* offsets, uint64_t n, uint32_t step, uint32_t* hits, uint64_t* nk,
+                           int nthreads) {
+    if (k < 1 || k > 240 || nhash < 1 || nhash > 64 || step < 1 || nbytes == 0) return -1;
+    init_tables();
+    const uint64_t mbits = nbytes * 8, magic = ~0ull / mbits;
+    int failed = 0;
+    enum { kLook = 12 };
+#ifdef _OPENMP
+    if (nthreads > 0) omp_set_num_threads(nthreads);
+#pragma omp parallel
+#endif
+    {
+        uint8_t canon[256];
+        uint64_t cap = 0;
+        uint64_t* idx = NULL;  /* [k-mer][hash] bit indices of one read */
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 64)
+#endif
+        for (int64_t r = 0; r < (int64_t)n; ++r) {
+            const uint8_t* s = seqs + offsets[r];
+            const uint64_t cnt = xo_num_kmers(offsets[r + 1] - offsets[r], k, step);
+            if (cnt * nhash > cap) {
+                uint64_t* grown = (uint64_t*)realloc(idx, cnt * nhash * sizeof(*idx));
+                if (!grown) {
+                    failed = 1;
+                    continue;
+                }
+                idx = grown;
+                cap = cnt * nhash;
+            }
+            for (uint64_t i = 0; i < cnt; ++i) {
+                xo_canonical_bio(s + i * step, k, canon);
+                __uint128_t st = xo_xxh3_64(canon, (uint64_t)k, 0);
+                for (uint64_t j = 0; j < nhash; ++j) {
+                    st = st * LCG_M + LCG_C;
+                    idx[i * nhash + j] = mod_barrett((uint64_t)(st >> 64), mbits, magic);
+                }
+            }
+            for (uint64_t i = 0; i < cnt && i < kLook; ++i)
+                for (uint64_t j = 0; j < nhash; ++j) __builtin_prefetch(bits + (idx[i * nhash + j] >> 3));
+            uint32_t c = 0;
+            for (uint64_t i = 0; i < cnt; ++i) {
+                if (i + kLook < cnt)
+                    for (uint64_t j = 0; j < nhash; ++j) __builtin_prefetch(bits + (idx[(i + kLook) * nhash + j] >> 3));
+                const uint64_t* x = idx + i * nhash;
+                int in = 1;
+                for (uint64_t j = 0; j < nhash && in; ++j) in = (bits[x[j] >> 3] >> (x[j] & 7)) & 1;
+                c += (uint32_t)in;
+            }
+            hits[r] = c;
+            nk[r] = cnt;
+        }
+        free(idx);
+    }
+    return failed ? -2 : 0;
+}
+
 int xo_num_threads(void) {
 #ifdef _OPENMP
     return omp_get_max_threads();

@@ -175,3 +175,31 @@ def test_batched_cobs_query_equals_the_oracle(oracle_mod, D, k, h, page):
             assert np.array_equal(got_n, want_n)
             assert np.array_equal(got_h, want_h), (step, threads, int((got_h != want_h).sum()))
     assert int(want_h[-1].max()) > 0
+
+
+@pytest.mark.parametrize("nbytes,K,k", [(None, None, 21), (1, 3, 21), (977, 7, 21), (4096, 64, 15),
+                                        ((1 << 29) + 12345, 5, 31), (None, None, 240)])
+def test_batched_bloom_query_equals_the_oracle(oracle_mod, nbytes, K, k):
+    """xo_bloom_query_batched (bench.py's genus CPU baseline: a read's bit
+    indices first with Barrett remainders, bytes prefetched ahead) gives the
+    scalar oracle's hits and counts bit for bit: sized and overfilled filters,
+    one byte, 64 hashes, a filter past 2**32 bits, k 15..240, non-ACGT and short
+    reads, steps 1/2/5, threads 1 and 4."""
+    rng = np.random.default_rng(k + (nbytes or 0) % 1000)
+    seqs = ["".join(rng.choice(list("ACGTacgtN"), int(rng.integers(k, k + 400)))) for _ in range(30)]
+    if nbytes is None:
+        nbytes, K = oracle_mod.BloomFilter.params(sum(len(s) for s in seqs), 0.01)
+    bf = oracle_mod.BloomFilter(np.zeros(nbytes, dtype=np.uint8), K, k)
+    bf.build(seqs)
+    queries = seqs[:15] + ["".join(rng.choice(list("ACGTNacgtRY"), int(rng.integers(0, 600)))) for _ in range(40)]
+    queries += ["ACG", "", seqs[0] * 3]
+    buf, offs = oracle_mod.pack(queries)
+    for step in (1, 2, 5):
+        want_h, want_n = bf.query_packed(buf, offs, step=step)
+        assert int(want_h[:15].min()) > 0 or step > 1
+        for threads in (1, 4):
+            got_h, got_n = bf.query_packed_batched(buf, offs, step=step, threads=threads)
+            assert np.array_equal(got_n, want_n)
+            assert np.array_equal(got_h, want_h), (step, threads, int((got_h != want_h).sum()))
+    with pytest.raises(ValueError):
+        oracle_mod.BloomFilter(np.zeros(0, dtype=np.uint8), 3, k).query_packed_batched(buf, offs)
