@@ -1,7 +1,6 @@
 """Host-side logic of the drop-in surface (CPU only, no device calls)."""
 from __future__ import annotations
 
-import math
 from pathlib import Path
 
 import numpy as np
