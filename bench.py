@@ -279,7 +279,7 @@ class Workload:
         else:  # mlst
             reads, loci_info = self._mlst(args, dev, s)
             self.config.update(loci=len(self.banks), **loci_info)
-            self.kernel = "probe_cobs_wide<31,1,C=4,P=2,G=3> (compact, 3 groups x 4 chunk lanes)"
+            self.kernel = "probe_cobs_vslice<31,3> (compact, 3 groups of 64-B pages; one lane per 32 docs, bit-sliced counters)"
         if args.probe_path != "auto":  # diagnostic runs of one path (the default line never sets it)
             mode = {"direct": 0, "partitioned": 2}[args.probe_path]
             for b in self.banks:

@@ -284,6 +284,35 @@ def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
     gb.close()
 
 
+@pytest.mark.parametrize("D,k,G", [(1430, 31, 3), (1025, 31, 3), (1536, 31, 3), (2048, 31, 4), (1537, 21, 4),
+                                   (1300, 15, 3), (1800, 32, 4)])
+def test_vslice_probe_matches_oracle(xs, oracle_mod, D, k, G):
+    """Compact banks of 3-4 groups of 64-byte pages with one hash (MLST loci)
+    take the bit-sliced probe (xs_probe_vslice.hip): hits, k-mer counts and
+    totals equal the oracle's for random and document reads, reads of exactly
+    256 k-mers from one document (a count of 256: the weight-256 plane), reads
+    of two full units, non-ACGT, empty and short reads, at steps 1 and 3."""
+    rng = np.random.default_rng(D + 7 * k)
+    sig = [int(x) for x in rng.integers(3000, 40000, G)]
+    ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, 1, sig, page=64, seed=D + k, per_doc=1)
+    long_docs = [s for s in seqs if len(s) >= 600]
+    assert len(long_docs) >= 20
+    reads = _reads(rng, 200, k) + [s[: int(rng.integers(k, len(s) + 1))] for s in seqs[:60]]
+    reads += [s[: 255 + k] for s in long_docs[:10]]   # 256 k-mers at step 1: one whole unit
+    reads += [s[: 511 + k] for s in long_docs[10:20]]  # two full units
+    reads += _reads(rng, 20, k, alphabet="ACGTNacgtnRY") + [b"", b"A" * (k - 1), seqs[0] * 3]
+    for step in (1, 3):
+        want_h, want_n = ob.query(reads, step=step)
+        got_h, got_n = gb.query(reads, step=step)
+        assert np.array_equal(got_n, want_n)
+        assert np.array_equal(got_h, want_h), _explain(got_h, want_h, reads)
+        tot, nk = gb.query_totals(reads, step=step)
+        assert np.array_equal(tot, want_h.sum(axis=0, dtype=np.uint64)) and nk == int(want_n.sum())
+        if step == 1:
+            assert int(want_h.max()) >= 256
+    gb.close()
+
+
 def _random_direct_configs(n=32, seed=20261018):
     """Seeded random banks for the direct COBS probe families (fast, wide,
     slots, general): classic with 1..2200 docs, or compact with page sizes

@@ -23,7 +23,7 @@ CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 SO_PATH = PKG / "libxspect_hip.so"
 SOURCE_NAMES = ["xs_api.cpp", "xs_pool.cpp", "xs_fastx.cpp", "xs_fastx_dev.hip", "xs_json.cpp", "xs_kernels.hip",
-                "xs_probe_fast.hip", "xs_probe_wide.hip", "xs_probe_slots.hip", "xs_probe_general.hip",
+                "xs_probe_fast.hip", "xs_probe_vslice.hip", "xs_probe_wide.hip", "xs_probe_slots.hip", "xs_probe_general.hip",
                 "xs_probe_bloompart.hip", "xs_probe_cobspart.hip"]
 HEADER_NAMES = ["xs_internal.h", "xs_device.h", "xs_part.h"]
 SOURCES = [CSRC / s for s in SOURCE_NAMES]

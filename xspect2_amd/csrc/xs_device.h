@@ -536,6 +536,11 @@ int wide_for(const CobsView& bv);
 int grid_cobs_wide(const CobsView& bv, uint32_t k);
 hipError_t launch_cobs_wide(const ReadView& rv, const CobsView& bv, uint32_t* hits, uint64_t* partials,
                             int blocks, hipStream_t s);
+// xs_probe_vslice.hip: compact, one hash, 3-4 groups of 64-byte pages (MLST loci)
+bool vslice_take(const CobsView& bv);
+int grid_cobs_vslice(const CobsView& bv, uint32_t k);
+hipError_t launch_cobs_vslice(const ReadView& rv, const CobsView& bv, uint32_t* hits, uint64_t* partials,
+                              int blocks, hipStream_t s);
 // xs_probe_slots.hip: compile-time group x chunk layouts (false = not taken)
 bool slots_take(const CobsView& bv);
 int grid_cobs_slots(const CobsView& bv, uint32_t k);

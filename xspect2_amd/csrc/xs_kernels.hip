@@ -438,9 +438,10 @@ int probe_blocks(uint64_t D, int* waves_per_block, size_t* lds_bytes) {
 
 // Grid of the probe kernel launch_probe_cobs picks for this bank (partials
 // are sized by it).  Cached per variant; every device of a run is an MI355X.
-// Order: fast (D <= 128), wide (classic, 2..16 chunks), slots, general.
+// Order: fast (D <= 128), bit-sliced (MLST loci), wide (2..16 chunks), slots, general.
 int probe_grid_cobs(const CobsView& bv, uint32_t k) {
     if (cobs_fast(bv, k)) return grid_cobs_fast(k);
+    if (vslice_take(bv)) return grid_cobs_vslice(bv, k);
     if (wide_for(bv)) return grid_cobs_wide(bv, k);
     if (slots_take(bv)) return grid_cobs_slots(bv, k);
     return grid_cobs_general(bv);
@@ -449,6 +450,7 @@ int probe_grid_cobs(const CobsView& bv, uint32_t k) {
 hipError_t launch_probe_cobs(const ReadView& rv, const CobsView& bv, uint32_t* hits,
                              uint64_t* partials, int blocks, hipStream_t s) {
     if (cobs_fast(bv, rv.k)) return launch_cobs_fast(rv, bv, hits, partials, blocks, s);
+    if (vslice_take(bv)) return launch_cobs_vslice(rv, bv, hits, partials, blocks, s);
     if (wide_for(bv)) return launch_cobs_wide(rv, bv, hits, partials, blocks, s);
     if (slots_take(bv)) return launch_cobs_slots(rv, bv, hits, partials, blocks, s);
     return launch_cobs_general(rv, bv, hits, partials, blocks, s);
