@@ -285,13 +285,16 @@ def test_compact_probe_matches_oracle(xs, oracle_mod, D, k, h, page, G):
 
 
 @pytest.mark.parametrize("D,k,G", [(1430, 31, 3), (1025, 31, 3), (1536, 31, 3), (2048, 31, 4), (1537, 21, 4),
-                                   (1300, 15, 3), (1800, 32, 4)])
+                                   (1300, 15, 3), (1800, 32, 4), (400, 31, 1), (512, 31, 1), (70, 31, 1),
+                                   (300, 21, 1), (900, 31, 2), (513, 31, 2), (1024, 17, 2)])
 def test_vslice_probe_matches_oracle(xs, oracle_mod, D, k, G):
-    """Compact banks of 3-4 groups of 64-byte pages with one hash (MLST loci)
-    take the bit-sliced probe (xs_probe_vslice.hip): hits, k-mer counts and
-    totals equal the oracle's for random and document reads, reads of exactly
-    256 k-mers from one document (a count of 256: the weight-256 plane), reads
-    of two full units, non-ACGT, empty and short reads, at steps 1 and 3."""
+    """Compact banks of 1-4 groups of 64-byte pages with one hash (MLST loci)
+    take the bit-sliced probe (xs_probe_vslice.hip; 4 or 2 k-mer slots per
+    wave at 1 or 2 groups): hits, k-mer counts and totals equal the oracle's
+    for random and document reads, reads of exactly 256 k-mers from one
+    document (a count of 256: the weight-256 plane at 3-4 groups, the slots'
+    sum at 1-2), reads of two full units, non-ACGT, empty and short reads, at
+    steps 1 and 3."""
     rng = np.random.default_rng(D + 7 * k)
     sig = [int(x) for x in rng.integers(3000, 40000, G)]
     ob, gb, seqs, _ = _pair(xs, oracle_mod, D, k, 1, sig, page=64, seed=D + k, per_doc=1)

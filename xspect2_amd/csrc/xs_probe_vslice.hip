@@ -1,5 +1,5 @@
-// xs_probe_vslice.hip — COBS probe of compact banks with one hash and 64-byte pages
-// (MLST loci: 3 or 4 groups of 512 alleles), counting with bit-sliced adders.
+// xs_probe_vslice.hip — COBS probe of banks of 1-4 groups of 64-byte pages with one hash
+// (MLST loci of up to 2048 alleles), counting with bit-sliced adders.
 #include "xs_device.h"
 
 namespace xs {
@@ -7,9 +7,11 @@ namespace xs {
 // ------------------------------------------------------------------ COBS probe (bit-sliced)
 // One wavefront per unit (<= kSegKmers k-mers of one read), as the other
 // probes.  Hashing is one lane per k-mer.  Counting is one lane per 32 docs:
-// lane l owns word l % 16 of group l / 16's 64-byte row, so a k-mer's G rows are
-// one dword load across G * 16 lanes (each row one line), and the lane adds that
-// word into a bit-sliced counter of its 32 docs.  Carry-save adders
+// a k-mer's G rows are one dword load across G * 16 lanes (each row one line),
+// and each lane adds its word into a bit-sliced counter of its 32 docs.  With
+// G = 1 or 2 the wave holds S = 4 or 2 such lane sets, each taking every S-th
+// k-mer (slot, group, word = lane / 16G, lane / 16 % G, lane % 16); their
+// counts are summed at the end.  Carry-save adders
 // (Harley-Seal: 15 per 16 k-mers, 2 VALU each) put the whole k-mer's G * 512
 // docs at ~2 VALU, where probe_cobs_wide's column-popcount transpose takes ~27
 // VALU per 32-doc word and ran at the VALU issue limit on MLST loci
@@ -18,7 +20,7 @@ namespace xs {
 // lane turn the planes into byte counts; they go through LDS in doc order, so
 // the hit row is stored 64 consecutive docs per instruction.
 constexpr int kVsBatch = 16;       // k-mers per carry-save round (row loads in flight per lane)
-constexpr int kVsMinBlocks = 8;    // 8 waves per SIMD: the register budget is 64 VGPRs
+constexpr int kVsMinBlocks = 6;    // waves per SIMD the register budget is sized for (LDS allows 6-7)
 
 // carry-save add of three bit vectors: hi = majority, lo = parity (one
 // three-input v_bitop3_b32 each on gfx950)
@@ -95,8 +97,12 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
                                                                                  uint64_t* __restrict__ partials) {
     constexpr int kDocs = GM * 512;  // docs of the bank's groups (D <= kDocs)
     constexpr int kWaves = kProbeThreads / kWave;
-    // per wave: the tile's row indices [group][k-mer] while counting, then the
-    // unit's byte counts in doc order (the same bytes: one wave uses one at a time)
+    constexpr int LW = GM * 16;                         // lanes per k-mer
+    constexpr int S = GM == 1 ? 4 : GM == 2 ? 2 : 1;    // k-mer slots per wave
+    constexpr int SK = kWave / S;                       // k-mers per slot per tile
+    static_assert(GM >= 1 && GM <= 4 && S * kDocs <= kWave * 32, "counts of every slot fit the LDS buffer");
+    // per wave: the tile's row offsets [group][slot][k-mer] while counting, then
+    // the unit's byte counts [slot][doc] (the same bytes: one wave uses one at a time)
     __shared__ __attribute__((aligned(16))) uint32_t s_buf[kWaves][kWave * 8];
     __shared__ uint32_t s_p256[kWaves][kWave];  // weight-256 plane (a doc hit by all 256 k-mers of a unit)
     __shared__ uint64_t s_tot[kDocs];
@@ -112,8 +118,10 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
     GroupDesc gd[GM];
 #pragma unroll
     for (int g = 0; g < GM; ++g) gd[g] = bv.groups[g];
-    // counting lane: group my_g (lanes past the groups repeat the last one; their sums are never read)
-    const int my_g = min(lane >> 4, GM - 1);
+    // counting lane: slot my_slot, group my_g (at G = 3, lanes 48-63 repeat slot 0 group 0; their
+    // counts land past the docs and are never read)
+    const int my_slot = min(lane / LW, S - 1);
+    const int my_g = min((lane % LW) >> 4, GM - 1);
     uint32_t my_base = (uint32_t)gd[0].base;
 #pragma unroll
     for (int g = 1; g < GM; ++g)
@@ -155,10 +163,11 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
                 }
                 __builtin_amdgcn_wave_barrier();  // the previous unit's count reads are done
 #pragma unroll
-                for (int g = 0; g < GM; ++g) s_buf[wid][g * 64 + lane] = ri[g] * 64u;
+                for (int g = 0; g < GM; ++g) s_buf[wid][g * 64 + (lane % S) * SK + lane / S] = ri[g] * 64u;
                 __builtin_amdgcn_wave_barrier();
-                for (uint32_t u0 = 0; u0 < tile; u0 += kVsBatch) {
-                    const uint4* src = reinterpret_cast<const uint4*>(&s_buf[wid][my_g * 64 + u0]);
+                const uint32_t per_slot = (tile + S - 1) / S;
+                for (uint32_t u0 = 0; u0 < per_slot; u0 += kVsBatch) {
+                    const uint4* src = reinterpret_cast<const uint4*>(&s_buf[wid][my_g * 64 + my_slot * SK + u0]);
                     uint32_t x[kVsBatch];
 #pragma unroll
                     for (int q = 0; q < kVsBatch / 4; ++q) {
@@ -168,17 +177,17 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
                         x[4 * q + 2] = *reinterpret_cast<const uint32_t*>(rows + (my_base + o.z));
                         x[4 * q + 3] = *reinterpret_cast<const uint32_t*>(rows + (my_base + o.w));
                     }
-                    if (u0 + kVsBatch > tile) {  // uniform: the k-mers past the tile add nothing
+                    if ((u0 + kVsBatch) * S > tile) {  // uniform: the k-mers past the tile add nothing
 #pragma unroll
                         for (int q = 0; q < kVsBatch; ++q)
-                            if (u0 + q >= tile) x[q] = 0;
+                            if ((u0 + q) * S + my_slot >= tile) x[q] = 0;
                     }
                     uint32_t carry = hs16(ones, twos, fours, eights, x), t;
                     t = p16 & carry; p16 ^= carry; carry = t;
                     t = p32 & carry; p32 ^= carry; carry = t;
                     t = p64 & carry; p64 ^= carry; carry = t;
                     t = p128 & carry; p128 ^= carry; carry = t;
-                    p256 |= carry;  // <= 256 k-mers per unit: set only for a count of exactly 256
+                    p256 |= carry;  // <= 256 k-mers per slot: set only for a count of exactly 256 (S = 1)
                 }
             }
             const uint32_t pl[8] = {ones, twos, fours, eights, p16, p32, p64, p128};
@@ -195,6 +204,8 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
             uint32_t* hrow = hits ? hits + (uint64_t)r * D : nullptr;
             for (uint32_t d = (uint32_t)lane; d < D; d += 64) {
                 uint32_t v = s_cnt[d];
+#pragma unroll
+                for (int sl = 1; sl < S; ++sl) v += s_cnt[sl * kDocs + d];
                 if (any256) v += ((s_p256[wid][d >> 5] >> (d & 31)) & 1u) << 8;
                 if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&s_tot[d]), (unsigned long long)v);
                 if (hrow) {
@@ -218,23 +229,26 @@ __global__ void __launch_bounds__(kProbeThreads, kVsMinBlocks) probe_cobs_vslice
 }
 
 // ------------------------------------------------------------------ launch
-// Compact banks of 3 or 4 groups of 64-byte pages (512 docs each) with one
-// hash, whose image fits 32-bit offsets: XspecT's MLST loci.
+// Banks of 1-4 groups of 64-byte pages (512 docs each) with one hash, whose
+// image fits 32-bit offsets: XspecT's MLST loci of up to 2048 alleles.
 bool vslice_take(const CobsView& bv) {
-    return (bv.G == 3 || bv.G == 4) && bv.h == 1 && bv.page == 64 && bv.pitch == 64 && bv.D <= bv.G * 512ull &&
+    return bv.G >= 1 && bv.G <= 4 && bv.h == 1 && bv.page == 64 && bv.pitch == 64 && bv.D <= bv.G * 512ull &&
            bv.sig_max < (1ull << 30) && (uint64_t)bv.G * bv.sig_max * 64 < (1ull << 32);
 }
 
 using VsFn = void (*)(ReadView, CobsView, uint32_t*, uint64_t*);
 
-static VsFn pick_vslice(uint32_t k, uint32_t G) {
-    if (k == 31) return G == 3 ? probe_cobs_vslice<31, 3> : probe_cobs_vslice<31, 4>;
-    return G == 3 ? probe_cobs_vslice<0, 3> : probe_cobs_vslice<0, 4>;
+template <int KT>
+static VsFn pick_vslice_g(uint32_t G) {
+    return G == 1 ? probe_cobs_vslice<KT, 1> : G == 2 ? probe_cobs_vslice<KT, 2>
+         : G == 3 ? probe_cobs_vslice<KT, 3> : probe_cobs_vslice<KT, 4>;
 }
 
+static VsFn pick_vslice(uint32_t k, uint32_t G) { return k == 31 ? pick_vslice_g<31>(G) : pick_vslice_g<0>(G); }
+
 int grid_cobs_vslice(const CobsView& bv, uint32_t k) {
-    static std::atomic<int> grid[2][2];  // k == 31 x G
-    return cached_grid(grid[k == 31 ? 0 : 1][bv.G == 3 ? 0 : 1],
+    static std::atomic<int> grid[2][4];  // k == 31 x G
+    return cached_grid(grid[k == 31 ? 0 : 1][bv.G - 1],
                        [&] { return resident_grid(pick_vslice(k, bv.G), kProbeThreads, 0); });
 }
 
