@@ -646,6 +646,9 @@ int xo_bloom_query_batched(const uint8_t* bits, uint64_t nbytes, uint64_t nhash,
             if (cnt * nhash > cap) {
                 uint64_t* grown = (uint64_t*)realloc(idx, cnt * nhash * sizeof(*idx));
                 if (!grown) {
+#ifdef _OPENMP
+#pragma omp atomic write
+#endif
                     failed = 1;
                     continue;
                 }
