@@ -1158,7 +1158,12 @@ def _random_mlst_configs(n=16, seed=20261021):
     return out
 
 
-@pytest.mark.parametrize("D,page,G,k,h,step,threshold,seed", _random_mlst_configs())
+# and MLST loci as XspecT trains them (k = 31, one hash, 64-byte pages: the bit-sliced probe)
+_VSLICE_MLST = [(400, 64, 1, 31, 1, 1, 50, 11), (900, 64, 2, 31, 1, 2, 20, 12), (1430, 64, 3, 31, 1, 1, 50, 13),
+                (2048, 64, 4, 31, 1, 1, 0, 14), (700, 64, 2, 21, 1, 3, 1, 15)]
+
+
+@pytest.mark.parametrize("D,page,G,k,h,step,threshold,seed", _random_mlst_configs() + _VSLICE_MLST)
 def test_mlst_query_random_configs(xs, oracle_mod, D, page, G, k, h, step, threshold, seed):
     """Seeded random compact banks through xs_mlst_query (one MLST locus per
     call, probabilistic_filter_mlst_model.py:192-303): 1-4 groups of pages
